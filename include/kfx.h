@@ -1,0 +1,172 @@
+/*
+ * kfx.h — C-ABI drop-in boundary of the MI355X-native KinectFusion hot path.
+ *
+ * The reference exposes the hot path only as the C++ class `kf::kinectfusion`
+ * (kfusion/include/kinectfusion.h:31-73) whose methods take OpenCV types.  There
+ * is no FFI in the reference; this header is the plain-C seam a binding (ctypes,
+ * cgo, JNI, or the header-only C++ adapter in
+ * slam-kinectfusion_amd/adapter/kinectfusion.h) calls.  Every entry point below
+ * names the reference interface it replaces.
+ *
+ * Conventions
+ *   - All host buffers belong to the caller and are copied; the context owns all
+ *     device memory.  No torch / HIP types cross this boundary.
+ *   - Images are row-major, tightly packed (no pitch): depth f32 or u16 in
+ *     millimetres (depth_sensor.cpp:191 converts PNG u16 mm -> f32 mm), colour
+ *     BGR8 interleaved (cv::Mat CV_8UC3), vertex/normal maps float3 AoS.
+ *   - Poses are kfx_pose {R row-major 3x3, t}; a cv::Affine3f maps 1:1.
+ *   - Every function returns an int status (KFX_OK = 0).  The reference prints
+ *     CUDA errors and continues (safe_call.hpp:8-14); here they are returned.
+ */
+#ifndef KFX_H
+#define KFX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KFX_ABI_VERSION 1
+#define KFX_MAX_LEVELS 4
+
+/* status codes */
+#define KFX_OK 0
+#define KFX_TRACKING_LOST 1 /* kinectfusion.cpp:97-101: "tracking fail!" -> reset() */
+#define KFX_ERR_ARG (-1)
+#define KFX_ERR_HIP (-2)
+#define KFX_ERR_OOM (-3)
+#define KFX_ERR_STATE (-4)
+#define KFX_ERR_NO_DEVICE (-5)
+
+/* kf::Intrinsics (types.hpp:13-29).  `c` (types.hpp:17) is unused on the path. */
+typedef struct kfx_intrinsics {
+  int width, height;
+  float fx, fy, cx, cy;
+} kfx_intrinsics;
+
+/* cv::Affine3f as used on the path: rotation row-major R[3*i+j] = R(i,j). */
+typedef struct kfx_pose {
+  float R[9];
+  float t[3];
+} kfx_pose;
+
+/* kf::kinectfuison_params (kinectfusion.h:9-30); defaults kinectfusion.cpp:167-190. */
+typedef struct kfx_params {
+  int pyramid_height;            /* 3 */
+  float dfilter_dist;            /* 5 m depth truncation (image_process.cu:15) */
+  int bfilter_kernel_size;       /* 5 */
+  float bfilter_spatial_sigma;   /* 10 (pixels) */
+  float bfilter_color_sigma;     /* 10 (mm) */
+  float icp_dist_threshold;      /* 0.015 m */
+  float icp_angle_threshold;     /* 30 degrees; stored as sinf(deg2rad) (icp_registration.cpp:5) */
+  int icp_iter_count[KFX_MAX_LEVELS]; /* indexed by level: {4,5,10} */
+  float volu_range[3];           /* metres, 3 */
+  int volu_dims[3];              /* 512 */
+  float volu_trun_dist;          /* 2.1 * range / dims */
+  kfx_pose volu_pose;            /* translate(-L/2, -L/2, 0.5) */
+  int tsdf_max_weight;           /* 64; the kernel uses MAX_WEIGHT (device_utils.cuh:5) */
+  float min_pose_move;           /* unused by the reference path */
+} kfx_params;
+
+typedef struct kfx_ctx kfx_ctx;
+
+/* ---- library ------------------------------------------------------------ */
+int kfx_abi_version(void);
+const char *kfx_last_error(void);
+/* kinectfuison_params::default_params (kinectfusion.cpp:167-190). */
+int kfx_default_params(kfx_params *out);
+
+/* ---- kf::kinectfusion ---------------------------------------------------- */
+/* kinectfusion::kinectfusion(intr, params) (kinectfusion.cpp:9-27).  device =
+ * HIP ordinal.  Allocates frames, the TSDF volume and ICP workspaces, then
+ * reset()s. */
+int kfx_create(const kfx_intrinsics *intr, const kfx_params *params, int device,
+               kfx_ctx **out);
+/* kinectfusion::release() + ~kinectfusion() (kinectfusion.cpp:28-31,191-195). */
+int kfx_destroy(kfx_ctx *ctx);
+/* kinectfusion::reset() (kinectfusion.cpp:133-141): frame_count=1, frames and
+ * volume zeroed (the reference's partial reset, SURVEY A5, is made total),
+ * pose_record = [I]. */
+int kfx_reset(kfx_ctx *ctx);
+
+/* kinectfusion::pipeline(cmap, dmap) (kinectfusion.cpp:78-127).  Host images;
+ * blocks until the frame is done.  Returns KFX_OK, or KFX_TRACKING_LOST when ICP
+ * failed and the reference's reset() semantics were applied (frame dropped). */
+int kfx_pipeline(kfx_ctx *ctx, const uint8_t *bgr, const float *depth_mm);
+int kfx_pipeline_u16(kfx_ctx *ctx, const uint8_t *bgr, const uint16_t *depth_mm);
+
+/* Device-resident input: frames uploaded once with kfx_stage_frames are
+ * processed without PCIe traffic and without a host sync (tracking state lives
+ * on the device).  kfx_synchronize waits for queued frames. */
+int kfx_stage_frames(kfx_ctx *ctx, int n_frames, const uint8_t *bgr,
+                     const float *depth_mm);
+int kfx_pipeline_staged(kfx_ctx *ctx, int frame_index);
+int kfx_synchronize(kfx_ctx *ctx);
+/* Use a captured hipGraph for the per-frame launch sequence (default on). */
+int kfx_set_graph_mode(kfx_ctx *ctx, int enabled);
+
+/* kinectfusion::getCurCameraPose() (kinectfusion.cpp:128-132). */
+int kfx_get_cur_camera_pose(kfx_ctx *ctx, kfx_pose *out);
+/* kinectfusion::frame_count (kinectfusion.h:58). */
+int kfx_get_frame_count(kfx_ctx *ctx, int *out);
+/* kinectfusion::pose_record (kinectfusion.h:59).  Writes min(cap, n) poses. */
+int kfx_get_pose_record(kfx_ctx *ctx, kfx_pose *out, int cap, int *n);
+/* main.cpp:95-98: pose_record as `Matx44f operator<<` text ("%.8g"). */
+int kfx_write_poses_txt(kfx_ctx *ctx, const char *path);
+
+/* ---- frame / volume access (Frame, TSDFVolume::Data) --------------------- */
+#define KFX_FRAME_CUR 0  /* cframe: measured maps of the current frame */
+#define KFX_FRAME_PREV 1 /* pframe: raycast (model) maps used as ICP target */
+/* Download one pyramid level of a frame.  Any pointer may be NULL.  dmap is
+ * metres (after bilateral + truncation), vmap/nmap float3 AoS. */
+int kfx_get_frame_maps(kfx_ctx *ctx, int which, int level, float *dmap,
+                       float *vmap, float *nmap);
+/* Upload maps (test seam for ICP / resize). */
+int kfx_set_frame_maps(kfx_ctx *ctx, int which, int level, const float *vmap,
+                       const float *nmap);
+/* TSDFVolume::Data() (tsdf_volume.cpp:4): export the volume as the
+ * reference's 8-byte x-fastest records {int16 tsdf, int16 weight, u8 c0,c1,c2,
+ * u8 pad=0} (device_types.hpp:51-56).  dst holds X*Y*Z*8 bytes. */
+int kfx_download_tsdf(kfx_ctx *ctx, void *dst_records);
+int kfx_upload_tsdf(kfx_ctx *ctx, const void *src_records);
+/* SoA export: tsdf int16[N], weight int16[N], colour u8x4[N] (any may be NULL). */
+int kfx_download_volume_soa(kfx_ctx *ctx, int16_t *tsdf, int16_t *weight,
+                            uint8_t *rgba);
+
+/* ---- stage entry points (kf::device seam, device_types.hpp:113-128) ------ */
+/* imageProcess (kinectfusion.cpp:48-76): upload, pyrDown, bilateral,
+ * depthTruncation, getVertexmap, getNormalmap into the CUR frame. */
+int kfx_stage_preprocess(kfx_ctx *ctx, const uint8_t *bgr, const float *depth_mm);
+/* rigidICP (rigid_icp.cu:135-169) one iteration at `level`: CUR vs PREV maps
+ * under `pose`; returns the 27 sums (i<=j upper triangle with b, in the
+ * reference's shift order) as int64 fixed point (value * 2^32). */
+int kfx_stage_icp_accumulate(kfx_ctx *ctx, int level, const kfx_pose *pose,
+                             int64_t sums[27]);
+/* ICPRegistration::rigidTransform (icp_registration.cpp:16-46) on CUR vs PREV
+ * maps: the whole coarse-to-fine loop.  Returns KFX_OK or KFX_TRACKING_LOST. */
+int kfx_stage_icp(kfx_ctx *ctx, kfx_pose *cam_pose_out);
+/* device::integrate (tsdf_volume.cu:103-111) of the CUR frame level-0 depth and
+ * colour with vol2cam; optional counts of updated / colour-updated voxels. */
+int kfx_stage_integrate(kfx_ctx *ctx, const kfx_pose *vol2cam,
+                        int64_t *n_updated, int64_t *n_colored);
+/* device::raycast (tsdf_volume.cu:264-273) into PREV level 0, with cam2vol and
+ * Rinv (row-major 3x3), then resizePointsNormals for levels >= 1. */
+int kfx_stage_raycast(kfx_ctx *ctx, const kfx_pose *cam2vol, const float Rinv[9]);
+
+/* ---- timing -------------------------------------------------------------- */
+/* Per-stage device milliseconds of the last kfx_pipeline* call run in
+ * profiled mode (graph off): {preprocess, icp, integrate, raycast, total}. */
+int kfx_set_profiling(kfx_ctx *ctx, int enabled);
+int kfx_get_stage_ms(kfx_ctx *ctx, float out_ms[5]);
+/* Voxel counts of the last processed frame's integrate (the algorithmic-byte
+ * inputs of the roofline): voxels whose tsdf/weight were
+ * updated and those whose colour was also blended.  Count-only kernel, the
+ * volume is not touched. */
+int kfx_integrate_counts(kfx_ctx *ctx, int64_t *n_updated, int64_t *n_colored);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KFX_H */

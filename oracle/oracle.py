@@ -1,0 +1,282 @@
+"""TEST INFRASTRUCTURE ONLY — ctypes binding of the CPU oracle (kfx_oracle.h).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import
+this module, and only as the checker.  The product (libkfx.so) never links or
+calls it.  Parity status: unpinned against the CUDA original (see
+kfx_oracle.h); pinned by analytic KATs in tests/test_oracle_kat.py.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_ROOT = os.path.dirname(_HERE)
+sys.path.insert(0, os.path.join(_ROOT, "slam-kinectfusion_amd"))
+from kfx.abi import (Intrinsics, Params, Pose, fptr, i16ptr, i32ptr, i64ptr, u8ptr)  # noqa: E402
+
+LIB_PATH = os.path.join(_HERE, "build", "libkfx_oracle.so")
+_lib = None
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = C.CDLL(LIB_PATH)
+        P = C.POINTER
+        f, i, v = C.c_float, C.c_int, None
+        L.kfo_expf.argtypes = [f]
+        L.kfo_expf.restype = f
+        L.kfo_pyr_down.argtypes = [P(f), i, i, P(f)]
+        L.kfo_bilateral.argtypes = [P(f), i, i, i, f, f, P(f)]
+        L.kfo_depth_truncation.argtypes = [P(f), i, f]
+        L.kfo_vertex_map.argtypes = [P(f), i, i, f, f, f, f, P(f)]
+        L.kfo_normal_map.argtypes = [P(f), i, i, P(f)]
+        L.kfo_resize_points_normals.argtypes = [P(f), P(f), i, i, P(f), P(f)]
+        L.kfo_preprocess.argtypes = [P(f), i, i, i, P(Intrinsics), P(Params), P(P(f)), P(P(f)), P(P(f))]
+        L.kfo_icp_accumulate.argtypes = [P(f), P(f), P(f), P(f), i, i, P(Intrinsics), P(Pose), f, f,
+                                         P(C.c_int64)]
+        L.kfo_icp_update.argtypes = [P(C.c_int64), P(Pose), P(C.c_double)]
+        L.kfo_icp_update.restype = i
+        L.kfo_pose_mul.argtypes = [P(Pose), P(Pose), P(Pose)]
+        L.kfo_pose_inv.argtypes = [P(Pose), P(Pose)]
+        L.kfo_integrate.argtypes = [P(C.c_int16), P(C.c_int16), P(C.c_uint8), P(i), P(f), f,
+                                    P(Intrinsics), P(Pose), P(f), P(C.c_uint8), P(C.c_int32), C.c_int64,
+                                    P(C.c_int64), P(C.c_int64)]
+        L.kfo_raycast.argtypes = [P(C.c_int16), P(i), P(f), P(f), P(Intrinsics), P(Pose), P(f), P(f), P(f),
+                                  P(C.c_int32), C.c_int64]
+        L.kfo_pipe_create.argtypes = [P(Intrinsics), P(Params)]
+        L.kfo_pipe_create.restype = C.c_void_p
+        L.kfo_pipe_destroy.argtypes = [C.c_void_p]
+        L.kfo_pipe_reset.argtypes = [C.c_void_p]
+        L.kfo_pipe_process.argtypes = [C.c_void_p, P(C.c_uint8), P(f)]
+        L.kfo_pipe_process.restype = i
+        L.kfo_pipe_frame_count.argtypes = [C.c_void_p]
+        L.kfo_pipe_pose_count.argtypes = [C.c_void_p]
+        L.kfo_pipe_get_pose.argtypes = [C.c_void_p, i, P(Pose)]
+        L.kfo_pipe_tsdf.argtypes = [C.c_void_p]
+        L.kfo_pipe_tsdf.restype = P(C.c_int16)
+        L.kfo_pipe_weight.argtypes = [C.c_void_p]
+        L.kfo_pipe_weight.restype = P(C.c_int16)
+        L.kfo_pipe_rgb.argtypes = [C.c_void_p]
+        L.kfo_pipe_rgb.restype = P(C.c_uint8)
+        L.kfo_pipe_map.argtypes = [C.c_void_p, i, i, i]
+        L.kfo_pipe_map.restype = P(f)
+        L.kfo_pipe_last_counts.argtypes = [C.c_void_p, P(C.c_int64), P(C.c_int64)]
+        L.kfo_format_pose.argtypes = [P(Pose), C.c_char_p, i]
+        _lib = L
+    return _lib
+
+
+def _f32(a):
+    return np.ascontiguousarray(a, dtype=np.float32)
+
+
+def expf(x: float) -> float:
+    return lib().kfo_expf(float(x))
+
+
+def pyr_down(src: np.ndarray) -> np.ndarray:
+    src = _f32(src)
+    h, w = src.shape
+    dst = np.empty(((h + 1) // 2, (w + 1) // 2), np.float32)
+    lib().kfo_pyr_down(fptr(src), w, h, fptr(dst))
+    return dst
+
+
+def bilateral(src: np.ndarray, ksz=5, sigma_color=10.0, sigma_spatial=10.0) -> np.ndarray:
+    src = _f32(src)
+    h, w = src.shape
+    dst = np.empty_like(src)
+    lib().kfo_bilateral(fptr(src), w, h, ksz, sigma_color, sigma_spatial, fptr(dst))
+    return dst
+
+
+def vertex_map(d: np.ndarray, li: Intrinsics) -> np.ndarray:
+    d = _f32(d)
+    h, w = d.shape
+    v = np.empty((h, w, 3), np.float32)
+    lib().kfo_vertex_map(fptr(d), w, h, li.fx, li.fy, li.cx, li.cy, fptr(v))
+    return v
+
+
+def normal_map(v: np.ndarray) -> np.ndarray:
+    v = _f32(v)
+    h, w, _ = v.shape
+    n = np.empty_like(v)
+    lib().kfo_normal_map(fptr(v), w, h, fptr(n))
+    return n
+
+
+def resize_points_normals(vbig, nbig):
+    vbig, nbig = _f32(vbig), _f32(nbig)
+    hs, ws = vbig.shape[0] // 2, vbig.shape[1] // 2
+    vs = np.empty((hs, ws, 3), np.float32)
+    ns = np.empty((hs, ws, 3), np.float32)
+    lib().kfo_resize_points_normals(fptr(vbig), fptr(nbig), ws, hs, fptr(vs), fptr(ns))
+    return vs, ns
+
+
+def preprocess(depth_mm: np.ndarray, intr: Intrinsics, p: Params):
+    """Returns lists (dmap[l], vmap[l], nmap[l])."""
+    depth_mm = _f32(depth_mm)
+    L = p.pyramid_height
+    ds, vs, ns = [], [], []
+    for l in range(L):
+        li = intr.level(l)
+        ds.append(np.zeros((li.height, li.width), np.float32))
+        vs.append(np.zeros((li.height, li.width, 3), np.float32))
+        ns.append(np.zeros((li.height, li.width, 3), np.float32))
+    PA = C.POINTER(C.c_float) * L
+    lib().kfo_preprocess(fptr(depth_mm), intr.width, intr.height, L, C.byref(intr), C.byref(p),
+                         PA(*[fptr(a) for a in ds]), PA(*[fptr(a) for a in vs]),
+                         PA(*[fptr(a) for a in ns]))
+    return ds, vs, ns
+
+
+def icp_accumulate(cur_v, cur_n, pre_v, pre_n, li: Intrinsics, pose: Pose, dist=0.015, angle=None):
+    if angle is None:
+        angle = float(np.float32(np.sin(np.float32(30.0) * np.float32(0.017453293))))
+    cur_v, cur_n, pre_v, pre_n = map(_f32, (cur_v, cur_n, pre_v, pre_n))
+    h, w = cur_v.shape[:2]
+    sums = np.zeros(27, np.int64)
+    lib().kfo_icp_accumulate(fptr(cur_v), fptr(cur_n), fptr(pre_v), fptr(pre_n), w, h, C.byref(li),
+                             C.byref(pose), dist, angle, i64ptr(sums))
+    return sums
+
+
+def icp_update(sums: np.ndarray, pose: Pose):
+    """Returns (status, new_pose, x[6])."""
+    sums = np.ascontiguousarray(sums, np.int64)
+    p = Pose()
+    C.memmove(C.byref(p), C.byref(pose), C.sizeof(Pose))
+    x = (C.c_double * 6)()
+    st = lib().kfo_icp_update(i64ptr(sums), C.byref(p), x)
+    return st, p, np.array(x[:])
+
+
+def pose_mul(a: Pose, b: Pose) -> Pose:
+    out = Pose()
+    lib().kfo_pose_mul(C.byref(a), C.byref(b), C.byref(out))
+    return out
+
+
+def pose_inv(a: Pose) -> Pose:
+    out = Pose()
+    lib().kfo_pose_inv(C.byref(a), C.byref(out))
+    return out
+
+
+class Volume:
+    """SoA TSDF volume (tsdf int16, weight int16, rgb u8x4), x fastest."""
+
+    def __init__(self, dims, range_m):
+        self.dims = np.array(dims, np.int32)
+        X, Y, Z = (int(d) for d in dims)
+        self.tsdf = np.zeros(X * Y * Z, np.int16)
+        self.weight = np.zeros(X * Y * Z, np.int16)
+        self.rgb = np.zeros(4 * X * Y * Z, np.uint8)
+        self.range = np.array(range_m, np.float32)
+        self.voxel_size = (self.range / self.dims.astype(np.float32)).astype(np.float32)
+
+
+def integrate(vol: Volume, trunc: float, intr: Intrinsics, vol2cam: Pose, dmap_m: np.ndarray,
+              bgr: np.ndarray, cols: np.ndarray | None = None):
+    dmap_m = _f32(dmap_m)
+    bgr = np.ascontiguousarray(bgr, np.uint8)
+    nu, nc = C.c_int64(0), C.c_int64(0)
+    if cols is not None:
+        cols = np.ascontiguousarray(cols, np.int32)
+        cp, ncol = i32ptr(cols), cols.shape[0]
+    else:
+        cp, ncol = None, 0
+    lib().kfo_integrate(i16ptr(vol.tsdf), i16ptr(vol.weight), u8ptr(vol.rgb),
+                        vol.dims.ctypes.data_as(C.POINTER(C.c_int)), fptr(vol.voxel_size), trunc,
+                        C.byref(intr), C.byref(vol2cam), fptr(dmap_m), u8ptr(bgr), cp, ncol,
+                        C.byref(nu), C.byref(nc))
+    return nu.value, nc.value
+
+
+def raycast(vol: Volume, intr: Intrinsics, cam2vol: Pose, Rinv: np.ndarray, pix: np.ndarray | None = None):
+    vmap = np.zeros((intr.height, intr.width, 3), np.float32)
+    nmap = np.zeros_like(vmap)
+    Rinv = _f32(Rinv).reshape(9)
+    if pix is not None:
+        pix = np.ascontiguousarray(pix, np.int32)
+        pp, npix = i32ptr(pix), pix.shape[0]
+    else:
+        pp, npix = None, 0
+    lib().kfo_raycast(i16ptr(vol.tsdf), vol.dims.ctypes.data_as(C.POINTER(C.c_int)), fptr(vol.voxel_size),
+                      fptr(vol.range), C.byref(intr), C.byref(cam2vol), fptr(Rinv), fptr(vmap), fptr(nmap),
+                      pp, npix)
+    return vmap, nmap
+
+
+def format_pose(p: Pose) -> str:
+    buf = C.create_string_buffer(512)
+    lib().kfo_format_pose(C.byref(p), buf, 512)
+    return buf.value.decode()
+
+
+class Pipeline:
+    """kf::kinectfusion restated on the CPU (single thread)."""
+
+    def __init__(self, intr: Intrinsics, p: Params):
+        self.intr, self.p = intr, p
+        self.h = lib().kfo_pipe_create(C.byref(intr), C.byref(p))
+        X, Y, Z = (int(d) for d in p.volu_dims)
+        self.nvox = X * Y * Z
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().kfo_pipe_destroy(self.h)
+            self.h = None
+
+    def reset(self):
+        lib().kfo_pipe_reset(self.h)
+
+    def process(self, bgr: np.ndarray, depth_mm: np.ndarray) -> int:
+        bgr = np.ascontiguousarray(bgr, np.uint8)
+        d = _f32(depth_mm)
+        return lib().kfo_pipe_process(self.h, u8ptr(bgr), fptr(d))
+
+    @property
+    def frame_count(self) -> int:
+        return lib().kfo_pipe_frame_count(self.h)
+
+    def poses(self) -> np.ndarray:
+        n = lib().kfo_pipe_pose_count(self.h)
+        out = np.zeros((n, 4, 4), np.float32)
+        for i in range(n):
+            p = Pose()
+            lib().kfo_pipe_get_pose(self.h, i, C.byref(p))
+            out[i] = p.matrix()
+        return out
+
+    def volume(self):
+        t = np.ctypeslib.as_array(lib().kfo_pipe_tsdf(self.h), shape=(self.nvox,)).copy()
+        w = np.ctypeslib.as_array(lib().kfo_pipe_weight(self.h), shape=(self.nvox,)).copy()
+        c = np.ctypeslib.as_array(lib().kfo_pipe_rgb(self.h), shape=(4 * self.nvox,)).copy()
+        return t, w, c
+
+    def map(self, which: int, kind: int, level: int) -> np.ndarray:
+        li = self.intr.level(level)
+        n = li.width * li.height * (1 if kind == 0 else 3)
+        a = np.ctypeslib.as_array(lib().kfo_pipe_map(self.h, which, kind, level), shape=(n,)).copy()
+        return a.reshape((li.height, li.width) if kind == 0 else (li.height, li.width, 3))
+
+    def last_counts(self):
+        a, b = C.c_int64(), C.c_int64()
+        lib().kfo_pipe_last_counts(self.h, C.byref(a), C.byref(b))
+        return a.value, b.value

@@ -1,0 +1,809 @@
+// kfx_api.hip — host runtime behind the C-ABI (include/kfx.h).
+//
+// Owns every device buffer of one kf::kinectfusion instance, enqueues the
+// per-frame kernel sequence on one HIP stream (captured once into a hipGraph),
+// and keeps the tracking state on the device so a frame needs no host round
+// trip.
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/kfx.h"
+#include "kfx_internal.h"
+
+using namespace kfx;
+
+namespace {
+
+thread_local std::string g_err;
+
+int set_err(int code, const std::string &msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIPCHK(expr)                                                                      \
+  do {                                                                                    \
+    hipError_t e_ = (expr);                                                               \
+    if (e_ != hipSuccess)                                                                 \
+      return set_err(KFX_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));     \
+  } while (0)
+
+DevPose to_dev(const kfx_pose &p) {
+  DevPose d;
+  std::memcpy(d.R, p.R, sizeof(d.R));
+  std::memcpy(d.t, p.t, sizeof(d.t));
+  return d;
+}
+kfx_pose to_api(const DevPose &d) {
+  kfx_pose p;
+  std::memcpy(p.R, d.R, sizeof(p.R));
+  std::memcpy(p.t, d.t, sizeof(p.t));
+  return p;
+}
+DevPose identity_pose() {
+  DevPose p{};
+  p.R[0] = p.R[4] = p.R[8] = 1.f;
+  return p;
+}
+
+// Intrinsics::level (types.hpp:18-28)
+LevelGeom level_geom(const kfx_intrinsics &in, int level) {
+  LevelGeom g;
+  if (level == 0) {
+    g = {in.width, in.height, in.fx, in.fy, in.cx, in.cy};
+    return g;
+  }
+  const float s = std::pow(0.5f, (float)level);
+  g.w = in.width >> level;
+  g.h = in.height >> level;
+  g.fx = in.fx * s;
+  g.fy = in.fy * s;
+  g.cx = (in.cx + 0.5f) * s - 0.5f;
+  g.cy = (in.cy + 0.5f) * s - 0.5f;
+  return g;
+}
+
+constexpr int kInitialPoseCap = 1 << 16;
+
+}  // namespace
+
+struct kfx_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  kfx_intrinsics intr{};
+  kfx_params p{};
+  int L = 0;
+  LevelGeom g[kMaxLevels]{};
+  float angle_thr = 0.f;
+
+  float *raw[kMaxLevels]{};  // raw[0] = f32 mm input, raw[l] = pyrDown outputs
+  uint16_t *raw0_u16 = nullptr;
+  uint8_t *bgr = nullptr;
+  FrameView cur{}, prev{};
+  float *inv_lambda = nullptr;
+  VolView vol{};
+  DevState *st = nullptr;
+  DevPose *pose_log = nullptr;
+  int pose_cap = 0;
+  long long *partials = nullptr;
+  unsigned long long *counters = nullptr;
+  std::vector<void *> allocs;
+
+  float *staged_depth = nullptr;
+  uint8_t *staged_bgr = nullptr;
+  int n_staged = 0;
+
+  bool graph_mode = true;
+  bool profiling = false;
+  hipGraphExec_t graph[2] = {nullptr, nullptr};  // [u16 input]
+  hipEvent_t ev[5]{};
+  float stage_ms[5]{};
+  int pending = 0;      // frames enqueued since the last host sync
+  int known_poses = 1;  // n_poses at the last sync
+};
+
+namespace {
+
+int dalloc(kfx_ctx *c, void **p, size_t bytes) {
+  hipError_t e = hipMalloc(p, bytes);
+  if (e != hipSuccess) {
+    *p = nullptr;
+    return set_err(KFX_ERR_OOM, "hipMalloc(" + std::to_string(bytes) + "): " + hipGetErrorString(e));
+  }
+  c->allocs.push_back(*p);
+  e = hipMemset(*p, 0, bytes);
+  if (e != hipSuccess) return set_err(KFX_ERR_HIP, std::string("hipMemset: ") + hipGetErrorString(e));
+  return KFX_OK;
+}
+
+size_t nvox(const kfx_ctx *c) { return c->vol.slice * (size_t)c->vol.Z; }
+
+void destroy_graphs(kfx_ctx *c) {
+  for (auto &gx : c->graph)
+    if (gx) {
+      (void)hipGraphExecDestroy(gx);
+      gx = nullptr;
+    }
+}
+
+// The per-frame launch sequence (kinectfusion.cpp:78-127 with the frame-1 and
+// failure branches resolved on the device).  ev != nullptr records stage events.
+void enqueue_frame(kfx_ctx *c, bool u16, bool events) {
+  hipStream_t s = c->stream;
+  if (events) (void)hipEventRecord(c->ev[0], s);
+  // imageProcess (kinectfusion.cpp:48-76)
+  if (c->L > 1) {
+    launch_pyr_down(s, c->raw[0], u16 ? c->raw0_u16 : nullptr, c->g[0].w, c->g[0].h, c->raw[1],
+                    c->st);
+    for (int l = 2; l < c->L; ++l)
+      launch_pyr_down(s, c->raw[l - 1], nullptr, c->g[l - 1].w, c->g[l - 1].h, c->raw[l], nullptr);
+  } else {
+    launch_frame_begin(s, c->st);
+  }
+  launch_bilateral_vertex(s, c->L, c->raw, u16 ? c->raw0_u16 : nullptr, c->g, c->cur,
+                          c->p.bfilter_kernel_size, c->p.bfilter_color_sigma,
+                          c->p.bfilter_spatial_sigma, c->p.dfilter_dist, c->st);
+  launch_normals(s, c->L, c->g, c->cur);
+  if (events) (void)hipEventRecord(c->ev[1], s);
+  // ICPRegistration::rigidTransform (icp_registration.cpp:16-46)
+  for (int level = c->L - 1; level >= 0; --level) {
+    const int nb = icp_blocks(c->g[level]);
+    for (int it = 0; it < c->p.icp_iter_count[level]; ++it) {
+      launch_icp_acc(s, c->g[level], c->cur.v[level], c->cur.n[level], c->prev.v[level],
+                     c->prev.n[level], c->p.icp_dist_threshold, c->angle_thr, c->st, c->partials,
+                     0);
+      launch_icp_solve(s, c->st, c->partials, nb, 0, 1);
+    }
+  }
+  launch_commit(s, c->st, c->pose_log, to_dev(c->p.volu_pose));
+  if (events) (void)hipEventRecord(c->ev[2], s);
+  launch_integrate(s, c->vol, c->g[0], c->cur.d[0], c->bgr, c->inv_lambda, c->st, nullptr);
+  if (events) (void)hipEventRecord(c->ev[3], s);
+  launch_raycast(s, c->vol, c->g[0], c->cur, c->prev, c->st);
+  launch_resize(s, c->L, c->g, c->cur, c->prev, c->st);
+  if (events) (void)hipEventRecord(c->ev[4], s);
+}
+
+int build_graph(kfx_ctx *c, bool u16) {
+  hipGraph_t graph = nullptr;
+  HIPCHK(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+  enqueue_frame(c, u16, false);
+  HIPCHK(hipStreamEndCapture(c->stream, &graph));
+  hipError_t e = hipGraphInstantiate(&c->graph[u16 ? 1 : 0], graph, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(graph);
+  if (e != hipSuccess) return set_err(KFX_ERR_HIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(e));
+  return KFX_OK;
+}
+
+int read_state(kfx_ctx *c, DevState *out) {
+  HIPCHK(hipMemcpyAsync(out, c->st, sizeof(DevState), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  c->pending = 0;
+  c->known_poses = out->n_poses;
+  return KFX_OK;
+}
+
+template <typename T>
+int write_field(kfx_ctx *c, size_t off, const T &v) {
+  HIPCHK(hipMemcpyAsync(reinterpret_cast<char *>(c->st) + off, &v, sizeof(T),
+                        hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return KFX_OK;
+}
+
+// Grow the device pose log if the frames about to be queued could overflow it.
+int ensure_pose_capacity(kfx_ctx *c, int more) {
+  if (c->known_poses + c->pending + more < c->pose_cap) return KFX_OK;
+  DevState s;
+  int r = read_state(c, &s);
+  if (r) return r;
+  if (s.n_poses + more < c->pose_cap) return KFX_OK;
+  const int ncap = c->pose_cap * 2;
+  DevPose *nl = nullptr;
+  HIPCHK(hipMalloc(&nl, sizeof(DevPose) * (size_t)ncap));
+  HIPCHK(hipMemcpy(nl, c->pose_log, sizeof(DevPose) * (size_t)c->pose_cap, hipMemcpyDeviceToDevice));
+  for (auto &a : c->allocs)
+    if (a == c->pose_log) a = nl;
+  HIPCHK(hipFree(c->pose_log));
+  c->pose_log = nl;
+  c->pose_cap = ncap;
+  r = write_field(c, offsetof(DevState, pose_cap), ncap);
+  if (r) return r;
+  destroy_graphs(c);  // the commit node holds the old pointer
+  return KFX_OK;
+}
+
+int run_frame(kfx_ctx *c, bool u16) {
+  int r = ensure_pose_capacity(c, 1);
+  if (r) return r;
+  if (c->profiling) {
+    enqueue_frame(c, u16, true);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventSynchronize(c->ev[4]));
+    for (int i = 0; i < 4; ++i) HIPCHK(hipEventElapsedTime(&c->stage_ms[i], c->ev[i], c->ev[i + 1]));
+    HIPCHK(hipEventElapsedTime(&c->stage_ms[4], c->ev[0], c->ev[4]));
+    // stage order in the events: preprocess, icp(+commit), integrate, raycast(+resize)
+  } else if (c->graph_mode) {
+    hipGraphExec_t &gx = c->graph[u16 ? 1 : 0];
+    if (!gx) {
+      r = build_graph(c, u16);
+      if (r) return r;
+    }
+    HIPCHK(hipGraphLaunch(gx, c->stream));
+  } else {
+    enqueue_frame(c, u16, false);
+    HIPCHK(hipGetLastError());
+  }
+  c->pending += 1;
+  return KFX_OK;
+}
+
+int finish_frame(kfx_ctx *c) {
+  DevState s;
+  int r = read_state(c, &s);
+  if (r) return r;
+  return s.mode == MODE_FAIL ? KFX_TRACKING_LOST : KFX_OK;
+}
+
+VolView make_vol(const kfx_params &p) {
+  VolView v{};
+  v.X = p.volu_dims[0];
+  v.Y = p.volu_dims[1];
+  v.Z = p.volu_dims[2];
+  v.tiles_x = v.X / 8;
+  v.tiles_y = v.Y / 8;
+  v.slice = (size_t)v.X * v.Y;
+  for (int i = 0; i < 3; ++i) {
+    v.vs[i] = p.volu_range[i] / (float)p.volu_dims[i];  // tsdf_volume.cpp:16
+    v.range[i] = p.volu_range[i];
+  }
+  v.trunc = p.volu_trun_dist;
+  return v;
+}
+
+int do_reset(kfx_ctx *c) {
+  const size_t n = nvox(c);
+  HIPCHK(hipMemsetAsync(c->vol.tsdf, 0, n * sizeof(int16_t), c->stream));
+  HIPCHK(hipMemsetAsync(c->vol.weight, 0, n * sizeof(int16_t), c->stream));
+  HIPCHK(hipMemsetAsync(c->vol.rgb, 0, n * sizeof(uint32_t), c->stream));
+  for (int l = 0; l < c->L; ++l) {
+    const size_t np = (size_t)c->g[l].w * c->g[l].h;
+    for (FrameView *f : {&c->cur, &c->prev}) {
+      if (f->d[l]) HIPCHK(hipMemsetAsync(f->d[l], 0, np * 4, c->stream));
+      HIPCHK(hipMemsetAsync(f->v[l], 0, np * 12, c->stream));
+      HIPCHK(hipMemsetAsync(f->n[l], 0, np * 12, c->stream));
+    }
+  }
+  DevState s{};
+  s.frame_count = 1;
+  s.mode = MODE_BOOT;
+  s.n_poses = 1;
+  s.pose_cap = c->pose_cap;
+  s.icp_pose = identity_pose();
+  const DevPose I = identity_pose();
+  HIPCHK(hipMemcpyAsync(c->st, &s, sizeof(s), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(c->pose_log, &I, sizeof(I), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  c->pending = 0;
+  c->known_poses = 1;
+  return KFX_OK;
+}
+
+int check_ctx(kfx_ctx *c) {
+  if (!c) return set_err(KFX_ERR_ARG, "null context");
+  hipError_t e = hipSetDevice(c->device);
+  if (e != hipSuccess) return set_err(KFX_ERR_HIP, std::string("hipSetDevice: ") + hipGetErrorString(e));
+  return KFX_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int kfx_abi_version(void) { return KFX_ABI_VERSION; }
+const char *kfx_last_error(void) { return g_err.c_str(); }
+
+int kfx_default_params(kfx_params *p) {
+  if (!p) return set_err(KFX_ERR_ARG, "null params");
+  std::memset(p, 0, sizeof(*p));
+  p->pyramid_height = 3;
+  p->bfilter_color_sigma = 10;
+  p->bfilter_spatial_sigma = 10;
+  p->bfilter_kernel_size = 5;
+  p->dfilter_dist = 5.f;
+  p->icp_angle_threshold = 30.f;
+  p->icp_dist_threshold = 0.015f;
+  p->icp_iter_count[0] = 4;
+  p->icp_iter_count[1] = 5;
+  p->icp_iter_count[2] = 10;
+  for (int i = 0; i < 3; ++i) {
+    p->volu_dims[i] = 512;
+    p->volu_range[i] = 3.f;
+  }
+  p->volu_trun_dist = 2.1f * p->volu_range[0] / (float)p->volu_dims[0];
+  std::memset(&p->volu_pose, 0, sizeof(p->volu_pose));
+  p->volu_pose.R[0] = p->volu_pose.R[4] = p->volu_pose.R[8] = 1.f;
+  p->volu_pose.t[0] = -p->volu_range[0] / 2;
+  p->volu_pose.t[1] = -p->volu_range[1] / 2;
+  p->volu_pose.t[2] = 0.5f;
+  p->min_pose_move = 0.008f;
+  p->tsdf_max_weight = 64;
+  return KFX_OK;
+}
+
+int kfx_create(const kfx_intrinsics *intr, const kfx_params *params, int device, kfx_ctx **out) {
+  if (!intr || !params || !out) return set_err(KFX_ERR_ARG, "null argument");
+  *out = nullptr;
+  const kfx_params &p = *params;
+  if (p.pyramid_height < 1 || p.pyramid_height > KFX_MAX_LEVELS)
+    return set_err(KFX_ERR_ARG, "pyramid_height must be 1..4");
+  const int div = 1 << (p.pyramid_height - 1);
+  if (intr->width <= 0 || intr->height <= 0 || intr->width % (2 * div) || intr->height % (2 * div))
+    return set_err(KFX_ERR_ARG, "width/height must be positive multiples of 2^pyramid_height");
+  for (int i = 0; i < 3; ++i)
+    if (p.volu_dims[i] < 8 || p.volu_range[i] <= 0.f)
+      return set_err(KFX_ERR_ARG, "volume dims must be >= 8 and range > 0");
+  if (p.volu_dims[0] % 8 || p.volu_dims[1] % 8)
+    return set_err(KFX_ERR_ARG, "volume dims x,y must be multiples of 8 (8x8 slice tiles)");
+  if (p.bfilter_kernel_size < 1 || p.bfilter_kernel_size > 15)
+    return set_err(KFX_ERR_ARG, "bfilter_kernel_size must be 1..15");
+  for (int l = 0; l < p.pyramid_height; ++l)
+    if (p.icp_iter_count[l] < 0) return set_err(KFX_ERR_ARG, "negative icp_iter_count");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+    return set_err(KFX_ERR_NO_DEVICE, "no HIP device");
+  if (device < 0 || device >= ndev) return set_err(KFX_ERR_ARG, "bad device ordinal");
+
+  kfx_ctx *c = new kfx_ctx();
+  c->device = device;
+  c->intr = *intr;
+  c->p = p;
+  c->L = p.pyramid_height;
+  for (int l = 0; l < c->L; ++l) c->g[l] = level_geom(*intr, l);
+  c->angle_thr = std::sin(p.icp_angle_threshold * 0.017453293f);  // icp_registration.cpp:5
+  int r = KFX_OK;
+  auto fail = [&](int code) {
+    kfx_destroy(c);
+    return code;
+  };
+  if (hipSetDevice(device) != hipSuccess) return fail(set_err(KFX_ERR_HIP, "hipSetDevice failed"));
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
+    return fail(set_err(KFX_ERR_HIP, "hipStreamCreate failed"));
+  for (auto &e : c->ev)
+    if (hipEventCreate(&e) != hipSuccess) return fail(set_err(KFX_ERR_HIP, "hipEventCreate failed"));
+
+  for (int l = 0; l < c->L; ++l) {
+    const size_t np = (size_t)c->g[l].w * c->g[l].h;
+    if ((r = dalloc(c, (void **)&c->raw[l], np * 4))) return fail(r);
+    if ((r = dalloc(c, (void **)&c->cur.d[l], np * 4))) return fail(r);
+    if ((r = dalloc(c, (void **)&c->cur.v[l], np * 12))) return fail(r);
+    if ((r = dalloc(c, (void **)&c->cur.n[l], np * 12))) return fail(r);
+    if ((r = dalloc(c, (void **)&c->prev.v[l], np * 12))) return fail(r);
+    if ((r = dalloc(c, (void **)&c->prev.n[l], np * 12))) return fail(r);
+  }
+  const size_t np0 = (size_t)intr->width * intr->height;
+  if ((r = dalloc(c, (void **)&c->raw0_u16, np0 * 2))) return fail(r);
+  if ((r = dalloc(c, (void **)&c->bgr, np0 * 3))) return fail(r);
+  if ((r = dalloc(c, (void **)&c->inv_lambda, np0 * 4))) return fail(r);
+  c->vol = make_vol(p);
+  const size_t n = nvox(c);
+  if ((r = dalloc(c, (void **)&c->vol.tsdf, n * 2))) return fail(r);
+  if ((r = dalloc(c, (void **)&c->vol.weight, n * 2))) return fail(r);
+  if ((r = dalloc(c, (void **)&c->vol.rgb, n * 4))) return fail(r);
+  if ((r = dalloc(c, (void **)&c->st, sizeof(DevState)))) return fail(r);
+  c->pose_cap = kInitialPoseCap;
+  if ((r = dalloc(c, (void **)&c->pose_log, sizeof(DevPose) * (size_t)c->pose_cap))) return fail(r);
+  int maxnb = 1;
+  for (int l = 0; l < c->L; ++l) maxnb = std::max(maxnb, icp_blocks(c->g[l]));
+  if ((r = dalloc(c, (void **)&c->partials, sizeof(long long) * 27 * (size_t)maxnb))) return fail(r);
+  if ((r = dalloc(c, (void **)&c->counters, sizeof(unsigned long long) * 32))) return fail(r);
+  launch_inv_lambda(c->stream, c->g[0], c->inv_lambda);
+  if ((r = do_reset(c))) return fail(r);
+  *out = c;
+  return KFX_OK;
+}
+
+int kfx_destroy(kfx_ctx *c) {
+  if (!c) return KFX_OK;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  destroy_graphs(c);
+  for (void *a : c->allocs) (void)hipFree(a);
+  for (auto &e : c->ev)
+    if (e) (void)hipEventDestroy(e);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+  return KFX_OK;
+}
+
+int kfx_reset(kfx_ctx *c) {
+  int r = check_ctx(c);
+  if (r) return r;
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return do_reset(c);
+}
+
+int kfx_pipeline(kfx_ctx *c, const uint8_t *bgr, const float *depth_mm) {
+  int r = check_ctx(c);
+  if (r) return r;
+  if (!bgr || !depth_mm) return set_err(KFX_ERR_ARG, "null image");
+  const size_t np = (size_t)c->intr.width * c->intr.height;
+  HIPCHK(hipMemcpyAsync(c->raw[0], depth_mm, np * 4, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(c->bgr, bgr, np * 3, hipMemcpyHostToDevice, c->stream));
+  if ((r = run_frame(c, false))) return r;
+  return finish_frame(c);
+}
+
+int kfx_pipeline_u16(kfx_ctx *c, const uint8_t *bgr, const uint16_t *depth_mm) {
+  int r = check_ctx(c);
+  if (r) return r;
+  if (!bgr || !depth_mm) return set_err(KFX_ERR_ARG, "null image");
+  const size_t np = (size_t)c->intr.width * c->intr.height;
+  HIPCHK(hipMemcpyAsync(c->raw0_u16, depth_mm, np * 2, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(c->bgr, bgr, np * 3, hipMemcpyHostToDevice, c->stream));
+  if ((r = run_frame(c, true))) return r;
+  return finish_frame(c);
+}
+
+int kfx_stage_frames(kfx_ctx *c, int n, const uint8_t *bgr, const float *depth_mm) {
+  int r = check_ctx(c);
+  if (r) return r;
+  if (n <= 0 || !bgr || !depth_mm) return set_err(KFX_ERR_ARG, "bad staged frames");
+  HIPCHK(hipStreamSynchronize(c->stream));
+  const size_t np = (size_t)c->intr.width * c->intr.height;
+  for (void *pp : {(void *)c->staged_depth, (void *)c->staged_bgr}) {
+    if (!pp) continue;
+    c->allocs.erase(std::remove(c->allocs.begin(), c->allocs.end(), pp), c->allocs.end());
+    (void)hipFree(pp);
+  }
+  c->staged_depth = nullptr;
+  c->staged_bgr = nullptr;
+  c->n_staged = 0;
+  if ((r = dalloc(c, (void **)&c->staged_depth, np * 4 * (size_t)n))) return r;
+  if ((r = dalloc(c, (void **)&c->staged_bgr, np * 3 * (size_t)n))) return r;
+  HIPCHK(hipMemcpy(c->staged_depth, depth_mm, np * 4 * (size_t)n, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(c->staged_bgr, bgr, np * 3 * (size_t)n, hipMemcpyHostToDevice));
+  c->n_staged = n;
+  return KFX_OK;
+}
+
+int kfx_pipeline_staged(kfx_ctx *c, int idx) {
+  int r = check_ctx(c);
+  if (r) return r;
+  if (idx < 0 || idx >= c->n_staged) return set_err(KFX_ERR_ARG, "staged frame index out of range");
+  const size_t np = (size_t)c->intr.width * c->intr.height;
+  HIPCHK(hipMemcpyAsync(c->raw[0], c->staged_depth + np * idx, np * 4, hipMemcpyDeviceToDevice,
+                        c->stream));
+  HIPCHK(hipMemcpyAsync(c->bgr, c->staged_bgr + np * 3 * idx, np * 3, hipMemcpyDeviceToDevice,
+                        c->stream));
+  return run_frame(c, false);
+}
+
+int kfx_synchronize(kfx_ctx *c) {
+  int r = check_ctx(c);
+  if (r) return r;
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return KFX_OK;
+}
+
+int kfx_set_graph_mode(kfx_ctx *c, int enabled) {
+  if (!c) return set_err(KFX_ERR_ARG, "null context");
+  c->graph_mode = enabled != 0;
+  return KFX_OK;
+}
+
+int kfx_set_profiling(kfx_ctx *c, int enabled) {
+  if (!c) return set_err(KFX_ERR_ARG, "null context");
+  c->profiling = enabled != 0;
+  return KFX_OK;
+}
+
+int kfx_get_stage_ms(kfx_ctx *c, float out[5]) {
+  if (!c || !out) return set_err(KFX_ERR_ARG, "null argument");
+  std::memcpy(out, c->stage_ms, sizeof(c->stage_ms));
+  return KFX_OK;
+}
+
+int kfx_get_cur_camera_pose(kfx_ctx *c, kfx_pose *out) {
+  int r = check_ctx(c);
+  if (r) return r;
+  if (!out) return set_err(KFX_ERR_ARG, "null pose");
+  DevState s;
+  if ((r = read_state(c, &s))) return r;
+  DevPose d;
+  HIPCHK(hipMemcpy(&d, c->pose_log + (s.n_poses - 1), sizeof(d), hipMemcpyDeviceToHost));
+  *out = to_api(d);
+  return KFX_OK;
+}
+
+int kfx_get_frame_count(kfx_ctx *c, int *out) {
+  int r = check_ctx(c);
+  if (r) return r;
+  if (!out) return set_err(KFX_ERR_ARG, "null out");
+  DevState s;
+  if ((r = read_state(c, &s))) return r;
+  *out = s.frame_count;
+  return KFX_OK;
+}
+
+int kfx_get_pose_record(kfx_ctx *c, kfx_pose *out, int cap, int *n) {
+  int r = check_ctx(c);
+  if (r) return r;
+  if (!n) return set_err(KFX_ERR_ARG, "null n");
+  DevState s;
+  if ((r = read_state(c, &s))) return r;
+  *n = s.n_poses;
+  const int m = std::min(cap, s.n_poses);
+  if (out && m > 0) {
+    std::vector<DevPose> tmp(m);
+    HIPCHK(hipMemcpy(tmp.data(), c->pose_log, sizeof(DevPose) * m, hipMemcpyDeviceToHost));
+    for (int i = 0; i < m; ++i) out[i] = to_api(tmp[i]);
+  }
+  return s.pose_overflow ? set_err(KFX_ERR_STATE, "pose log overflow") : KFX_OK;
+}
+
+int kfx_write_poses_txt(kfx_ctx *c, const char *path) {
+  int n = 0;
+  int r = kfx_get_pose_record(c, nullptr, 0, &n);
+  if (r) return r;
+  std::vector<kfx_pose> ps(n);
+  if ((r = kfx_get_pose_record(c, ps.data(), n, &n))) return r;
+  FILE *f = std::fopen(path, "w");
+  if (!f) return set_err(KFX_ERR_ARG, std::string("cannot open ") + path);
+  for (const kfx_pose &p : ps)  // main.cpp:96-97: outfile << matrix << std::endl
+    std::fprintf(f,
+                 "[%.8g, %.8g, %.8g, %.8g;\n %.8g, %.8g, %.8g, %.8g;\n %.8g, %.8g, %.8g, %.8g;\n "
+                 "0, 0, 0, 1]\n",
+                 p.R[0], p.R[1], p.R[2], p.t[0], p.R[3], p.R[4], p.R[5], p.t[1], p.R[6], p.R[7],
+                 p.R[8], p.t[2]);
+  std::fclose(f);
+  return KFX_OK;
+}
+
+int kfx_get_frame_maps(kfx_ctx *c, int which, int level, float *dmap, float *vmap, float *nmap) {
+  int r = check_ctx(c);
+  if (r) return r;
+  if (level < 0 || level >= c->L || (which != KFX_FRAME_CUR && which != KFX_FRAME_PREV))
+    return set_err(KFX_ERR_ARG, "bad frame/level");
+  HIPCHK(hipStreamSynchronize(c->stream));
+  const FrameView &f = which == KFX_FRAME_CUR ? c->cur : c->prev;
+  const size_t np = (size_t)c->g[level].w * c->g[level].h;
+  if (dmap) {
+    if (which == KFX_FRAME_CUR)
+      HIPCHK(hipMemcpy(dmap, f.d[level], np * 4, hipMemcpyDeviceToHost));
+    else
+      std::memset(dmap, 0, np * 4);
+  }
+  if (vmap) HIPCHK(hipMemcpy(vmap, f.v[level], np * 12, hipMemcpyDeviceToHost));
+  if (nmap) HIPCHK(hipMemcpy(nmap, f.n[level], np * 12, hipMemcpyDeviceToHost));
+  return KFX_OK;
+}
+
+int kfx_set_frame_maps(kfx_ctx *c, int which, int level, const float *vmap, const float *nmap) {
+  int r = check_ctx(c);
+  if (r) return r;
+  if (level < 0 || level >= c->L || (which != KFX_FRAME_CUR && which != KFX_FRAME_PREV))
+    return set_err(KFX_ERR_ARG, "bad frame/level");
+  HIPCHK(hipStreamSynchronize(c->stream));
+  const FrameView &f = which == KFX_FRAME_CUR ? c->cur : c->prev;
+  const size_t np = (size_t)c->g[level].w * c->g[level].h;
+  if (vmap) HIPCHK(hipMemcpy(f.v[level], vmap, np * 12, hipMemcpyHostToDevice));
+  if (nmap) HIPCHK(hipMemcpy(f.n[level], nmap, np * 12, hipMemcpyHostToDevice));
+  return KFX_OK;
+}
+
+static int slab_z(const kfx_ctx *c, size_t bytes_per_voxel) {
+  const size_t budget = 64u << 20;
+  size_t nz = budget / (c->vol.slice * bytes_per_voxel);
+  if (nz < 1) nz = 1;
+  if (nz > (size_t)c->vol.Z) nz = c->vol.Z;
+  return (int)nz;
+}
+
+int kfx_download_tsdf(kfx_ctx *c, void *dst) {
+  int r = check_ctx(c);
+  if (r) return r;
+  if (!dst) return set_err(KFX_ERR_ARG, "null dst");
+  const int nz = slab_z(c, 8);
+  uint64_t *tmp = nullptr;
+  HIPCHK(hipMalloc(&tmp, c->vol.slice * 8 * (size_t)nz));
+  for (int z0 = 0; z0 < c->vol.Z; z0 += nz) {
+    const int k = std::min(nz, c->vol.Z - z0);
+    launch_export_records(c->stream, c->vol, z0, k, tmp);
+    hipError_t e = hipMemcpyAsync((char *)dst + c->vol.slice * 8 * (size_t)z0, tmp,
+                                  c->vol.slice * 8 * (size_t)k, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) {
+      (void)hipFree(tmp);
+      return set_err(KFX_ERR_HIP, std::string("download_tsdf: ") + hipGetErrorString(e));
+    }
+  }
+  HIPCHK(hipFree(tmp));
+  return KFX_OK;
+}
+
+int kfx_upload_tsdf(kfx_ctx *c, const void *src) {
+  int r = check_ctx(c);
+  if (r) return r;
+  if (!src) return set_err(KFX_ERR_ARG, "null src");
+  HIPCHK(hipStreamSynchronize(c->stream));
+  const int nz = slab_z(c, 8);
+  uint64_t *tmp = nullptr;
+  HIPCHK(hipMalloc(&tmp, c->vol.slice * 8 * (size_t)nz));
+  for (int z0 = 0; z0 < c->vol.Z; z0 += nz) {
+    const int k = std::min(nz, c->vol.Z - z0);
+    hipError_t e = hipMemcpyAsync(tmp, (const char *)src + c->vol.slice * 8 * (size_t)z0,
+                                  c->vol.slice * 8 * (size_t)k, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) {
+      launch_import_records(c->stream, c->vol, z0, k, tmp);
+      e = hipStreamSynchronize(c->stream);
+    }
+    if (e != hipSuccess) {
+      (void)hipFree(tmp);
+      return set_err(KFX_ERR_HIP, std::string("upload_tsdf: ") + hipGetErrorString(e));
+    }
+  }
+  HIPCHK(hipFree(tmp));
+  return KFX_OK;
+}
+
+int kfx_download_volume_soa(kfx_ctx *c, int16_t *t, int16_t *w, uint8_t *rgba) {
+  int r = check_ctx(c);
+  if (r) return r;
+  const int nz = slab_z(c, 8);
+  const size_t cap = c->vol.slice * (size_t)nz;
+  char *tmp = nullptr;
+  HIPCHK(hipMalloc(&tmp, cap * 8));
+  int16_t *dt = (int16_t *)tmp;
+  int16_t *dw = (int16_t *)(tmp + cap * 2);
+  uint32_t *dc = (uint32_t *)(tmp + cap * 4);
+  for (int z0 = 0; z0 < c->vol.Z; z0 += nz) {
+    const int k = std::min(nz, c->vol.Z - z0);
+    const size_t cnt = c->vol.slice * (size_t)k, off = c->vol.slice * (size_t)z0;
+    launch_export_soa(c->stream, c->vol, z0, k, dt, dw, dc);
+    hipError_t e = hipSuccess;
+    if (t) e = hipMemcpyAsync(t + off, dt, cnt * 2, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess && w) e = hipMemcpyAsync(w + off, dw, cnt * 2, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess && rgba)
+      e = hipMemcpyAsync(rgba + 4 * off, dc, cnt * 4, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) {
+      (void)hipFree(tmp);
+      return set_err(KFX_ERR_HIP, std::string("download_soa: ") + hipGetErrorString(e));
+    }
+  }
+  HIPCHK(hipFree(tmp));
+  return KFX_OK;
+}
+
+int kfx_stage_preprocess(kfx_ctx *c, const uint8_t *bgr, const float *depth_mm) {
+  int r = check_ctx(c);
+  if (r) return r;
+  if (!bgr || !depth_mm) return set_err(KFX_ERR_ARG, "null image");
+  const size_t np = (size_t)c->intr.width * c->intr.height;
+  HIPCHK(hipMemcpyAsync(c->raw[0], depth_mm, np * 4, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(c->bgr, bgr, np * 3, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemsetAsync(reinterpret_cast<char *>(c->st) + offsetof(DevState, dmax_bits), 0,
+                        sizeof(((DevState *)nullptr)->dmax_bits), c->stream));
+  for (int l = 1; l < c->L; ++l)
+    launch_pyr_down(c->stream, c->raw[l - 1], nullptr, c->g[l - 1].w, c->g[l - 1].h, c->raw[l],
+                    nullptr);
+  launch_bilateral_vertex(c->stream, c->L, c->raw, nullptr, c->g, c->cur, c->p.bfilter_kernel_size,
+                          c->p.bfilter_color_sigma, c->p.bfilter_spatial_sigma, c->p.dfilter_dist,
+                          c->st);
+  launch_normals(c->stream, c->L, c->g, c->cur);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return KFX_OK;
+}
+
+int kfx_stage_icp_accumulate(kfx_ctx *c, int level, const kfx_pose *pose, int64_t sums[27]) {
+  int r = check_ctx(c);
+  if (r) return r;
+  if (level < 0 || level >= c->L || !pose || !sums) return set_err(KFX_ERR_ARG, "bad argument");
+  if ((r = write_field(c, offsetof(DevState, icp_pose), to_dev(*pose)))) return r;
+  launch_icp_acc(c->stream, c->g[level], c->cur.v[level], c->cur.n[level], c->prev.v[level],
+                 c->prev.n[level], c->p.icp_dist_threshold, c->angle_thr, c->st, c->partials, 1);
+  launch_icp_solve(c->stream, c->st, c->partials, icp_blocks(c->g[level]), 1, 0);
+  HIPCHK(hipGetLastError());
+  DevState s;
+  if ((r = read_state(c, &s))) return r;
+  for (int k = 0; k < 27; ++k) sums[k] = s.sums[k];
+  return KFX_OK;
+}
+
+int kfx_stage_icp(kfx_ctx *c, kfx_pose *out) {
+  int r = check_ctx(c);
+  if (r) return r;
+  DevState s0;
+  if ((r = read_state(c, &s0))) return r;
+  DevState s = s0;
+  s.mode = MODE_TRACK;
+  s.icp_fail = 0;
+  s.icp_pose = identity_pose();
+  HIPCHK(hipMemcpyAsync(c->st, &s, sizeof(s), hipMemcpyHostToDevice, c->stream));
+  for (int level = c->L - 1; level >= 0; --level) {
+    const int nb = icp_blocks(c->g[level]);
+    for (int it = 0; it < c->p.icp_iter_count[level]; ++it) {
+      launch_icp_acc(c->stream, c->g[level], c->cur.v[level], c->cur.n[level], c->prev.v[level],
+                     c->prev.n[level], c->p.icp_dist_threshold, c->angle_thr, c->st, c->partials,
+                     0);
+      launch_icp_solve(c->stream, c->st, c->partials, nb, 0, 1);
+    }
+  }
+  HIPCHK(hipGetLastError());
+  if ((r = read_state(c, &s))) return r;
+  if (out) *out = to_api(s.icp_pose);
+  const int failed = s.icp_fail;
+  HIPCHK(hipMemcpyAsync(c->st, &s0, sizeof(s0), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return failed ? KFX_TRACKING_LOST : KFX_OK;
+}
+
+static int integrate_counts_impl(kfx_ctx *c, int64_t *nu, int64_t *nc) {
+  HIPCHK(hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * 32, c->stream));
+  launch_integrate(c->stream, c->vol, c->g[0], c->cur.d[0], c->bgr, c->inv_lambda, c->st,
+                   c->counters);
+  HIPCHK(hipGetLastError());
+  unsigned long long h[32];
+  HIPCHK(hipMemcpyAsync(h, c->counters, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  int64_t a = 0, b = 0;
+  for (int i = 0; i < 16; ++i) {
+    a += (int64_t)h[2 * i];
+    b += (int64_t)h[2 * i + 1];
+  }
+  if (nu) *nu = a;
+  if (nc) *nc = b;
+  return KFX_OK;
+}
+
+int kfx_stage_integrate(kfx_ctx *c, const kfx_pose *vol2cam, int64_t *nu, int64_t *nc) {
+  int r = check_ctx(c);
+  if (r) return r;
+  if (!vol2cam) return set_err(KFX_ERR_ARG, "null pose");
+  DevState s0;
+  if ((r = read_state(c, &s0))) return r;
+  DevState s = s0;
+  s.mode = MODE_TRACK;
+  s.vol2cam = to_dev(*vol2cam);
+  HIPCHK(hipMemcpyAsync(c->st, &s, sizeof(s), hipMemcpyHostToDevice, c->stream));
+  if (nu || nc)
+    if ((r = integrate_counts_impl(c, nu, nc))) return r;
+  launch_integrate(c->stream, c->vol, c->g[0], c->cur.d[0], c->bgr, c->inv_lambda, c->st, nullptr);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(c->st, &s0, sizeof(s0), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return KFX_OK;
+}
+
+int kfx_integrate_counts(kfx_ctx *c, int64_t *nu, int64_t *nc) {
+  int r = check_ctx(c);
+  if (r) return r;
+  return integrate_counts_impl(c, nu, nc);
+}
+
+int kfx_stage_raycast(kfx_ctx *c, const kfx_pose *cam2vol, const float Rinv[9]) {
+  int r = check_ctx(c);
+  if (r) return r;
+  if (!cam2vol || !Rinv) return set_err(KFX_ERR_ARG, "null argument");
+  DevState s0;
+  if ((r = read_state(c, &s0))) return r;
+  DevState s = s0;
+  s.mode = MODE_TRACK;
+  s.cam2vol = to_dev(*cam2vol);
+  std::memcpy(s.Rinv, Rinv, sizeof(s.Rinv));
+  HIPCHK(hipMemcpyAsync(c->st, &s, sizeof(s), hipMemcpyHostToDevice, c->stream));
+  launch_raycast(c->stream, c->vol, c->g[0], c->cur, c->prev, c->st);
+  launch_resize(c->stream, c->L, c->g, c->cur, c->prev, c->st);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(c->st, &s0, sizeof(s0), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return KFX_OK;
+}
+
+}  // extern "C"

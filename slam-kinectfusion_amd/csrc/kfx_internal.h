@@ -1,0 +1,94 @@
+// kfx_internal.h — types shared by the HIP kernels (kfx_kernels.hip) and the
+// host runtime (kfx_api.hip).  Not part of the public ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace kfx {
+
+constexpr int kMaxLevels = 4;
+
+enum FrameMode : int { MODE_BOOT = 0, MODE_TRACK = 1, MODE_FAIL = 2 };
+
+struct DevPose {
+  float R[9];  // row-major
+  float t[3];
+};
+
+// Per-frame tracking state, resident in device memory so the whole frame runs
+// without a host round trip.
+struct DevState {
+  int frame_count;      // kinectfusion::frame_count (kinectfusion.h:58)
+  int mode;             // FrameMode of the frame in flight
+  int icp_fail;         // set by the ICP solve on det failure (icp_registration.cpp:35-37)
+  int n_poses;          // pose_record.size()
+  int pose_cap;         // capacity of the pose log
+  int pose_overflow;
+  int pad0[2];
+  unsigned dmax_bits[16];  // max valid level-0 depth of this frame (float bits), sharded
+  DevPose icp_pose;     // camera_pose inside rigidTransform
+  DevPose vol2cam;      // TSDFVolume::integrate pose (tsdf_volume.cpp:50)
+  DevPose cam2vol;      // TSDFVolume::raycast pose (tsdf_volume.cpp:59)
+  float Rinv[9];        // cam2vol.rotation().inv() (D: transpose)
+  float pad1[3];
+  long long sums[27];   // last ICP sums (test seam)
+  double x[6];          // last ICP increment
+};
+
+struct LevelGeom {
+  int w, h;
+  float fx, fy, cx, cy;
+};
+
+// SoA TSDF volume.  Each z slice is tiled in 8x8 (x,y) tiles; voxel (x,y,z)
+// lives at z*slice + ((y>>3)*tiles_x + (x>>3))*64 + (y&7)*8 + (x&7).
+struct VolView {
+  int16_t *tsdf;
+  int16_t *weight;
+  uint32_t *rgb;  // u8 c0,c1,c2,pad
+  int X, Y, Z;
+  int tiles_x, tiles_y;
+  float vs[3];     // voxel size per axis
+  float range[3];  // volume_range
+  float trunc;
+  size_t slice;    // voxels per z slice (= X*Y)
+};
+
+struct FrameView {
+  float *d[kMaxLevels];
+  float *v[kMaxLevels];
+  float *n[kMaxLevels];
+};
+
+// ---- launchers (kfx_kernels.hip) -----------------------------------------
+void launch_frame_begin(hipStream_t s, DevState *st);
+void launch_pyr_down(hipStream_t s, const float *src, const uint16_t *src16, int w, int h,
+                     float *dst, DevState *st_begin);
+void launch_bilateral_vertex(hipStream_t s, int levels, const float *const raw[kMaxLevels],
+                             const uint16_t *raw0_u16, const LevelGeom *g, FrameView cur,
+                             int ksz, float sigma_color, float sigma_spatial, float max_dist,
+                             DevState *st);
+void launch_normals(hipStream_t s, int levels, const LevelGeom *g, FrameView cur);
+int icp_blocks(const LevelGeom &g);
+void launch_icp_acc(hipStream_t s, const LevelGeom &g, const float *cv, const float *cn,
+                    const float *pv, const float *pn, float dist_thr, float angle_thr,
+                    DevState *st, long long *partials, int force);
+void launch_icp_solve(hipStream_t s, DevState *st, const long long *partials, int nblocks,
+                      int force_mode, int update);
+void launch_commit(hipStream_t s, DevState *st, DevPose *pose_log, DevPose volume_pose);
+void launch_integrate(hipStream_t s, VolView v, LevelGeom g0, const float *dmap,
+                      const uint8_t *bgr, const float *inv_lambda, const DevState *st,
+                      unsigned long long *counters /* non-null: count-only, 32 words */);
+void launch_raycast(hipStream_t s, VolView v, LevelGeom g0, FrameView cur, FrameView prev,
+                    const DevState *st);
+void launch_resize(hipStream_t s, int levels, const LevelGeom *g, FrameView cur, FrameView prev,
+                   const DevState *st);
+void launch_inv_lambda(hipStream_t s, LevelGeom g0, float *inv_lambda);
+void launch_export_records(hipStream_t s, VolView v, int z0, int nz, uint64_t *dst);
+void launch_import_records(hipStream_t s, VolView v, int z0, int nz, const uint64_t *src);
+void launch_export_soa(hipStream_t s, VolView v, int z0, int nz, int16_t *t, int16_t *w,
+                       uint32_t *c);
+
+}  // namespace kfx

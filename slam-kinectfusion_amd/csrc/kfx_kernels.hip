@@ -1,0 +1,1005 @@
+// kfx_kernels.hip — hand-written CDNA4 (gfx950) kernels of the KinectFusion hot
+// path: preprocess (pyrDown, bilateral, truncation, vertex/normal maps), ICP
+// (projective association + 27-term exact reduction + on-device 6x6 solve),
+// TSDF integrate, raycast and pyramid resize.
+//
+// Every float expression follows the reference's evaluation order (file:line
+// cited per kernel) and the file is compiled with -ffp-contract=off, so results
+// are bit-identical to the CPU oracle (oracle/kfx_oracle.cpp) on the same inputs.
+#include <climits>
+
+#include "kfx_internal.h"
+
+namespace kfx {
+namespace {
+
+constexpr float kDivShortMax = 0.0000305185f;  // device_utils.cuh:6
+constexpr int kShortMax = 32767;               // device_utils.cuh:7
+constexpr int kMaxWeight = 64;                 // device_utils.cuh:5 (A10)
+constexpr float kFix = 4294967296.0f;          // ICP fixed point 2^32 (D)
+constexpr int kDmaxShards = 16;
+
+struct f3 {
+  float x, y, z;
+};
+__device__ __forceinline__ f3 add(f3 a, f3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+__device__ __forceinline__ f3 sub(f3 a, f3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+__device__ __forceinline__ f3 scl(f3 a, float s) { return {a.x * s, a.y * s, a.z * s}; }
+__device__ __forceinline__ f3 mulc(f3 a, f3 b) { return {a.x * b.x, a.y * b.y, a.z * b.z}; }
+__device__ __forceinline__ float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ f3 cross(f3 a, f3 b) {
+  return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+}
+__device__ __forceinline__ f3 normalized(f3 v) {
+  const float t = sqrtf(dot(v, v));
+  return {v.x / t, v.y / t, v.z / t};
+}
+__device__ __forceinline__ f3 rmul(const float *R, f3 v) {
+  return {R[0] * v.x + R[1] * v.y + R[2] * v.z, R[3] * v.x + R[4] * v.y + R[5] * v.z,
+          R[6] * v.x + R[7] * v.y + R[8] * v.z};
+}
+__device__ __forceinline__ f3 ld3(const float *p, size_t i) {
+  return {p[3 * i], p[3 * i + 1], p[3 * i + 2]};
+}
+__device__ __forceinline__ void st3(float *p, size_t i, f3 v) {
+  p[3 * i] = v.x;
+  p[3 * i + 1] = v.y;
+  p[3 * i + 2] = v.z;
+}
+// __float2int_rn / __float2int_rd, out-of-range -> INT_MIN (rejected by every
+// bounds check, as the saturated CUDA result is)
+__device__ __forceinline__ int f2i_rn(float v) {
+  const float r = rintf(v);
+  return (r > -2.0e9f && r < 2.0e9f) ? (int)r : INT_MIN;
+}
+__device__ __forceinline__ int f2i_rd(float v) {
+  const float r = floorf(v);
+  return (r > -2.0e9f && r < 2.0e9f) ? (int)r : INT_MIN;
+}
+__device__ __forceinline__ int reflect101(int i, int n) {
+  if (i < 0) i = -i;
+  if (i >= n) i = 2 * n - 2 - i;
+  return i;
+}
+// Deterministic exp (same constants/order as the oracle's kfo_expf).
+__device__ __forceinline__ float det_expf(float x) {
+  if (!(x >= -86.0f)) return 0.0f;
+  const float kf = rintf(x * 1.44269502f);
+  const float r = (x - kf * 0.693145751953125f) - kf * 1.42860677e-6f;
+  float p = 1.98412698e-4f;
+  p = p * r + 1.38888889e-3f;
+  p = p * r + 8.33333377e-3f;
+  p = p * r + 4.16666679e-2f;
+  p = p * r + 1.66666672e-1f;
+  p = p * r + 0.5f;
+  p = p * r + 1.0f;
+  p = p * r + 1.0f;
+  const int k = (int)kf;
+  return p * __uint_as_float((unsigned)(k + 127) << 23);
+}
+
+__device__ __forceinline__ DevPose pose_identity() {
+  DevPose p;
+  for (int i = 0; i < 9; ++i) p.R[i] = (i % 4 == 0) ? 1.f : 0.f;
+  p.t[0] = p.t[1] = p.t[2] = 0.f;
+  return p;
+}
+// Affine3f a*b (OpenCV concatenate/rotate/translate order)
+__device__ DevPose pose_mul(const DevPose &a, const DevPose &b) {
+  DevPose r;
+  for (int j = 0; j < 3; ++j) {
+    for (int i = 0; i < 3; ++i) {
+      float v = 0.f;
+      for (int k = 0; k < 3; ++k) v += a.R[3 * j + k] * b.R[3 * k + i];
+      r.R[3 * j + i] = v;
+    }
+    float d = 0.f;
+    for (int k = 0; k < 3; ++k) d += a.R[3 * j + k] * b.t[k];
+    r.t[j] = d + a.t[j];
+  }
+  return r;
+}
+// Affine3f::inv (D: analytic rigid inverse)
+__device__ DevPose pose_inv(const DevPose &a) {
+  DevPose r;
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) r.R[3 * i + j] = a.R[3 * j + i];
+  for (int j = 0; j < 3; ++j) {
+    float d = 0.f;
+    for (int k = 0; k < 3; ++k) d += a.R[3 * k + j] * a.t[k];
+    r.t[j] = -d;
+  }
+  return r;
+}
+
+__device__ __forceinline__ void frame_begin(DevState *st) {
+  st->mode = (st->frame_count == 1) ? MODE_BOOT : MODE_TRACK;
+  st->icp_fail = 0;
+  st->icp_pose = pose_identity();
+  for (int i = 0; i < kDmaxShards; ++i) st->dmax_bits[i] = 0u;
+}
+
+__device__ __forceinline__ size_t vox_index(const VolView &v, int x, int y, int z) {
+  return (size_t)z * v.slice + ((size_t)(y >> 3) * v.tiles_x + (x >> 3)) * 64 + ((y & 7) << 3) +
+         (x & 7);
+}
+
+// Level-indexed block decomposition for kernels that process all pyramid
+// levels in one launch (16x16 pixel tiles).
+struct LevelTiles {
+  LevelGeom g[kMaxLevels];
+  int off[kMaxLevels + 1];
+  int nbx[kMaxLevels];
+  int levels;
+};
+__device__ __forceinline__ int find_level(const LevelTiles &t, int b) {
+  int l = 0;
+  while (l + 1 < t.levels && b >= t.off[l + 1]) ++l;
+  return l;
+}
+LevelTiles make_tiles(int levels, const LevelGeom *g) {
+  LevelTiles t{};
+  t.levels = levels;
+  int acc = 0;
+  for (int l = 0; l < levels; ++l) {
+    t.g[l] = g[l];
+    t.nbx[l] = (g[l].w + 15) / 16;
+    t.off[l] = acc;
+    acc += t.nbx[l] * ((g[l].h + 15) / 16);
+  }
+  t.off[levels] = acc;
+  return t;
+}
+
+// ---------------------------------------------------------------------------
+// Preprocess
+
+__global__ void k_frame_begin(DevState *st) { frame_begin(st); }
+
+// cv::cuda::pyrDown (kinectfusion.cpp:54-55; OpenCV pyr_down.cu): vertical
+// 5-tap at src row 2y for the 5 source columns, then horizontal 5-tap.
+template <typename T>
+__global__ __launch_bounds__(256) void k_pyr_down(const T *__restrict__ src, int w, int h,
+                                                  float *__restrict__ dst, int dw, int dh,
+                                                  DevState *st) {
+  if (st != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 &&
+      threadIdx.y == 0)
+    frame_begin(st);
+  const int x = blockIdx.x * blockDim.x + threadIdx.x;
+  const int y = blockIdx.y * blockDim.y + threadIdx.y;
+  if (x >= dw || y >= dh) return;
+  const float k0 = 0.0625f, k1 = 0.25f, k2 = 0.375f, k3 = 0.25f, k4 = 0.0625f;
+  const int sy = 2 * y;
+  const size_t r0 = (size_t)reflect101(sy - 2, h) * w, r1 = (size_t)reflect101(sy - 1, h) * w,
+               r2 = (size_t)reflect101(sy, h) * w, r3 = (size_t)reflect101(sy + 1, h) * w,
+               r4 = (size_t)reflect101(sy + 2, h) * w;
+  float col[5];
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {
+    const int cx = reflect101(2 * x + j - 2, w);
+    float s = k0 * (float)src[r0 + cx];
+    s = s + k1 * (float)src[r1 + cx];
+    s = s + k2 * (float)src[r2 + cx];
+    s = s + k3 * (float)src[r3 + cx];
+    s = s + k4 * (float)src[r4 + cx];
+    col[j] = s;
+  }
+  float s = k0 * col[0];
+  s = s + k1 * col[1];
+  s = s + k2 * col[2];
+  s = s + k3 * col[3];
+  s = s + k4 * col[4];
+  dst[(size_t)y * dw + x] = s;
+}
+
+struct BilatArgs {
+  LevelTiles t;
+  const float *raw[kMaxLevels];
+  const uint16_t *raw0_u16;
+  float *d[kMaxLevels];
+  float *v[kMaxLevels];
+  int ksz;
+  float s_half, c_half;
+  float max_dist;
+};
+
+// cv::cuda::bilateralFilter (kinectfusion.cpp:57-65, A1 D: out of place) +
+// kernal_depthTruncation (image_process.cu:8-17) + kernel_getVertexmap
+// (image_process.cu:29-43), fused, all levels in one launch.  Level 0 also
+// reduces the frame's max depth (conservative integrate bound).
+__global__ __launch_bounds__(256) void k_bilateral_vertex(BilatArgs a, DevState *st) {
+  const int l = find_level(a.t, blockIdx.x);
+  const int local = blockIdx.x - a.t.off[l];
+  const LevelGeom g = a.t.g[l];
+  const int x = (local % a.t.nbx[l]) * 16 + (threadIdx.x & 15);
+  const int y = (local / a.t.nbx[l]) * 16 + (threadIdx.x >> 4);
+  float dval = 0.f;
+  const bool in = x < g.w && y < g.h;
+  if (in) {
+    const float *src = a.raw[l];
+    const uint16_t *src16 = (l == 0) ? a.raw0_u16 : nullptr;
+    auto rd = [&](size_t i) -> float { return src16 ? (float)src16[i] : src[i]; };
+    const float center = rd((size_t)y * g.w + x);
+    const int r = a.ksz / 2;
+    const float r2 = (float)(r * r);
+    float sum1 = 0.f, sum2 = 0.f;
+    for (int cy = y - r; cy < y - r + a.ksz; ++cy) {
+      const size_t row = (size_t)reflect101(cy, g.h) * g.w;
+      for (int cx = x - r; cx < x - r + a.ksz; ++cx) {
+        const float space2 = (float)((x - cx) * (x - cx) + (y - cy) * (y - cy));
+        if (space2 > r2) continue;
+        const float vv = rd(row + reflect101(cx, g.w));
+        const float dd = fabsf(vv - center);
+        const float wgt = det_expf(space2 * a.s_half + (dd * dd) * a.c_half);
+        sum1 = sum1 + wgt * vv;
+        sum2 = sum2 + wgt;
+      }
+    }
+    dval = sum1 / sum2;
+    dval *= 0.001f;
+    if (dval > a.max_dist) dval = 0.f;
+    const size_t i = (size_t)y * g.w + x;
+    a.d[l][i] = dval;
+    f3 vtx;
+    if (isnan(dval))
+      vtx = {0.f, 0.f, 0.f};
+    else
+      vtx = {(dval * ((float)x - g.cx)) / g.fx, (dval * ((float)y - g.cy)) / g.fy, dval};
+    st3(a.v[l], i, vtx);
+  }
+  if (l == 0) {  // block-uniform
+    unsigned m = (in && dval > 0.f) ? __float_as_uint(dval) : 0u;
+    for (int o = 32; o > 0; o >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, o));
+    __shared__ unsigned wm[4];
+    if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned b = max(max(wm[0], wm[1]), max(wm[2], wm[3]));
+      if (b) atomicMax(&st->dmax_bits[blockIdx.x % kDmaxShards], b);
+    }
+  }
+}
+
+struct NormalArgs {
+  LevelTiles t;
+  const float *v[kMaxLevels];
+  float *n[kMaxLevels];
+};
+
+// kernel_getNormalmap (image_process.cu:57-84), all levels; border written 0
+// (the value Frame::reset leaves there, types.hpp:53-62).
+__global__ __launch_bounds__(256) void k_normals(NormalArgs a) {
+  const int l = find_level(a.t, blockIdx.x);
+  const int local = blockIdx.x - a.t.off[l];
+  const LevelGeom g = a.t.g[l];
+  const int x = (local % a.t.nbx[l]) * 16 + (threadIdx.x & 15);
+  const int y = (local / a.t.nbx[l]) * 16 + (threadIdx.x >> 4);
+  if (x >= g.w || y >= g.h) return;
+  const float *vm = a.v[l];
+  const size_t i = (size_t)y * g.w + x;
+  if (x < 1 || x >= g.w - 1 || y < 1 || y >= g.h - 1) {
+    st3(a.n[l], i, {0.f, 0.f, 0.f});
+    return;
+  }
+  const f3 lf = ld3(vm, i - 1), rt = ld3(vm, i + 1), up = ld3(vm, i - g.w), dn = ld3(vm, i + g.w);
+  f3 n;
+  if (lf.z == 0 || rt.z == 0 || up.z == 0 || dn.z == 0) {
+    n = {0.f, 0.f, 0.f};
+  } else {
+    n = cross(sub(lf, rt), sub(up, dn));
+    if (n.z > 0) n = scl(n, -1.f);
+  }
+  st3(a.n[l], i, normalized(n));
+}
+
+// ---------------------------------------------------------------------------
+// ICP
+
+// ICP::findCoresp + kernel_rigidICP (rigid_icp.cu:46-113): per pixel of the
+// floor-covered region (A2), the 7-vector row and its 27 products, summed as
+// exact int64 fixed point (D), reduced per block through LDS.
+__global__ __launch_bounds__(256) void k_icp_acc(LevelGeom g, int xe, int npix,
+                                                 const float *__restrict__ cv,
+                                                 const float *__restrict__ cn,
+                                                 const float *__restrict__ pv,
+                                                 const float *__restrict__ pn, float dist_thr,
+                                                 float angle_thr, const DevState *__restrict__ st,
+                                                 long long *__restrict__ partials, int force) {
+  if (!force && (st->mode != MODE_TRACK || st->icp_fail)) return;
+  const DevPose P = st->icp_pose;
+  const f3 t = {P.t[0], P.t[1], P.t[2]};
+  long long acc[27];
+#pragma unroll
+  for (int k = 0; k < 27; ++k) acc[k] = 0;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < npix; i += gridDim.x * 256) {
+    const int x = i % xe, y = i / xe;
+    const size_t idx = (size_t)y * g.w + x;
+    const f3 n0 = ld3(cn, idx);
+    if (isnan(n0.x)) continue;
+    const f3 vcur = add(rmul(P.R, ld3(cv, idx)), t);
+    const int px = f2i_rn((vcur.x / vcur.z) * g.fx + g.cx);
+    const int py = f2i_rn((vcur.y / vcur.z) * g.fy + g.cy);
+    if (!(vcur.z > 0 && px >= 0 && py >= 0 && px < g.w && py < g.h)) continue;
+    const size_t j = (size_t)py * g.w + px;
+    const f3 vpre = ld3(pv, j);
+    const f3 dd = sub(vcur, vpre);
+    const float dist = sqrtf(dot(dd, dd));
+    if (!(dist <= dist_thr)) continue;
+    const f3 ncur = rmul(P.R, n0);
+    const f3 npre = ld3(pn, j);
+    const f3 sa = cross(ncur, npre);
+    const float sine = sqrtf(dot(sa, sa));
+    if (!(sine <= angle_thr)) continue;
+    const f3 c = cross(vcur, npre);
+    const float row[7] = {c.x, c.y, c.z, npre.x, npre.y, npre.z, dot(npre, sub(vpre, vcur))};
+    int s = 0;
+#pragma unroll
+    for (int a = 0; a < 6; ++a)
+#pragma unroll
+      for (int b = a; b < 7; ++b) {
+        const float prod = row[a] * row[b];
+        acc[s++] += (long long)rintf(prod * kFix);
+      }
+  }
+  __shared__ long long red[27 * 256];
+#pragma unroll
+  for (int k = 0; k < 27; ++k) red[k * 256 + threadIdx.x] = acc[k];
+  __syncthreads();
+  __shared__ long long red2[8 * 27];
+  if (threadIdx.x < 216) {
+    const int k = threadIdx.x % 27, seg = threadIdx.x / 27;
+    long long s = 0;
+    for (int q = 0; q < 32; ++q) s += red[k * 256 + seg * 32 + q];
+    red2[seg * 27 + k] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x < 27) {
+    long long s = 0;
+    for (int seg = 0; seg < 8; ++seg) s += red2[seg * 27 + threadIdx.x];
+    partials[(size_t)blockIdx.x * 27 + threadIdx.x] = s;
+  }
+}
+
+// icp_registration.cpp:33-42 on the device: A/b unpack (rigid_icp.cu:156-165),
+// LU det check, LU solve (D: instead of SVD), Rodrigues, pose = pose * Tinc.
+__device__ int icp_update(const long long *sums, DevPose &pose, double *xo) {
+  double A[6][6], b[6];
+  int s = 0;
+  for (int i = 0; i < 6; ++i)
+    for (int j = i; j < 7; ++j) {
+      const double v = (double)sums[s++] * (1.0 / 4294967296.0);
+      if (j == 6)
+        b[i] = v;
+      else
+        A[i][j] = A[j][i] = v;
+    }
+  int sign = 1;
+  for (int k = 0; k < 6; ++k) {
+    int p = k;
+    double best = fabs(A[k][k]);
+    for (int i = k + 1; i < 6; ++i)
+      if (fabs(A[i][k]) > best) {
+        best = fabs(A[i][k]);
+        p = i;
+      }
+    if (p != k) {
+      for (int j = 0; j < 6; ++j) {
+        const double tmp = A[k][j];
+        A[k][j] = A[p][j];
+        A[p][j] = tmp;
+      }
+      const double tb = b[k];
+      b[k] = b[p];
+      b[p] = tb;
+      sign = -sign;
+    }
+    if (A[k][k] != 0.0) {
+      for (int i = k + 1; i < 6; ++i) {
+        const double f = A[i][k] / A[k][k];
+        for (int j = k + 1; j < 6; ++j) A[i][j] = A[i][j] - f * A[k][j];
+        b[i] = b[i] - f * b[k];
+      }
+    }
+  }
+  double det = (double)sign;
+  for (int k = 0; k < 6; ++k) det = det * A[k][k];
+  if (fabs(det) < 1e-15 || isnan(det)) return 1;
+  double x[6];
+  for (int i = 5; i >= 0; --i) {
+    double acc = b[i];
+    for (int j = i + 1; j < 6; ++j) acc = acc - A[i][j] * x[j];
+    x[i] = acc / A[i][i];
+  }
+  for (int i = 0; i < 6; ++i) xo[i] = x[i];
+  const float rv[3] = {(float)x[0], (float)x[1], (float)x[2]};
+  DevPose inc;
+  inc.t[0] = (float)x[3];
+  inc.t[1] = (float)x[4];
+  inc.t[2] = (float)x[5];
+  const double theta =
+      sqrt((double)rv[0] * rv[0] + (double)rv[1] * rv[1] + (double)rv[2] * rv[2]);
+  if (theta < 2.220446049250313e-16) {
+    for (int i = 0; i < 9; ++i) inc.R[i] = (i % 4 == 0) ? 1.f : 0.f;
+  } else {
+    const double c = cos(theta), sn = sin(theta), c1 = 1.0 - c;
+    const double it = 1.0 / theta;
+    const float r[3] = {(float)(rv[0] * it), (float)(rv[1] * it), (float)(rv[2] * it)};
+    const float rrt[9] = {r[0] * r[0], r[0] * r[1], r[0] * r[2], r[0] * r[1], r[1] * r[1],
+                          r[1] * r[2], r[0] * r[2], r[1] * r[2], r[2] * r[2]};
+    const float rx[9] = {0.f, -r[2], r[1], r[2], 0.f, -r[0], -r[1], r[0], 0.f};
+    for (int i = 0; i < 9; ++i) {
+      const float e = (i % 4 == 0) ? 1.f : 0.f;
+      inc.R[i] = ((float)(c * e) + (float)(c1 * rrt[i])) + (float)(sn * rx[i]);
+    }
+  }
+  pose = pose_mul(pose, inc);
+  return 0;
+}
+
+__global__ __launch_bounds__(256) void k_icp_solve(DevState *st, const long long *partials,
+                                                   int nb, int force, int update) {
+  if (!force && (st->mode != MODE_TRACK || st->icp_fail)) return;
+  __shared__ long long red2[9 * 27];
+  if (threadIdx.x < 243) {
+    const int k = threadIdx.x % 27, seg = threadIdx.x / 27;
+    long long s = 0;
+    for (int b = seg; b < nb; b += 9) s += partials[(size_t)b * 27 + k];
+    red2[seg * 27 + k] = s;
+  }
+  __syncthreads();
+  __shared__ long long sums[27];
+  if (threadIdx.x < 27) {
+    long long s = 0;
+    for (int seg = 0; seg < 9; ++seg) s += red2[seg * 27 + threadIdx.x];
+    sums[threadIdx.x] = s;
+    st->sums[threadIdx.x] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && update) {
+    DevPose p = st->icp_pose;
+    double x[6];
+    if (icp_update(sums, p, x)) {
+      st->icp_fail = 1;
+    } else {
+      st->icp_pose = p;
+      for (int i = 0; i < 6; ++i) st->x[i] = x[i];
+    }
+  }
+}
+
+// kinectfusion.cpp:84-104 bookkeeping, single thread: frame-1 bootstrap,
+// tracking failure -> reset() semantics, pose_record push, derived poses for
+// integrate (tsdf_volume.cpp:50) and raycast (tsdf_volume.cpp:59-61).
+__global__ void k_commit(DevState *st, DevPose *log, DevPose vpose) {
+  const int mode = st->mode;
+  if (mode == MODE_BOOT) {
+    const DevPose back = log[st->n_poses - 1];
+    st->vol2cam = pose_mul(pose_inv(back), vpose);
+    st->frame_count += 1;
+  } else if (mode == MODE_TRACK) {
+    if (st->icp_fail) {
+      st->mode = MODE_FAIL;
+      st->frame_count = 1;
+      st->n_poses = 1;
+      log[0] = pose_identity();
+    } else {
+      const DevPose g = pose_mul(log[st->n_poses - 1], st->icp_pose);
+      if (st->n_poses < st->pose_cap) {
+        log[st->n_poses] = g;
+        st->n_poses += 1;
+      } else {
+        log[st->pose_cap - 1] = g;
+        st->pose_overflow = 1;
+      }
+      st->vol2cam = pose_mul(pose_inv(g), vpose);
+      const DevPose c2v = pose_mul(pose_inv(vpose), g);
+      st->cam2vol = c2v;
+      for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) st->Rinv[3 * i + j] = c2v.R[3 * j + i];
+      st->frame_count += 1;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// TSDF integrate — tsdfhelper::operator() (tsdf_volume.cu:41-99).
+//
+// One wave = one 8x8 tile of (x,y) columns; a lane sweeps its column in z with
+// vc accumulated by repeated float adds exactly as the reference (so the
+// projected pixel of every voxel is bit-identical).  A conservative z interval
+// per column (frustum + max depth, computed in double with margins) skips the
+// projection work outside it; the adds are still replayed there.
+
+// Solve alpha + beta*z >= 0 into [lo, hi].
+__device__ __forceinline__ void clip_lin(double alpha, double beta, double &lo, double &hi) {
+  if (beta > 0.0) {
+    lo = fmax(lo, -alpha / beta);
+  } else if (beta < 0.0) {
+    hi = fmin(hi, -alpha / beta);
+  } else if (alpha < 0.0) {
+    hi = -1.0;
+  }
+}
+
+// kCount: count-only variant (no voxel traffic) giving N_upd / N_col, the
+// algorithmic-byte inputs of the roofline.
+template <bool kCount>
+__global__ __launch_bounds__(256) void k_integrate(VolView v, LevelGeom g,
+                                                   const float *__restrict__ dmap,
+                                                   const uint8_t *__restrict__ bgr,
+                                                   const float *__restrict__ invl,
+                                                   const DevState *__restrict__ st,
+                                                   unsigned long long *counters) {
+  const int lane = threadIdx.x & 63;
+  const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (tile >= v.tiles_x * v.tiles_y) return;
+  const int x = (tile % v.tiles_x) * 8 + (lane & 7);
+  const int y = (tile / v.tiles_x) * 8 + (lane >> 3);
+  const size_t base = (size_t)tile * 64 + lane;
+  const int mode = st->mode;
+  if (mode == MODE_FAIL) {  // reset(): whole volume zeroed (A5 D)
+    if (kCount) return;
+    for (int z = 0; z < v.Z; ++z) {
+      const size_t i = base + (size_t)z * v.slice;
+      v.tsdf[i] = 0;
+      v.weight[i] = 0;
+      v.rgb[i] = 0u;
+    }
+    return;
+  }
+  const DevPose P = st->vol2cam;
+  const f3 vx = {(float)x * v.vs[0], (float)y * v.vs[1], 0.f * v.vs[2]};
+  f3 vc = add(rmul(P.R, vx), {P.t[0], P.t[1], P.t[2]});
+  const f3 zs = {P.R[2] * v.vs[0], P.R[5] * v.vs[0], P.R[8] * v.vs[0]};
+
+  // conservative interval [zlo, zhi] of z where any check can pass
+  unsigned dm = 0u;
+#pragma unroll
+  for (int i = 0; i < kDmaxShards; ++i) dm = max(dm, st->dmax_bits[i]);
+  const float dmax = __uint_as_float(dm);
+  double lo = 1.0, hi = (double)(v.Z - 1);
+  {
+    const double ax = vc.x, ay = vc.y, az = vc.z, sx = zs.x, sy = zs.y, sz = zs.z;
+    const double M = 2.0;  // pixels
+    clip_lin(az + 1e-3, sz, lo, hi);  // vc.z > 0
+    const double cxl = (double)g.cx + 0.5 + M, cxh = (double)g.w - 0.5 + M - (double)g.cx;
+    const double cyl = (double)g.cy + 0.5 + M, cyh = (double)g.h - 0.5 + M - (double)g.cy;
+    clip_lin(g.fx * ax + cxl * az, g.fx * sx + cxl * sz, lo, hi);
+    clip_lin(cxh * az - g.fx * ax, cxh * sz - g.fx * sx, lo, hi);
+    clip_lin(g.fy * ay + cyl * az, g.fy * sy + cyl * sz, lo, hi);
+    clip_lin(cyh * az - g.fy * ay, cyh * sz - g.fy * sy, lo, hi);
+    const double zfar = ((double)dmax + (double)v.trunc) * 1.02 + 0.01;
+    clip_lin(zfar - az, -sz, lo, hi);
+  }
+  if (!(hi >= lo)) return;
+  const int zlo = max(1, (int)floor(lo) - 2);
+  const int zhi = min(v.Z - 1, (int)ceil(hi) + 2);
+  if (zhi < zlo) return;
+
+  const float trunc = v.trunc;
+  const float thres_color = trunc / 2;
+  unsigned cu = 0, cc = 0;
+  int z = 1;
+  for (; z < zlo; ++z) vc = add(vc, zs);
+  for (; z <= zhi; ++z) {
+    vc = add(vc, zs);
+    if (vc.z <= 0) continue;
+    const int u = f2i_rn((vc.x / vc.z) * g.fx + g.cx);
+    const int vv = f2i_rn((vc.y / vc.z) * g.fy + g.cy);
+    if (u < 0 || u >= g.w || vv < 0 || vv >= g.h) continue;
+    const size_t pix = (size_t)vv * g.w + u;
+    const float depth = dmap[pix];
+    if (depth <= 0) continue;
+    const float sdf = -(invl[pix] * sqrtf(dot(vc, vc)) - depth);
+    if (sdf >= -trunc) {
+      const size_t i = base + (size_t)z * v.slice;
+      if (kCount) {
+        ++cu;
+        if (sdf <= thres_color && sdf >= -thres_color) ++cc;
+        continue;
+      }
+      const float ts = fminf(1.f, sdf / trunc);
+      const int16_t t0 = v.tsdf[i];
+      const int pre_w = v.weight[i];
+      const float pre_t = (float)t0 * kDivShortMax;
+      const int new_w = min(pre_w + 1, kMaxWeight);
+      const float new_t = fmaf(pre_t, (float)pre_w, ts) / (float)(pre_w + 1);
+      int q = (int)(new_t * (float)kShortMax);
+      q = max(-kShortMax, min(kShortMax, q));
+      v.tsdf[i] = (int16_t)q;
+      v.weight[i] = (int16_t)new_w;
+      if (sdf <= thres_color && sdf >= -thres_color) {
+        const uint32_t mc = v.rgb[i];
+        const uint8_t *px = bgr + 3 * pix;
+        const float c = (float)(new_w + 1);
+        uint32_t out = 0u;
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) {
+          const int m0 = (int)((mc >> (8 * ch)) & 0xffu);
+          const float m = (float)(new_w * m0 + (int)px[ch]);
+          out |= (uint32_t)(uint8_t)(m / c) << (8 * ch);
+        }
+        v.rgb[i] = out;
+      }
+    }
+  }
+  if (kCount) {
+    const int sh = blockIdx.x % 16;
+    atomicAdd(&counters[2 * sh], (unsigned long long)cu);
+    atomicAdd(&counters[2 * sh + 1], (unsigned long long)cc);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Raycast — raycasthelper (tsdf_volume.cu:120-260)
+
+struct RayConsts {
+  f3 vs, vs_inv, gd;
+  float step;
+};
+
+__device__ __forceinline__ float voxel2tsdf(const VolView &v, const RayConsts &rc, f3 p) {
+  const int x = f2i_rn(p.x * rc.vs_inv.x);
+  const int y = f2i_rn(p.y * rc.vs_inv.y);
+  const int z = f2i_rn(p.z * rc.vs_inv.z);
+  if (x >= v.X - 1 || y >= v.Y - 1 || z >= v.Z - 1 || x < 1 || y < 1 || z < 1) return NAN;
+  return (float)v.tsdf[vox_index(v, x, y, z)] * kDivShortMax;
+}
+
+__device__ __forceinline__ float interp(const VolView &v, f3 cf) {
+  const int gx = f2i_rd(cf.x), gy = f2i_rd(cf.y), gz = f2i_rd(cf.z);
+  if (gx < 0 || gx >= v.X - 1 || gy < 0 || gy >= v.Y - 1 || gz < 0 || gz >= v.Z - 1) return NAN;
+  const float a = cf.x - (float)gx, b = cf.y - (float)gy, c = cf.z - (float)gz;
+  const float t000 = (float)v.tsdf[vox_index(v, gx, gy, gz)] * kDivShortMax;
+  const float t001 = (float)v.tsdf[vox_index(v, gx, gy, gz + 1)] * kDivShortMax;
+  const float t010 = (float)v.tsdf[vox_index(v, gx, gy + 1, gz)] * kDivShortMax;
+  const float t011 = (float)v.tsdf[vox_index(v, gx, gy + 1, gz + 1)] * kDivShortMax;
+  const float t100 = (float)v.tsdf[vox_index(v, gx + 1, gy, gz)] * kDivShortMax;
+  const float t101 = (float)v.tsdf[vox_index(v, gx + 1, gy, gz + 1)] * kDivShortMax;
+  const float t110 = (float)v.tsdf[vox_index(v, gx + 1, gy + 1, gz)] * kDivShortMax;
+  const float t111 = (float)v.tsdf[vox_index(v, gx + 1, gy + 1, gz + 1)] * kDivShortMax;
+  float s = 0.f;
+  s += t000 * (1 - a) * (1 - b) * (1 - c);
+  s += t001 * (1 - a) * (1 - b) * c;
+  s += t010 * (1 - a) * b * (1 - c);
+  s += t011 * (1 - a) * b * c;
+  s += t100 * a * (1 - b) * (1 - c);
+  s += t101 * a * (1 - b) * c;
+  s += t110 * a * b * (1 - c);
+  s += t111 * a * b * c;
+  return s;
+}
+
+__device__ f3 compute_normal(const VolView &v, const RayConsts &rc, f3 p) {
+  f3 n;
+  const float fx1 = interp(v, mulc({p.x + rc.gd.x, p.y, p.z}, rc.vs_inv));
+  const float fx2 = interp(v, mulc({p.x - rc.gd.x, p.y, p.z}, rc.vs_inv));
+  n.x = (fx1 - fx2) / rc.gd.x;
+  const float fy1 = interp(v, mulc({p.x, p.y + rc.gd.y, p.z}, rc.vs_inv));
+  const float fy2 = interp(v, mulc({p.x, p.y - rc.gd.y, p.z}, rc.vs_inv));
+  n.y = (fy1 - fy2) / rc.gd.y;
+  const float fz1 = interp(v, mulc({p.x, p.y, p.z + rc.gd.z}, rc.vs_inv));
+  const float fz2 = interp(v, mulc({p.x, p.y, p.z - rc.gd.z}, rc.vs_inv));
+  n.z = (fz1 - fz2) / rc.gd.z;
+  return normalized(n);
+}
+
+// One wave = an 8x8 pixel tile (rays of a wave sample neighbouring voxels).
+// BOOT frames copy the measured level-0 maps instead (kinectfusion.cpp:88-89).
+__global__ __launch_bounds__(256) void k_raycast(VolView v, LevelGeom g, RayConsts rc,
+                                                 FrameView cur, FrameView prev,
+                                                 const DevState *__restrict__ st) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int x = blockIdx.x * 16 + (wv & 1) * 8 + (lane & 7);
+  const int y = blockIdx.y * 16 + (wv >> 1) * 8 + (lane >> 3);
+  if (x >= g.w || y >= g.h) return;
+  const size_t o = (size_t)y * g.w + x;
+  const int mode = st->mode;
+  if (mode == MODE_BOOT) {
+    st3(prev.v[0], o, ld3(cur.v[0], o));
+    st3(prev.n[0], o, ld3(cur.n[0], o));
+    return;
+  }
+  f3 vout = {0.f, 0.f, 0.f}, nout = {0.f, 0.f, 0.f};
+  if (mode == MODE_TRACK) {
+    const DevPose P = st->cam2vol;
+    const f3 org = {P.t[0], P.t[1], P.t[2]};
+    const f3 pp = {(1.f * ((float)x - g.cx)) / g.fx, (1.f * ((float)y - g.cy)) / g.fy, 1.f};
+    const f3 dir = normalized(rmul(P.R, pp));
+    const f3 invR = {1.f / dir.x, 1.f / dir.y, 1.f / dir.z};
+    const f3 tbot = mulc(invR, sub({0.f, 0.f, 0.f}, org));
+    const f3 ttop = mulc(invR, sub({v.range[0], v.range[1], v.range[2]}, org));
+    const f3 tmin = {fminf(ttop.x, tbot.x), fminf(ttop.y, tbot.y), fminf(ttop.z, tbot.z)};
+    const f3 tmax = {fmaxf(ttop.x, tbot.x), fmaxf(ttop.y, tbot.y), fmaxf(ttop.z, tbot.z)};
+    const float tnear = fmaxf(fmaxf(tmin.x, tmin.y), fmaxf(tmin.x, tmin.z));
+    const float tfar = fminf(fminf(tmax.x, tmax.y), fminf(tmax.x, tmax.z));
+    float ray_len = fmaxf(tnear, 0.f);
+    if (ray_len < tfar) {
+      const f3 vstep = mulc(dir, rc.vs);
+      ray_len += rc.step;
+      f3 nextp = add(org, scl(dir, ray_len));
+      float tn = voxel2tsdf(v, rc, nextp);
+      for (; ray_len < tfar; ray_len += rc.step) {
+        nextp = add(nextp, vstep);
+        const float tcur = tn;
+        tn = voxel2tsdf(v, rc, nextp);
+        if (isnan(tn)) continue;
+        if (tcur < 0.f && tn > 0.f) break;
+        if (tcur > 0.f && tn < 0.f) {
+          const float Ts = ray_len - (v.vs[0] * tcur) / (tcur - tn);  // A3 (R)
+          const f3 vertex = add(org, scl(dir, Ts));
+          const f3 n = compute_normal(v, rc, vertex);
+          if (!isnan(n.x * n.y * n.z)) {
+            nout = rmul(st->Rinv, n);
+            vout = rmul(st->Rinv, sub(vertex, org));
+            break;
+          }
+        }
+      }
+    }
+  }
+  st3(prev.v[0], o, vout);
+  st3(prev.n[0], o, nout);
+}
+
+// kernel_resizePointsNormals (image_process.cu:95-125) for every level >= 1 in
+// one launch: a block owns a 16x16 tile of level 1 and the 8x8 / 4x4 tiles of
+// levels 2 / 3 under it, passing values through LDS (same float ops).
+__device__ __forceinline__ void resize_one(f3 d00, f3 d01, f3 d10, f3 d11, f3 n00, f3 n01,
+                                           f3 n10, f3 n11, f3 &vo, f3 &no) {
+  vo = {0.f, 0.f, 0.f};
+  no = {0.f, 0.f, 0.f};
+  if (!isnan(d00.x * d01.x * d10.x * d11.x)) {
+    vo = scl(add(add(add(d00, d01), d10), d11), 0.25f);
+    no = scl(add(add(add(n00, n01), n10), n11), 0.25f);
+  }
+}
+
+struct ResizeArgs {
+  LevelGeom g[kMaxLevels];
+  int levels;
+};
+
+__global__ __launch_bounds__(256) void k_resize(ResizeArgs a, FrameView cur, FrameView prev,
+                                                const DevState *__restrict__ st) {
+  if (a.levels < 2) return;
+  const int mode = st->mode;
+  __shared__ f3 sv[2][16 * 16], sn[2][16 * 16];
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  int side = 16;
+  for (int l = 1; l < a.levels; ++l) {
+    const LevelGeom g = a.g[l];
+    const int X = blockIdx.x * side + tx, Y = blockIdx.y * side + ty;
+    const bool act = tx < side && ty < side && X < g.w && Y < g.h;
+    f3 vo = {0.f, 0.f, 0.f}, no = {0.f, 0.f, 0.f};
+    if (act) {
+      const size_t o = (size_t)Y * g.w + X;
+      if (mode == MODE_BOOT) {
+        vo = ld3(cur.v[l], o);
+        no = ld3(cur.n[l], o);
+      } else if (mode == MODE_TRACK) {
+        f3 d[4], n[4];
+        if (l == 1) {
+          const int wb = a.g[0].w;
+          const size_t i00 = (size_t)(2 * Y) * wb + 2 * X;
+          const size_t ii[4] = {i00, i00 + 1, i00 + wb, i00 + wb + 1};
+          for (int q = 0; q < 4; ++q) {
+            d[q] = ld3(prev.v[0], ii[q]);
+            n[q] = ld3(prev.n[0], ii[q]);
+          }
+        } else {
+          const int pb = (l - 1) & 1;
+          const int ps = side * 2;
+          const int i00 = (2 * ty) * ps + 2 * tx;
+          const int ii[4] = {i00, i00 + 1, i00 + ps, i00 + ps + 1};
+          for (int q = 0; q < 4; ++q) {
+            d[q] = sv[pb][ii[q]];
+            n[q] = sn[pb][ii[q]];
+          }
+        }
+        resize_one(d[0], d[1], d[2], d[3], n[0], n[1], n[2], n[3], vo, no);
+      }
+      st3(prev.v[l], o, vo);
+      st3(prev.n[l], o, no);
+    }
+    __syncthreads();
+    if (tx < side && ty < side) {
+      sv[l & 1][ty * side + tx] = vo;
+      sn[l & 1][ty * side + tx] = no;
+    }
+    __syncthreads();
+    side >>= 1;
+  }
+}
+
+__global__ void k_inv_lambda(LevelGeom g, float *out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= g.w * g.h) return;
+  const int u = i % g.w, vv = i / g.w;
+  const f3 xyl = {(1.f * ((float)u - g.cx)) / g.fx, (1.f * ((float)vv - g.cy)) / g.fy, 1.f};
+  const float lambda = sqrtf(dot(xyl, xyl));
+  out[i] = 1.f / lambda;
+}
+
+// Reference 8-byte record {int16 tsdf, int16 weight, u8 c0,c1,c2, pad}
+// (device_types.hpp:51-56), x-fastest linear order, for slices [z0, z0+nz).
+__global__ void k_export_records(VolView v, int z0, int nz, uint64_t *dst) {
+  const size_t n = v.slice * (size_t)nz;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const int x = (int)(i % v.X);
+    const int y = (int)((i / v.X) % v.Y);
+    const int z = z0 + (int)(i / v.slice);
+    const size_t s = vox_index(v, x, y, z);
+    const uint64_t rec = (uint64_t)(uint16_t)v.tsdf[s] | ((uint64_t)(uint16_t)v.weight[s] << 16) |
+                         ((uint64_t)(v.rgb[s] & 0xffffffu) << 32);
+    dst[i] = rec;
+  }
+}
+
+__global__ void k_import_records(VolView v, int z0, int nz, const uint64_t *src) {
+  const size_t n = v.slice * (size_t)nz;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const int x = (int)(i % v.X);
+    const int y = (int)((i / v.X) % v.Y);
+    const int z = z0 + (int)(i / v.slice);
+    const size_t s = vox_index(v, x, y, z);
+    const uint64_t rec = src[i];
+    v.tsdf[s] = (int16_t)(rec & 0xffffu);
+    v.weight[s] = (int16_t)((rec >> 16) & 0xffffu);
+    v.rgb[s] = (uint32_t)((rec >> 32) & 0xffffffu);
+  }
+}
+
+__global__ void k_export_soa(VolView v, int z0, int nz, int16_t *t, int16_t *w, uint32_t *c) {
+  const size_t n = v.slice * (size_t)nz;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const int x = (int)(i % v.X);
+    const int y = (int)((i / v.X) % v.Y);
+    const int z = z0 + (int)(i / v.slice);
+    const size_t s = vox_index(v, x, y, z);
+    if (t) t[i] = v.tsdf[s];
+    if (w) w[i] = v.weight[s];
+    if (c) c[i] = v.rgb[s];
+  }
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// launchers
+
+void launch_frame_begin(hipStream_t s, DevState *st) {
+  hipLaunchKernelGGL(k_frame_begin, dim3(1), dim3(1), 0, s, st);
+}
+
+void launch_pyr_down(hipStream_t s, const float *src, const uint16_t *src16, int w, int h,
+                     float *dst, DevState *st_begin) {
+  const int dw = (w + 1) / 2, dh = (h + 1) / 2;
+  dim3 blk(64, 4), grd((dw + 63) / 64, (dh + 3) / 4);
+  if (src16)
+    hipLaunchKernelGGL(k_pyr_down<uint16_t>, grd, blk, 0, s, src16, w, h, dst, dw, dh, st_begin);
+  else
+    hipLaunchKernelGGL(k_pyr_down<float>, grd, blk, 0, s, src, w, h, dst, dw, dh, st_begin);
+}
+
+void launch_bilateral_vertex(hipStream_t s, int levels, const float *const raw[kMaxLevels],
+                             const uint16_t *raw0_u16, const LevelGeom *g, FrameView cur,
+                             int ksz, float sigma_color, float sigma_spatial, float max_dist,
+                             DevState *st) {
+  BilatArgs a{};
+  a.t = make_tiles(levels, g);
+  for (int l = 0; l < levels; ++l) {
+    a.raw[l] = raw[l];
+    a.d[l] = cur.d[l];
+    a.v[l] = cur.v[l];
+  }
+  a.raw0_u16 = raw0_u16;
+  a.ksz = ksz;
+  a.s_half = -0.5f / (sigma_spatial * sigma_spatial);
+  a.c_half = -0.5f / (sigma_color * sigma_color);
+  a.max_dist = max_dist;
+  hipLaunchKernelGGL(k_bilateral_vertex, dim3(a.t.off[levels]), dim3(256), 0, s, a, st);
+}
+
+void launch_normals(hipStream_t s, int levels, const LevelGeom *g, FrameView cur) {
+  NormalArgs a{};
+  a.t = make_tiles(levels, g);
+  for (int l = 0; l < levels; ++l) {
+    a.v[l] = cur.v[l];
+    a.n[l] = cur.n[l];
+  }
+  hipLaunchKernelGGL(k_normals, dim3(a.t.off[levels]), dim3(256), 0, s, a);
+}
+
+static int icp_npix(const LevelGeom &g, int *xe) {
+  *xe = (g.w / 32) * 32;  // A2: grid = floor(W/32) x floor(H/32) blocks of 32x32
+  return *xe * ((g.h / 32) * 32);
+}
+
+int icp_blocks(const LevelGeom &g) {
+  int xe;
+  const int n = icp_npix(g, &xe);
+  int nb = (n + 1023) / 1024;
+  return nb < 1 ? 1 : nb;
+}
+
+void launch_icp_acc(hipStream_t s, const LevelGeom &g, const float *cv, const float *cn,
+                    const float *pv, const float *pn, float dist_thr, float angle_thr,
+                    DevState *st, long long *partials, int force) {
+  int xe;
+  const int n = icp_npix(g, &xe);
+  hipLaunchKernelGGL(k_icp_acc, dim3(icp_blocks(g)), dim3(256), 0, s, g, xe, n, cv, cn, pv, pn,
+                     dist_thr, angle_thr, st, partials, force);
+}
+
+void launch_icp_solve(hipStream_t s, DevState *st, const long long *partials, int nblocks,
+                      int force_mode, int update) {
+  hipLaunchKernelGGL(k_icp_solve, dim3(1), dim3(256), 0, s, st, partials, nblocks, force_mode,
+                     update);
+}
+
+void launch_commit(hipStream_t s, DevState *st, DevPose *pose_log, DevPose volume_pose) {
+  hipLaunchKernelGGL(k_commit, dim3(1), dim3(1), 0, s, st, pose_log, volume_pose);
+}
+
+void launch_integrate(hipStream_t s, VolView v, LevelGeom g0, const float *dmap,
+                      const uint8_t *bgr, const float *inv_lambda, const DevState *st,
+                      unsigned long long *counters) {
+  const int tiles = v.tiles_x * v.tiles_y;
+  dim3 grd((tiles + 3) / 4);
+  if (counters)
+    hipLaunchKernelGGL(k_integrate<true>, grd, dim3(256), 0, s, v, g0, dmap, bgr, inv_lambda, st,
+                       counters);
+  else
+    hipLaunchKernelGGL(k_integrate<false>, grd, dim3(256), 0, s, v, g0, dmap, bgr, inv_lambda, st,
+                       counters);
+}
+
+void launch_raycast(hipStream_t s, VolView v, LevelGeom g0, FrameView cur, FrameView prev,
+                    const DevState *st) {
+  RayConsts rc;
+  rc.vs = {v.vs[0], v.vs[1], v.vs[2]};
+  rc.vs_inv = {1.f / v.vs[0], 1.f / v.vs[1], 1.f / v.vs[2]};
+  rc.gd = {v.vs[0] * 0.5f, v.vs[1] * 0.5f, v.vs[2] * 0.5f};
+  rc.step = v.vs[0];
+  dim3 grd((g0.w + 15) / 16, (g0.h + 15) / 16);
+  hipLaunchKernelGGL(k_raycast, grd, dim3(256), 0, s, v, g0, rc, cur, prev, st);
+}
+
+void launch_resize(hipStream_t s, int levels, const LevelGeom *g, FrameView cur, FrameView prev,
+                   const DevState *st) {
+  if (levels < 2) return;
+  ResizeArgs a{};
+  a.levels = levels;
+  for (int l = 0; l < levels; ++l) a.g[l] = g[l];
+  dim3 grd((g[1].w + 15) / 16, (g[1].h + 15) / 16);
+  hipLaunchKernelGGL(k_resize, grd, dim3(256), 0, s, a, cur, prev, st);
+}
+
+void launch_inv_lambda(hipStream_t s, LevelGeom g0, float *inv_lambda) {
+  const int n = g0.w * g0.h;
+  hipLaunchKernelGGL(k_inv_lambda, dim3((n + 255) / 256), dim3(256), 0, s, g0, inv_lambda);
+}
+
+static dim3 slab_grid(const VolView &v, int nz) {
+  const size_t n = v.slice * (size_t)nz;
+  size_t b = (n + 255) / 256;
+  if (b > 8192) b = 8192;
+  return dim3((unsigned)b);
+}
+
+void launch_export_records(hipStream_t s, VolView v, int z0, int nz, uint64_t *dst) {
+  hipLaunchKernelGGL(k_export_records, slab_grid(v, nz), dim3(256), 0, s, v, z0, nz, dst);
+}
+void launch_import_records(hipStream_t s, VolView v, int z0, int nz, const uint64_t *src) {
+  hipLaunchKernelGGL(k_import_records, slab_grid(v, nz), dim3(256), 0, s, v, z0, nz, src);
+}
+void launch_export_soa(hipStream_t s, VolView v, int z0, int nz, int16_t *t, int16_t *w,
+                       uint32_t *c) {
+  hipLaunchKernelGGL(k_export_soa, slab_grid(v, nz), dim3(256), 0, s, v, z0, nz, t, w, c);
+}
+
+}  // namespace kfx

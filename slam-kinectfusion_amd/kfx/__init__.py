@@ -1,0 +1,256 @@
+"""kfx — Python binding of libkfx.so (the MI355X KinectFusion hot path).
+
+`KinectFusion` mirrors the reference's `kf::kinectfusion` (kinectfusion.h:31-73):
+pipeline(color, depth) / reset() / getCurCameraPose() / pose_record /
+frame_count, plus the stage seams of include/kfx.h used by the parity tests.
+
+There is no CPU fallback: constructing a KinectFusion without the HIP library or
+without a GPU raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+from .abi import (KFX_FRAME_CUR, KFX_FRAME_PREV, KFX_OK, KFX_TRACKING_LOST, Intrinsics, Params, Pose,
+                  default_params, fptr, i16ptr, i64ptr, u8ptr, u16ptr)
+
+__all__ = ["KinectFusion", "KfxError", "lib", "build", "LIB_PATH", "Intrinsics", "Params", "Pose",
+           "default_params", "KFX_FRAME_CUR", "KFX_FRAME_PREV", "KFX_OK", "KFX_TRACKING_LOST", "EXPORTS"]
+
+_PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(_PKG, "lib", "libkfx.so")
+
+# every symbol include/kfx.h declares
+EXPORTS = [
+    "kfx_abi_version", "kfx_last_error", "kfx_default_params", "kfx_create", "kfx_destroy", "kfx_reset",
+    "kfx_pipeline", "kfx_pipeline_u16", "kfx_stage_frames", "kfx_pipeline_staged", "kfx_synchronize",
+    "kfx_set_graph_mode", "kfx_get_cur_camera_pose", "kfx_get_frame_count", "kfx_get_pose_record",
+    "kfx_write_poses_txt", "kfx_get_frame_maps", "kfx_set_frame_maps", "kfx_download_tsdf",
+    "kfx_upload_tsdf", "kfx_download_volume_soa", "kfx_stage_preprocess", "kfx_stage_icp_accumulate",
+    "kfx_stage_icp", "kfx_stage_integrate", "kfx_stage_raycast", "kfx_set_profiling", "kfx_get_stage_ms",
+    "kfx_integrate_counts",
+]
+
+
+class KfxError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", _PKG], check=True)
+    return LIB_PATH
+
+
+def lib():
+    """Load libkfx.so (raises if it has not been built — no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise KfxError(f"{LIB_PATH} missing: run `make -C {_PKG}` (or __graft_entry__.build())")
+    L = C.CDLL(LIB_PATH)
+    P, i, f = C.POINTER, C.c_int, C.c_float
+    vp = C.c_void_p
+    sig = {
+        "kfx_abi_version": ([], i),
+        "kfx_last_error": ([], C.c_char_p),
+        "kfx_default_params": ([P(Params)], i),
+        "kfx_create": ([P(Intrinsics), P(Params), i, P(vp)], i),
+        "kfx_destroy": ([vp], i),
+        "kfx_reset": ([vp], i),
+        "kfx_pipeline": ([vp, P(C.c_uint8), P(f)], i),
+        "kfx_pipeline_u16": ([vp, P(C.c_uint8), P(C.c_uint16)], i),
+        "kfx_stage_frames": ([vp, i, P(C.c_uint8), P(f)], i),
+        "kfx_pipeline_staged": ([vp, i], i),
+        "kfx_synchronize": ([vp], i),
+        "kfx_set_graph_mode": ([vp, i], i),
+        "kfx_get_cur_camera_pose": ([vp, P(Pose)], i),
+        "kfx_get_frame_count": ([vp, P(i)], i),
+        "kfx_get_pose_record": ([vp, P(Pose), i, P(i)], i),
+        "kfx_write_poses_txt": ([vp, C.c_char_p], i),
+        "kfx_get_frame_maps": ([vp, i, i, P(f), P(f), P(f)], i),
+        "kfx_set_frame_maps": ([vp, i, i, P(f), P(f)], i),
+        "kfx_download_tsdf": ([vp, vp], i),
+        "kfx_upload_tsdf": ([vp, vp], i),
+        "kfx_download_volume_soa": ([vp, P(C.c_int16), P(C.c_int16), P(C.c_uint8)], i),
+        "kfx_stage_preprocess": ([vp, P(C.c_uint8), P(f)], i),
+        "kfx_stage_icp_accumulate": ([vp, i, P(Pose), P(C.c_int64)], i),
+        "kfx_stage_icp": ([vp, P(Pose)], i),
+        "kfx_stage_integrate": ([vp, P(Pose), P(C.c_int64), P(C.c_int64)], i),
+        "kfx_stage_raycast": ([vp, P(Pose), P(f)], i),
+        "kfx_set_profiling": ([vp, i], i),
+        "kfx_get_stage_ms": ([vp, P(f)], i),
+        "kfx_integrate_counts": ([vp, P(C.c_int64), P(C.c_int64)], i),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = res
+    _lib = L
+    return L
+
+
+def _check(rc: int, what: str, ok=(KFX_OK,)) -> int:
+    if rc not in ok:
+        raise KfxError(f"{what} failed ({rc}): {lib().kfx_last_error().decode(errors='replace')}")
+    return rc
+
+
+class KinectFusion:
+    """kf::kinectfusion over the C-ABI.  Images: depth (H,W) float32/uint16 mm,
+    colour (H,W,3) uint8 BGR."""
+
+    def __init__(self, intr, params: Params | None = None, device: int = 0):
+        self.intr = Intrinsics.from_any(intr)
+        self.params = params if params is not None else default_params()
+        h = C.c_void_p()
+        _check(lib().kfx_create(C.byref(self.intr), C.byref(self.params), device, C.byref(h)), "kfx_create")
+        self._h = h
+        X, Y, Z = (int(d) for d in self.params.volu_dims)
+        self.dims = (X, Y, Z)
+        self.nvox = X * Y * Z
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().kfx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # ---- kf::kinectfusion ------------------------------------------------
+    def pipeline(self, color: np.ndarray, depth: np.ndarray) -> int:
+        """Returns KFX_OK or KFX_TRACKING_LOST (reset applied, frame dropped)."""
+        color = np.ascontiguousarray(color, np.uint8)
+        if depth.dtype == np.uint16:
+            d = np.ascontiguousarray(depth)
+            rc = lib().kfx_pipeline_u16(self._h, u8ptr(color), u16ptr(d))
+        else:
+            d = np.ascontiguousarray(depth, np.float32)
+            rc = lib().kfx_pipeline(self._h, u8ptr(color), fptr(d))
+        return _check(rc, "kfx_pipeline", ok=(KFX_OK, KFX_TRACKING_LOST))
+
+    def reset(self):
+        _check(lib().kfx_reset(self._h), "kfx_reset")
+
+    def getCurCameraPose(self) -> np.ndarray:
+        p = Pose()
+        _check(lib().kfx_get_cur_camera_pose(self._h, C.byref(p)), "kfx_get_cur_camera_pose")
+        return p.matrix()
+
+    @property
+    def frame_count(self) -> int:
+        n = C.c_int()
+        _check(lib().kfx_get_frame_count(self._h, C.byref(n)), "kfx_get_frame_count")
+        return n.value
+
+    @property
+    def pose_record(self) -> np.ndarray:
+        n = C.c_int()
+        _check(lib().kfx_get_pose_record(self._h, None, 0, C.byref(n)), "kfx_get_pose_record")
+        buf = (Pose * max(n.value, 1))()
+        _check(lib().kfx_get_pose_record(self._h, buf, n.value, C.byref(n)), "kfx_get_pose_record")
+        return np.stack([buf[i].matrix() for i in range(n.value)])
+
+    def write_poses_txt(self, path: str):
+        _check(lib().kfx_write_poses_txt(self._h, path.encode()), "kfx_write_poses_txt")
+
+    # ---- device-resident frames ------------------------------------------
+    def stage_frames(self, colors: np.ndarray, depths: np.ndarray):
+        colors = np.ascontiguousarray(colors, np.uint8)
+        depths = np.ascontiguousarray(depths, np.float32)
+        _check(lib().kfx_stage_frames(self._h, depths.shape[0], u8ptr(colors), fptr(depths)), "kfx_stage_frames")
+
+    def pipeline_staged(self, idx: int):
+        _check(lib().kfx_pipeline_staged(self._h, int(idx)), "kfx_pipeline_staged")
+
+    def synchronize(self):
+        _check(lib().kfx_synchronize(self._h), "kfx_synchronize")
+
+    def set_graph_mode(self, on: bool):
+        _check(lib().kfx_set_graph_mode(self._h, int(on)), "kfx_set_graph_mode")
+
+    def set_profiling(self, on: bool):
+        _check(lib().kfx_set_profiling(self._h, int(on)), "kfx_set_profiling")
+
+    def stage_ms(self) -> dict:
+        a = (C.c_float * 5)()
+        _check(lib().kfx_get_stage_ms(self._h, a), "kfx_get_stage_ms")
+        return dict(zip(["preprocess", "icp", "integrate", "raycast", "total"], a[:]))
+
+    def integrate_counts(self):
+        a, b = C.c_int64(), C.c_int64()
+        _check(lib().kfx_integrate_counts(self._h, C.byref(a), C.byref(b)), "kfx_integrate_counts")
+        return a.value, b.value
+
+    # ---- frames / volume -------------------------------------------------
+    def frame_maps(self, which: int, level: int):
+        li = self.intr.level(level)
+        d = np.zeros((li.height, li.width), np.float32)
+        v = np.zeros((li.height, li.width, 3), np.float32)
+        n = np.zeros_like(v)
+        _check(lib().kfx_get_frame_maps(self._h, which, level, fptr(d), fptr(v), fptr(n)), "kfx_get_frame_maps")
+        return d, v, n
+
+    def set_frame_maps(self, which: int, level: int, vmap: np.ndarray, nmap: np.ndarray):
+        v = np.ascontiguousarray(vmap, np.float32)
+        n = np.ascontiguousarray(nmap, np.float32)
+        _check(lib().kfx_set_frame_maps(self._h, which, level, fptr(v), fptr(n)), "kfx_set_frame_maps")
+
+    def download_tsdf(self) -> np.ndarray:
+        """Reference 8-byte records as a structured array (x fastest)."""
+        rec = np.zeros(self.nvox, dtype=np.dtype([("tsdf", "<i2"), ("weight", "<i2"), ("rgb", "u1", 3),
+                                                  ("pad", "u1")]))
+        _check(lib().kfx_download_tsdf(self._h, rec.ctypes.data_as(C.c_void_p)), "kfx_download_tsdf")
+        return rec
+
+    def upload_tsdf(self, rec: np.ndarray):
+        rec = np.ascontiguousarray(rec)
+        assert rec.nbytes == 8 * self.nvox
+        _check(lib().kfx_upload_tsdf(self._h, rec.ctypes.data_as(C.c_void_p)), "kfx_upload_tsdf")
+
+    def volume_soa(self):
+        t = np.zeros(self.nvox, np.int16)
+        w = np.zeros(self.nvox, np.int16)
+        c = np.zeros(4 * self.nvox, np.uint8)
+        _check(lib().kfx_download_volume_soa(self._h, i16ptr(t), i16ptr(w), u8ptr(c)), "kfx_download_volume_soa")
+        return t, w, c
+
+    # ---- stage seams -----------------------------------------------------
+    def stage_preprocess(self, color, depth_mm):
+        color = np.ascontiguousarray(color, np.uint8)
+        d = np.ascontiguousarray(depth_mm, np.float32)
+        _check(lib().kfx_stage_preprocess(self._h, u8ptr(color), fptr(d)), "kfx_stage_preprocess")
+
+    def stage_icp_accumulate(self, level: int, pose: Pose) -> np.ndarray:
+        s = np.zeros(27, np.int64)
+        _check(lib().kfx_stage_icp_accumulate(self._h, level, C.byref(pose), i64ptr(s)), "kfx_stage_icp_accumulate")
+        return s
+
+    def stage_icp(self):
+        p = Pose()
+        rc = _check(lib().kfx_stage_icp(self._h, C.byref(p)), "kfx_stage_icp", ok=(KFX_OK, KFX_TRACKING_LOST))
+        return rc, p
+
+    def stage_integrate(self, vol2cam: Pose, counts: bool = True):
+        a, b = C.c_int64(), C.c_int64()
+        _check(lib().kfx_stage_integrate(self._h, C.byref(vol2cam), C.byref(a) if counts else None,
+                                         C.byref(b) if counts else None), "kfx_stage_integrate")
+        return a.value, b.value
+
+    def stage_raycast(self, cam2vol: Pose, Rinv: np.ndarray):
+        R = np.ascontiguousarray(Rinv, np.float32).reshape(9)
+        _check(lib().kfx_stage_raycast(self._h, C.byref(cam2vol), fptr(R)), "kfx_stage_raycast")

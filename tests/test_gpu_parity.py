@@ -1,0 +1,334 @@
+"""GPU-vs-oracle parity through the C-ABI (libkfx.so on an MI355X).
+
+Bar: every stage is bit-identical to the CPU oracle on the
+same inputs — float maps compared bit for bit (NaN positions equal), voxel
+records / ICP sums / counts exactly equal.  The end-to-end pose tolerance is
+stated where it is used (it is 0 when every stage is bit-exact).
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+from kfx import KFX_FRAME_CUR, KFX_FRAME_PREV, KFX_OK, KFX_TRACKING_LOST, KinectFusion, synth
+from kfx.abi import Intrinsics, Pose, default_params
+
+pytestmark = pytest.mark.gpu
+
+L_VOL = 2.048
+
+
+def feq(a, b):
+    """Bit equality of float32 arrays with NaNs compared by position."""
+    a = np.ascontiguousarray(a, np.float32)
+    b = np.ascontiguousarray(b, np.float32)
+    if a.shape != b.shape:
+        return False
+    na, nb = np.isnan(a), np.isnan(b)
+    if not np.array_equal(na, nb):
+        return False
+    z = np.float32(0)
+    return np.array_equal(np.where(na, z, a).view(np.uint32), np.where(nb, z, b).view(np.uint32))
+
+
+def mismatch(a, b):
+    a = np.asarray(a, np.float32).ravel()
+    b = np.asarray(b, np.float32).ravel()
+    bad = ~((a == b) | (np.isnan(a) & np.isnan(b)))
+    return int(bad.sum())
+
+
+@pytest.fixture(scope="module")
+def seq_qvga():
+    return synth.sequence(10, synth.Intrinsics.qvga(), noise=True, dropout=0.01)
+
+
+@pytest.fixture(scope="module")
+def seq_vga():
+    return synth.sequence(6, synth.Intrinsics.vga(), noise=True, dropout=0.01)
+
+
+def make(intr, dims=128, **kw):
+    p = default_params(dims=dims, range_m=L_VOL)
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return KinectFusion(Intrinsics.from_any(intr), p), p
+
+
+@pytest.mark.parametrize("which", ["qvga", "vga"])
+def test_preprocess_bit_exact(which, seq_qvga, seq_vga):
+    bgr, dep, _ = seq_qvga if which == "qvga" else seq_vga
+    intr = synth.Intrinsics.qvga() if which == "qvga" else synth.Intrinsics.vga()
+    kf, p = make(intr, dims=64)
+    I = Intrinsics.from_any(intr)
+    for k in (0, 3):
+        d = dep[k].astype(np.float32)
+        kf.stage_preprocess(bgr[k], d)
+        ds, vs, ns = O.preprocess(d, I, p)
+        for l in range(3):
+            gd, gv, gn = kf.frame_maps(KFX_FRAME_CUR, l)
+            assert feq(gd, ds[l]), f"dmap level {l}: {mismatch(gd, ds[l])} px differ"
+            assert feq(gv, vs[l]), f"vmap level {l}: {mismatch(gv, vs[l])} differ"
+            assert feq(gn, ns[l]), f"nmap level {l}: {mismatch(gn, ns[l])} differ"
+    kf.close()
+
+
+def test_icp_accumulate_bit_exact(seq_vga):
+    bgr, dep, gt = seq_vga
+    intr = synth.Intrinsics.vga()
+    I = Intrinsics.from_any(intr)
+    kf, p = make(intr, dims=64)
+    prev = O.preprocess(dep[1].astype(np.float32), I, p)
+    kf.stage_preprocess(bgr[2], dep[2].astype(np.float32))
+    cur = O.preprocess(dep[2].astype(np.float32), I, p)
+    for l in range(3):
+        kf.set_frame_maps(KFX_FRAME_PREV, l, prev[1][l], prev[2][l])
+    rel = (np.linalg.inv(gt[1]) @ gt[2]).astype(np.float32)
+    jitter = rel.copy()
+    jitter[:3, 3] += [0.003, -0.002, 0.004]
+    for pose_m in (np.eye(4, dtype=np.float32), rel, jitter):
+        pose = Pose.from_matrix(pose_m)
+        for l in range(3):
+            g = kf.stage_icp_accumulate(l, pose)
+            o = O.icp_accumulate(cur[1][l], cur[2][l], prev[1][l], prev[2][l], I.level(l), pose)
+            assert np.array_equal(g, o), f"level {l}: {g - o}"
+            assert g[0] > 0
+    kf.close()
+
+
+def test_icp_track_matches_oracle(seq_vga):
+    import ctypes as C
+    from kfx.abi import fptr
+    bgr, dep, gt = seq_vga
+    intr = synth.Intrinsics.vga()
+    I = Intrinsics.from_any(intr)
+    kf, p = make(intr, dims=64)
+    prev = O.preprocess(dep[2].astype(np.float32), I, p)
+    cur = O.preprocess(dep[3].astype(np.float32), I, p)
+    kf.stage_preprocess(bgr[3], dep[3].astype(np.float32))
+    for l in range(3):
+        kf.set_frame_maps(KFX_FRAME_PREV, l, prev[1][l], prev[2][l])
+    rc, gpose = kf.stage_icp()
+    assert rc == KFX_OK
+    PA = C.POINTER(C.c_float) * 3
+    opose = Pose()
+    st = O.lib().kfo_icp_track(PA(*[fptr(a) for a in cur[1]]), PA(*[fptr(a) for a in cur[2]]),
+                               PA(*[fptr(a) for a in prev[1]]), PA(*[fptr(a) for a in prev[2]]),
+                               C.byref(I), C.byref(p), C.byref(opose))
+    assert st == 0
+    # the double cos/sin of the Rodrigues step are the only non-IEEE-basic ops
+    assert np.abs(gpose.matrix() - opose.matrix()).max() <= 1e-6
+    kf.close()
+
+
+def _vol_equal(kf, vol):
+    t, w, c = kf.volume_soa()
+    assert np.array_equal(t, vol.tsdf), f"tsdf: {(t != vol.tsdf).sum()} voxels differ"
+    assert np.array_equal(w, vol.weight), f"weight: {(w != vol.weight).sum()} voxels differ"
+    assert np.array_equal(c, vol.rgb), f"rgb: {(c != vol.rgb).sum()} bytes differ"
+
+
+def test_integrate_bit_exact_128(seq_qvga):
+    bgr, dep, gt = seq_qvga
+    intr = synth.Intrinsics.qvga()
+    I = Intrinsics.from_any(intr)
+    kf, p = make(intr, dims=128)
+    vol = O.Volume((128,) * 3, (L_VOL,) * 3)
+    for k in (0, 1, 2):
+        d = dep[k].astype(np.float32)
+        kf.stage_preprocess(bgr[k], d)
+        ds, _, _ = O.preprocess(d, I, p)
+        cam = Pose.from_matrix(gt[k])
+        vol2cam = O.pose_mul(O.pose_inv(cam), p.volu_pose)
+        gu, gc = kf.stage_integrate(vol2cam)
+        ou, oc = O.integrate(vol, p.volu_trun_dist, I, vol2cam, ds[0], bgr[k])
+        assert (gu, gc) == (ou, oc)
+        assert ou > 0 and oc > 0
+        _vol_equal(kf, vol)
+    kf.close()
+
+
+def test_integrate_512_column_spot_check(seq_vga):
+    """Full BASELINE size (512^3 @ 4 mm): GPU volume vs the oracle on 3000
+    sampled columns (the oracle restates any column independently)."""
+    bgr, dep, gt = seq_vga
+    intr = synth.Intrinsics.vga()
+    I = Intrinsics.from_any(intr)
+    kf, p = make(intr, dims=512)
+    d = dep[0].astype(np.float32)
+    kf.stage_preprocess(bgr[0], d)
+    ds, _, _ = O.preprocess(d, I, p)
+    vol2cam = p.volu_pose
+    gu, gc = kf.stage_integrate(vol2cam)
+    t, w, c = kf.volume_soa()
+    rng = np.random.default_rng(5)
+    cols = np.stack([rng.integers(0, 512, 3000), rng.integers(0, 512, 3000)], 1).astype(np.int32)
+    cols = np.concatenate([cols, np.array([[256, 256], [0, 0], [511, 511], [255, 300]], np.int32)])
+    vol = O.Volume((512,) * 3, (L_VOL,) * 3)
+    O.integrate(vol, p.volu_trun_dist, I, vol2cam, ds[0], bgr[0], cols=cols)
+    idx = (cols[:, 0][None, :] + 512 * cols[:, 1][None, :] + 512 * 512 * np.arange(512)[:, None]).ravel()
+    assert np.array_equal(t[idx], vol.tsdf[idx])
+    assert np.array_equal(w[idx], vol.weight[idx])
+    c4 = c.reshape(-1, 4)
+    assert np.array_equal(c4[idx], vol.rgb.reshape(-1, 4)[idx])
+    assert (w[idx] > 0).sum() > 10000
+    # counts: total over the volume equals the per-column oracle sum where computed in full
+    assert gu > 0 and 0 < gc < gu
+    kf.close()
+
+
+def test_raycast_bit_exact(seq_qvga):
+    bgr, dep, gt = seq_qvga
+    intr = synth.Intrinsics.qvga()
+    I = Intrinsics.from_any(intr)
+    kf, p = make(intr, dims=128)
+    vol = O.Volume((128,) * 3, (L_VOL,) * 3)
+    for k in (0, 1, 2):
+        d = dep[k].astype(np.float32)
+        kf.stage_preprocess(bgr[k], d)
+        ds, _, _ = O.preprocess(d, I, p)
+        vol2cam = O.pose_mul(O.pose_inv(Pose.from_matrix(gt[k])), p.volu_pose)
+        kf.stage_integrate(vol2cam, counts=False)
+        O.integrate(vol, p.volu_trun_dist, I, vol2cam, ds[0], bgr[k])
+    for k in (2, 4):
+        cam2vol = O.pose_mul(O.pose_inv(p.volu_pose), Pose.from_matrix(gt[k]))
+        Rinv = cam2vol.matrix()[:3, :3].T.copy()
+        kf.stage_raycast(cam2vol, Rinv)
+        ov, on = O.raycast(vol, I, cam2vol, Rinv)
+        _, gv, gn = kf.frame_maps(KFX_FRAME_PREV, 0)
+        assert feq(gv, ov), f"vmap: {mismatch(gv, ov)} differ"
+        assert feq(gn, on), f"nmap: {mismatch(gn, on)} differ"
+        assert (ov[..., 2] > 0).mean() > 0.5
+        for l in (1, 2):
+            ov, on = O.resize_points_normals(ov, on)
+            _, gv, gn = kf.frame_maps(KFX_FRAME_PREV, l)
+            assert feq(gv, ov) and feq(gn, on), f"level {l}"
+    kf.close()
+
+
+def _run_pipeline(kf, bgr, dep, u16=False):
+    st = []
+    for k in range(len(dep)):
+        st.append(kf.pipeline(bgr[k], dep[k] if u16 else dep[k].astype(np.float32)))
+    return st
+
+
+@pytest.mark.parametrize("which", ["qvga", "vga"])
+def test_pipeline_matches_oracle(which, seq_qvga, seq_vga):
+    bgr, dep, gt = seq_qvga if which == "qvga" else seq_vga
+    intr = synth.Intrinsics.qvga() if which == "qvga" else synth.Intrinsics.vga()
+    I = Intrinsics.from_any(intr)
+    kf, p = make(intr, dims=128)
+    st = _run_pipeline(kf, bgr, dep)
+    pipe = O.Pipeline(I, p)
+    ost = [pipe.process(bgr[k], dep[k].astype(np.float32)) for k in range(len(dep))]
+    assert st == ost == [KFX_OK] * len(dep)
+    assert kf.frame_count == pipe.frame_count == len(dep) + 1
+    gp, op = kf.pose_record, pipe.poses()
+    assert gp.shape == op.shape == (len(dep), 4, 4)
+    # tolerance: 0 if every stage is bit-exact; 1e-6 absorbs a last-ulp
+    # difference of the double cos/sin inside the Rodrigues update
+    err = np.abs(gp - op).max()
+    assert err <= 1e-6, err
+    if err == 0:
+        t, w, c = kf.volume_soa()
+        ot, ow, oc = pipe.volume()
+        assert np.array_equal(t, ot) and np.array_equal(w, ow) and np.array_equal(c, oc)
+        for l in range(3):
+            _, gv, gn = kf.frame_maps(KFX_FRAME_PREV, l)
+            assert feq(gv, pipe.map(1, 1, l)) and feq(gn, pipe.map(1, 2, l))
+    kf.close()
+
+
+def test_pipeline_modes_and_inputs_identical(seq_qvga):
+    """graph / eager / profiled launches and u16 / f32 / staged inputs all give
+    the same poses and volume."""
+    bgr, dep, gt = seq_qvga
+    intr = synth.Intrinsics.qvga()
+    res = []
+    for mode in ("graph", "eager", "profile", "u16", "staged"):
+        kf, p = make(intr, dims=64)
+        if mode == "eager":
+            kf.set_graph_mode(False)
+        if mode == "profile":
+            kf.set_profiling(True)
+        if mode == "staged":
+            kf.stage_frames(bgr, dep.astype(np.float32))
+            for k in range(len(dep)):
+                kf.pipeline_staged(k)
+            kf.synchronize()
+        else:
+            _run_pipeline(kf, bgr, dep, u16=(mode == "u16"))
+        if mode == "profile":
+            ms = kf.stage_ms()
+            assert ms["total"] > 0 and ms["integrate"] > 0
+        res.append((kf.pose_record, kf.volume_soa()))
+        kf.close()
+    for poses, vol in res[1:]:
+        assert np.array_equal(poses, res[0][0])
+        for a, b in zip(vol, res[0][1]):
+            assert np.array_equal(a, b)
+
+
+def test_tracking_failure_resets_like_reference(seq_qvga):
+    bgr, dep, gt = seq_qvga
+    intr = synth.Intrinsics.qvga()
+    kf, p = make(intr, dims=64)
+    assert kf.pipeline(bgr[0], dep[0].astype(np.float32)) == KFX_OK
+    assert kf.pipeline(bgr[1], dep[1].astype(np.float32)) == KFX_OK
+    blank = np.zeros_like(dep[2], dtype=np.float32)
+    assert kf.pipeline(bgr[2], blank) == KFX_TRACKING_LOST
+    assert kf.frame_count == 1
+    assert kf.pose_record.shape == (1, 4, 4)
+    t, w, c = kf.volume_soa()
+    assert not t.any() and not w.any() and not c.any()
+    # next frame bootstraps again (kinectfusion.cpp:84-93)
+    assert kf.pipeline(bgr[3], dep[3].astype(np.float32)) == KFX_OK
+    assert kf.frame_count == 2
+    assert kf.volume_soa()[1].any()
+    kf.close()
+
+
+def test_tsdf_record_export_roundtrip(seq_qvga):
+    bgr, dep, gt = seq_qvga
+    intr = synth.Intrinsics.qvga()
+    kf, p = make(intr, dims=64)
+    _run_pipeline(kf, bgr[:3], dep[:3])
+    rec = kf.download_tsdf()
+    t, w, c = kf.volume_soa()
+    assert np.array_equal(rec["tsdf"], t) and np.array_equal(rec["weight"], w)
+    assert np.array_equal(rec["rgb"], c.reshape(-1, 4)[:, :3]) and not rec["pad"].any()
+    kf2, _ = make(intr, dims=64)
+    kf2.upload_tsdf(rec)
+    assert np.array_equal(kf2.download_tsdf().view(np.uint64), rec.view(np.uint64))
+    kf.close()
+    kf2.close()
+
+
+def test_poses_txt_matches_oracle_writer(seq_qvga, tmp_path):
+    bgr, dep, gt = seq_qvga
+    kf, p = make(synth.Intrinsics.qvga(), dims=64)
+    _run_pipeline(kf, bgr[:4], dep[:4])
+    path = tmp_path / "poses.txt"
+    kf.write_poses_txt(str(path))
+    exp = "".join(O.format_pose(Pose.from_matrix(m)) for m in kf.pose_record)
+    assert path.read_text() == exp
+    kf.close()
+
+
+def test_full_size_pipeline_512(seq_vga):
+    """BASELINE C2 geometry (640x480, 512^3 @ 4 mm): GPU pipeline vs the oracle
+    pipeline on the same frames (the oracle runs ~seconds per frame)."""
+    bgr, dep, gt = seq_vga
+    n = 4
+    intr = synth.Intrinsics.vga()
+    kf, p = make(intr, dims=512)
+    st = _run_pipeline(kf, bgr[:n], dep[:n])
+    assert st == [KFX_OK] * n
+    pipe = O.Pipeline(Intrinsics.from_any(intr), p)
+    for k in range(n):
+        assert pipe.process(bgr[k], dep[k].astype(np.float32)) == 0
+    gp, op = kf.pose_record, pipe.poses()
+    assert np.abs(gp - op).max() <= 1e-6
+    # A3 bias bounds accuracy to ~2 voxels (8 mm) against the analytic truth
+    assert np.abs(gp[:, :3, 3] - gt[:n, :3, 3]).max() < 0.012
+    kf.close()
