@@ -1,0 +1,223 @@
+#!/usr/bin/env python3
+"""KinectFusion hot-path benchmark (BASELINE.json metric: frames/sec at
+640x480, 512^3 TSDF; per-stage ms).
+
+Workload (BASELINE config C2): synthetic 640x480 depth + BGR frames of the
+analytic scene (kfx.synth), 512^3 TSDF @ 4 mm, 3-level ICP {10,5,4}.  A "step"
+is one kf::kinectfusion::pipeline() frame: preprocess, 19 ICP iterations,
+integrate, raycast, resize.  Frames are staged in HBM before the timed region
+(kfx_stage_frames); every timed frame then copies its input D2D and runs the
+captured per-frame hipGraph.
+
+Multi-GPU (`torchrun --nproc-per-node N`): one process per GPU, each running an
+independent replica on its own synthetic camera stream (DESIGN.md §multi-GPU:
+Z-slab sharding of one stream is the next step); value = frames of all ranks /
+max wall time over ranks.
+
+The JSON line also carries:
+  stage_ms      per-stage device ms (HIP events on the pipeline stream)
+  roofline      integrate kernel: algorithmic bytes (8*N_upd + 8*N_col + 7*W*H,
+                SURVEY.md §8d; N counted on the device) / its event-timed
+                duration vs 8 TB/s HBM
+  cpu_baseline  the serial C++ oracle running the same pipeline on host cores
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "slam-kinectfusion_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+REF_MS_PER_FRAME = 18.0  # README.md:8-9 (GTX 1650 Ti, 640x480, 512^3)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=300)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--dims", type=int, default=512)
+    ap.add_argument("--range", type=float, default=2.048)
+    ap.add_argument("--width", type=int, default=640)
+    ap.add_argument("--height", type=int, default=480)
+    ap.add_argument("--unique", type=int, default=48, help="distinct frames rendered (played ping-pong)")
+    ap.add_argument("--profile-frames", type=int, default=20)
+    ap.add_argument("--cpu-frames", type=int, default=3, help="oracle frames timed for cpu_baseline (0 = skip)")
+    ap.add_argument("--no-graph", action="store_true")
+    return ap.parse_args()
+
+
+def intrinsics(w, h):
+    from kfx import synth
+    if (w, h) == (640, 480):
+        return synth.Intrinsics.vga()
+    if (w, h) == (1280, 720):
+        return synth.Intrinsics.hd720()
+    s = w / 640.0
+    return synth.Intrinsics(w, h, 525.0 * s, 525.0 * s, (w - 1) / 2.0, (h - 1) / 2.0)
+
+
+def cpu_baseline(intr, params, bgr, dep, n):
+    """Serial oracle (TEST INFRASTRUCTURE, used here only as the reported CPU
+    baseline) on a bounded sample: frame 0 bootstraps untimed, frames 1..n timed."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    from kfx.abi import Intrinsics
+    pipe = oracle.Pipeline(Intrinsics.from_any(intr), params)
+    pipe.process(bgr[0], dep[0].astype(np.float32))
+    t0 = time.perf_counter()
+    for k in range(1, n + 1):
+        pipe.process(bgr[k], dep[k].astype(np.float32))
+    dt = time.perf_counter() - t0
+    return {"value": round(n / dt, 4), "unit": "frames/s", "cores": 1, "kind": "port",
+            "ms_per_frame": round(1000.0 * dt / n, 1),
+            "sample": f"frames 1..{n} of the same synthetic sequence at the same config "
+                      f"({intr.width}x{intr.height}, {params.volu_dims[0]}^3), full pipeline "
+                      f"(preprocess+ICP+integrate+raycast), single thread, oracle/kfx_oracle.cpp -O2",
+            "cpu": _cpu_model()}
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def main():
+    a = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+        dist.init_process_group(backend=backend)
+
+    import kfx
+    from kfx import synth
+    from kfx.abi import Intrinsics, default_params
+
+    intr = intrinsics(a.width, a.height)
+    params = default_params(dims=a.dims, range_m=a.range)
+    bgr, dep, gt = synth.sequence(a.unique, intr, L=a.range, noise=True, traj_seed=7 + rank, dropout=0.005)
+    order = synth.ping_pong(a.unique, a.warmup + a.steps + a.profile_frames)
+
+    kf = kfx.KinectFusion(Intrinsics.from_any(intr), params, device=local)
+    kf.set_graph_mode(not a.no_graph)
+    kf.stage_frames(bgr, dep.astype(np.float32))
+
+    def sync_all():
+        kf.synchronize()
+        if dist is not None:
+            dist.barrier()
+
+    for i in range(a.warmup):
+        kf.pipeline_staged(order[i])
+    sync_all()
+    n_before = kf.pose_record.shape[0]
+    t0 = time.perf_counter()
+    for i in range(a.warmup, a.warmup + a.steps):
+        kf.pipeline_staged(order[i])
+    kf.synchronize()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64,
+                         device="cuda" if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        dist.barrier()
+    n_after = kf.pose_record.shape[0]
+    tracked = n_after - n_before  # frames that appended a pose (failures reset the record)
+
+    # per-stage device ms + integrate roofline on further frames (profiled, eager)
+    kf.set_profiling(True)
+    stages = {k: [] for k in ("preprocess", "icp", "integrate", "raycast", "total")}
+    int_bytes, int_ms = [], []
+    W, H = intr.width, intr.height
+    for i in range(a.warmup + a.steps, a.warmup + a.steps + a.profile_frames):
+        kf.pipeline_staged(order[i])
+        ms = kf.stage_ms()
+        for k in stages:
+            stages[k].append(ms[k])
+        nu, nc = kf.integrate_counts()
+        int_bytes.append(8 * nu + 8 * nc + 7 * W * H)
+        int_ms.append(ms["integrate"])
+    kf.set_profiling(False)
+    stage_med = {k: round(statistics.median(v), 4) for k, v in stages.items()}
+    avg_bytes = float(np.mean(int_bytes))
+    avg_ms = float(np.mean(int_ms))
+    achieved = avg_bytes / (avg_ms * 1e-3) / 1e9
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", "integrate_pmc.json")
+    if os.path.exists(pmc_path):
+        try:
+            traffic = json.load(open(pmc_path)).get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            traffic = None
+
+    cpu = None
+    if rank == 0 and world == 1 and a.cpu_frames > 0:
+        cpu = cpu_baseline(intr, params, bgr, dep, min(a.cpu_frames, a.unique - 1))
+
+    total_frames = a.steps * world
+    value = total_frames / elapsed
+    if rank == 0:
+        out = {
+            "metric": "frames/sec at 640×480, 512³ TSDF; per-stage ms (ICP/integrate/raycast)",
+            "value": round(value, 3),
+            "unit": "frames/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(1000.0 * elapsed / a.steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round((value / world) / (1000.0 / REF_MS_PER_FRAME), 3),
+            "dtype": "f32",
+            "data": "synthetic",
+            "config": {
+                "workload": f"C2: synthetic {W}x{H} depth+BGR, {a.dims}^3 TSDF @ "
+                            f"{1000 * a.range / a.dims:.1f} mm, 3-level ICP {{10,5,4}}, full pipeline per frame",
+                "width": W, "height": H, "volume_dims": a.dims, "volume_range_m": a.range,
+                "frames_unique": a.unique, "graph": not a.no_graph,
+                "parallelism": f"replicas x{world}" if world > 1 else "single",
+                "tracked_frames": int(tracked),
+            },
+            "stage_ms": stage_med,
+            "roofline": {
+                "kernel": "k_integrate",
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "algorithmic_bytes_per_launch": int(avg_bytes),
+                "avg_launch_ms": round(avg_ms, 4),
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out))
+    kf.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -115,8 +115,11 @@ int dalloc(kfx_ctx *c, void **p, size_t bytes) {
     return set_err(KFX_ERR_OOM, "hipMalloc(" + std::to_string(bytes) + "): " + hipGetErrorString(e));
   }
   c->allocs.push_back(*p);
-  e = hipMemset(*p, 0, bytes);
-  if (e != hipSuccess) return set_err(KFX_ERR_HIP, std::string("hipMemset: ") + hipGetErrorString(e));
+  // zero on the context's (non-blocking) stream so later kernels on it are
+  // ordered after the fill; a null-stream hipMemset would race with them
+  e = hipMemsetAsync(*p, 0, bytes, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  if (e != hipSuccess) return set_err(KFX_ERR_HIP, std::string("hipMemsetAsync: ") + hipGetErrorString(e));
   return KFX_OK;
 }
 
@@ -205,7 +208,9 @@ int ensure_pose_capacity(kfx_ctx *c, int more) {
   const int ncap = c->pose_cap * 2;
   DevPose *nl = nullptr;
   HIPCHK(hipMalloc(&nl, sizeof(DevPose) * (size_t)ncap));
-  HIPCHK(hipMemcpy(nl, c->pose_log, sizeof(DevPose) * (size_t)c->pose_cap, hipMemcpyDeviceToDevice));
+  HIPCHK(hipMemcpyAsync(nl, c->pose_log, sizeof(DevPose) * (size_t)c->pose_cap,
+                        hipMemcpyDeviceToDevice, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
   for (auto &a : c->allocs)
     if (a == c->pose_log) a = nl;
   HIPCHK(hipFree(c->pose_log));
@@ -465,8 +470,10 @@ int kfx_stage_frames(kfx_ctx *c, int n, const uint8_t *bgr, const float *depth_m
   c->n_staged = 0;
   if ((r = dalloc(c, (void **)&c->staged_depth, np * 4 * (size_t)n))) return r;
   if ((r = dalloc(c, (void **)&c->staged_bgr, np * 3 * (size_t)n))) return r;
-  HIPCHK(hipMemcpy(c->staged_depth, depth_mm, np * 4 * (size_t)n, hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(c->staged_bgr, bgr, np * 3 * (size_t)n, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpyAsync(c->staged_depth, depth_mm, np * 4 * (size_t)n, hipMemcpyHostToDevice,
+                        c->stream));
+  HIPCHK(hipMemcpyAsync(c->staged_bgr, bgr, np * 3 * (size_t)n, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
   c->n_staged = n;
   return KFX_OK;
 }
@@ -515,7 +522,9 @@ int kfx_get_cur_camera_pose(kfx_ctx *c, kfx_pose *out) {
   DevState s;
   if ((r = read_state(c, &s))) return r;
   DevPose d;
-  HIPCHK(hipMemcpy(&d, c->pose_log + (s.n_poses - 1), sizeof(d), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpyAsync(&d, c->pose_log + (s.n_poses - 1), sizeof(d), hipMemcpyDeviceToHost,
+                        c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
   *out = to_api(d);
   return KFX_OK;
 }
@@ -540,7 +549,9 @@ int kfx_get_pose_record(kfx_ctx *c, kfx_pose *out, int cap, int *n) {
   const int m = std::min(cap, s.n_poses);
   if (out && m > 0) {
     std::vector<DevPose> tmp(m);
-    HIPCHK(hipMemcpy(tmp.data(), c->pose_log, sizeof(DevPose) * m, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpyAsync(tmp.data(), c->pose_log, sizeof(DevPose) * m, hipMemcpyDeviceToHost,
+                          c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
     for (int i = 0; i < m; ++i) out[i] = to_api(tmp[i]);
   }
   return s.pose_overflow ? set_err(KFX_ERR_STATE, "pose log overflow") : KFX_OK;
@@ -574,12 +585,13 @@ int kfx_get_frame_maps(kfx_ctx *c, int which, int level, float *dmap, float *vma
   const size_t np = (size_t)c->g[level].w * c->g[level].h;
   if (dmap) {
     if (which == KFX_FRAME_CUR)
-      HIPCHK(hipMemcpy(dmap, f.d[level], np * 4, hipMemcpyDeviceToHost));
+      HIPCHK(hipMemcpyAsync(dmap, f.d[level], np * 4, hipMemcpyDeviceToHost, c->stream));
     else
       std::memset(dmap, 0, np * 4);
   }
-  if (vmap) HIPCHK(hipMemcpy(vmap, f.v[level], np * 12, hipMemcpyDeviceToHost));
-  if (nmap) HIPCHK(hipMemcpy(nmap, f.n[level], np * 12, hipMemcpyDeviceToHost));
+  if (vmap) HIPCHK(hipMemcpyAsync(vmap, f.v[level], np * 12, hipMemcpyDeviceToHost, c->stream));
+  if (nmap) HIPCHK(hipMemcpyAsync(nmap, f.n[level], np * 12, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
   return KFX_OK;
 }
 
@@ -591,8 +603,9 @@ int kfx_set_frame_maps(kfx_ctx *c, int which, int level, const float *vmap, cons
   HIPCHK(hipStreamSynchronize(c->stream));
   const FrameView &f = which == KFX_FRAME_CUR ? c->cur : c->prev;
   const size_t np = (size_t)c->g[level].w * c->g[level].h;
-  if (vmap) HIPCHK(hipMemcpy(f.v[level], vmap, np * 12, hipMemcpyHostToDevice));
-  if (nmap) HIPCHK(hipMemcpy(f.n[level], nmap, np * 12, hipMemcpyHostToDevice));
+  if (vmap) HIPCHK(hipMemcpyAsync(f.v[level], vmap, np * 12, hipMemcpyHostToDevice, c->stream));
+  if (nmap) HIPCHK(hipMemcpyAsync(f.n[level], nmap, np * 12, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
   return KFX_OK;
 }
 

@@ -163,6 +163,7 @@ def test_integrate_512_column_spot_check(seq_vga):
     rng = np.random.default_rng(5)
     cols = np.stack([rng.integers(0, 512, 3000), rng.integers(0, 512, 3000)], 1).astype(np.int32)
     cols = np.concatenate([cols, np.array([[256, 256], [0, 0], [511, 511], [255, 300]], np.int32)])
+    cols = np.unique(cols, axis=0)  # a repeated column would be integrated twice
     vol = O.Volume((512,) * 3, (L_VOL,) * 3)
     O.integrate(vol, p.volu_trun_dist, I, vol2cam, ds[0], bgr[0], cols=cols)
     idx = (cols[:, 0][None, :] + 512 * cols[:, 1][None, :] + 512 * 512 * np.arange(512)[:, None]).ravel()
