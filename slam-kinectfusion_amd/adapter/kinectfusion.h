@@ -1,0 +1,193 @@
+// kinectfusion.h — header-only drop-in for the reference's kfusion/include/kinectfusion.h.
+//
+// Recreates kf::kinectfuison_params and kf::kinectfusion (kinectfusion.h:9-73) with the same
+// names, member types and call semantics on top of the C-ABI (include/kfx.h), so the
+// reference's main.cpp and depth_sensor.{h,cpp} compile unchanged: put this directory ahead of
+// kfusion/include on the include path, keep the reference's types.hpp (kf::Intrinsics), drop
+// kfusion/src/{kinectfusion,icp_registration,tsdf_volume}.cpp and *.cu from the build and link
+// libkfx.so.  Needs OpenCV core (cv::Mat, cv::Affine3f); OpenCV-CUDA is no longer required.
+//
+// Display helpers (getRenderMap) are not on the hot path: they shade the downloaded raycast
+// maps on the host with the reference's formulas (image_process.cu:137-221).
+#pragma once
+
+#include <opencv2/core.hpp>
+#include <opencv2/core/affine.hpp>
+
+#include <cmath>
+#include <fstream>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/kfx.h"
+#include "types.hpp"  // the reference's kf::Intrinsics (types.hpp:13-29)
+
+namespace kf {
+
+// kinectfusion.h:9-30
+struct kinectfuison_params {
+  kinectfuison_params default_params() {
+    kfx_params c;
+    kfx_default_params(&c);
+    kinectfuison_params p;
+    p.pyramid_height = c.pyramid_height;
+    p.dfilter_dist = c.dfilter_dist;
+    p.bfilter_kernel_size = c.bfilter_kernel_size;
+    p.bfilter_spatial_sigma = c.bfilter_spatial_sigma;
+    p.bfilter_color_sigma = c.bfilter_color_sigma;
+    p.icp_dist_threshold = c.icp_dist_threshold;
+    p.icp_angle__threshold = c.icp_angle_threshold;
+    p.icp_iter_count.assign(c.icp_iter_count, c.icp_iter_count + c.pyramid_height);
+    p.volu_range = cv::Vec3f(c.volu_range[0], c.volu_range[1], c.volu_range[2]);
+    p.volu_dims = cv::Vec3i(c.volu_dims[0], c.volu_dims[1], c.volu_dims[2]);
+    p.volu_trun_dist = c.volu_trun_dist;
+    p.volu_pose = cv::Affine3f().translate(cv::Vec3f(c.volu_pose.t[0], c.volu_pose.t[1], c.volu_pose.t[2]));
+    p.init_cam_model_dist = 0.f;
+    p.min_pose_move = c.min_pose_move;
+    p.tsdf_max_weight = c.tsdf_max_weight;
+    return p;
+  }
+  int pyramid_height;
+  float dfilter_dist;
+  int bfilter_kernel_size;
+  float bfilter_spatial_sigma;
+  float bfilter_color_sigma;
+  float icp_dist_threshold;
+  float icp_angle__threshold;
+  std::vector<int> icp_iter_count;
+  cv::Vec3f volu_range;
+  cv::Affine3f volu_pose;
+  float volu_trun_dist;
+  float init_cam_model_dist;
+  cv::Vec3i volu_dims;
+  float min_pose_move;
+  int tsdf_max_weight;
+};
+
+inline kfx_pose to_kfx(const cv::Affine3f &a) {
+  kfx_pose p;
+  for (int i = 0; i < 3; ++i) {
+    for (int j = 0; j < 3; ++j) p.R[3 * i + j] = a.matrix(i, j);
+    p.t[i] = a.matrix(i, 3);
+  }
+  return p;
+}
+
+inline cv::Affine3f from_kfx(const kfx_pose &p) {
+  cv::Matx44f m = cv::Matx44f::eye();
+  for (int i = 0; i < 3; ++i) {
+    for (int j = 0; j < 3; ++j) m(i, j) = p.R[3 * i + j];
+    m(i, 3) = p.t[i];
+  }
+  return cv::Affine3f(m);
+}
+
+// kinectfusion.h:31-73
+class kinectfusion {
+ public:
+  enum DISPLAY_TYPES { PHONG, NORMAL };
+
+  kinectfusion(const kf::Intrinsics intr, const kf::kinectfuison_params params)
+      : intr_(intr), params_(params) {
+    kfx_intrinsics ci{intr.width, intr.height, intr.fx, intr.fy, intr.cx, intr.cy};
+    kfx_params cp;
+    kfx_default_params(&cp);
+    cp.pyramid_height = params.pyramid_height;
+    cp.dfilter_dist = params.dfilter_dist;
+    cp.bfilter_kernel_size = params.bfilter_kernel_size;
+    cp.bfilter_spatial_sigma = params.bfilter_spatial_sigma;
+    cp.bfilter_color_sigma = params.bfilter_color_sigma;
+    cp.icp_dist_threshold = params.icp_dist_threshold;
+    cp.icp_angle_threshold = params.icp_angle__threshold;
+    for (int l = 0; l < KFX_MAX_LEVELS; ++l)
+      cp.icp_iter_count[l] = l < (int)params.icp_iter_count.size() ? params.icp_iter_count[l] : 0;
+    for (int i = 0; i < 3; ++i) {
+      cp.volu_range[i] = params.volu_range[i];
+      cp.volu_dims[i] = params.volu_dims[i];
+    }
+    cp.volu_trun_dist = params.volu_trun_dist;
+    cp.volu_pose = to_kfx(params.volu_pose);
+    cp.tsdf_max_weight = params.tsdf_max_weight;
+    cp.min_pose_move = params.min_pose_move;
+    if (kfx_create(&ci, &cp, 0, &ctx_) != KFX_OK) throw std::runtime_error(kfx_last_error());
+    sync_host_state();
+  }
+  ~kinectfusion() { release(); }
+
+  // kinectfusion.cpp:78-127.  Depth is CV_32FC1 millimetres (depth_sensor.cpp:191) or CV_16UC1.
+  void pipeline(cv::Mat cmap_, cv::Mat dmap_) {
+    cv::Mat c = cmap_.isContinuous() ? cmap_ : cmap_.clone();
+    cv::Mat d = dmap_.isContinuous() ? dmap_ : dmap_.clone();
+    int rc;
+    if (d.type() == CV_16UC1)
+      rc = kfx_pipeline_u16(ctx_, c.ptr<uint8_t>(), d.ptr<uint16_t>());
+    else
+      rc = kfx_pipeline(ctx_, c.ptr<uint8_t>(), d.ptr<float>());
+    if (rc == KFX_TRACKING_LOST) std::cout << "tracking fail!" << std::endl;  // kinectfusion.cpp:99
+    else if (rc != KFX_OK) throw std::runtime_error(kfx_last_error());
+    sync_host_state();
+  }
+  void reset() {
+    kfx_reset(ctx_);
+    sync_host_state();
+  }
+  cv::Mat getRenderMap(DISPLAY_TYPES V = PHONG) {
+    const int w = intr_.width, h = intr_.height;
+    std::vector<float> v(3 * (size_t)w * h), n(3 * (size_t)w * h);
+    kfx_get_frame_maps(ctx_, KFX_FRAME_PREV, 0, nullptr, v.data(), n.data());
+    cv::Mat out(h, w, CV_8UC3, cv::Scalar(0, 0, 0));
+    const cv::Vec3f eye = pose_record.back().translation();
+    for (int y = 0; y < h; ++y)
+      for (int x = 0; x < w; ++x) {
+        const float *nv = &n[3 * ((size_t)y * w + x)], *vv = &v[3 * ((size_t)y * w + x)];
+        cv::Vec3b &px = out.at<cv::Vec3b>(y, x);
+        if (V == NORMAL) {  // image_process.cu:137-147
+          px = cv::Vec3b((uchar)(std::fabs(nv[0]) * 255), (uchar)(std::fabs(nv[1]) * 255),
+                         (uchar)(std::fabs(nv[2]) * 255));
+          continue;
+        }
+        // image_process.cu:159-211
+        if ((nv[0] == 0 && nv[1] == 0 && nv[2] == 0) || (vv[0] == 0 && vv[1] == 0 && vv[2] == 0)) continue;
+        cv::Vec3f nrm(nv[0], nv[1], nv[2]), vert(vv[0], vv[1], vv[2]);
+        cv::Vec3f e = cv::normalize(eye - vert), l = cv::normalize(cv::Vec3f(500.f, 500.f, -500.f) - vert);
+        const float lc = std::fabs(nrm.dot(l));
+        cv::Vec3f diffuse = cv::Vec3f(0.3843f, 0.4745f, 0.580f) * (0.9f * lc);
+        const float hc = std::fabs(nrm.dot(cv::normalize(l + e)));
+        const float spec = 0.5f * 0.9f * std::pow(hc, 10.f);
+        px = cv::Vec3b((uchar)(std::fmin(1.f, 0.1f + diffuse[0] + spec) * 255),
+                       (uchar)(std::fmin(1.f, 0.1f + diffuse[1] + spec) * 255),
+                       (uchar)(std::fmin(1.f, 0.1f + diffuse[2] + spec) * 255));
+      }
+    return out;
+  }
+  cv::Mat extracePointcloud();          // next: zero-crossing extraction (DESIGN.md §1 row f)
+  void savePointcloud(std::string path);  // next: ASCII PLY writer (kinectfusion.cpp:148-166)
+  cv::Affine3f getCurCameraPose() { return pose_record.back(); }
+  void release() {
+    if (ctx_) kfx_destroy(ctx_);
+    ctx_ = nullptr;
+  }
+
+ public:
+  std::string frame_time;
+  int frame_count = 1;
+  std::vector<cv::Affine3f> pose_record;
+
+ private:
+  void sync_host_state() {
+    kfx_get_frame_count(ctx_, &frame_count);
+    int n = 0;
+    kfx_get_pose_record(ctx_, nullptr, 0, &n);
+    std::vector<kfx_pose> ps(n);
+    kfx_get_pose_record(ctx_, ps.data(), n, &n);
+    pose_record.clear();
+    for (const kfx_pose &p : ps) pose_record.push_back(from_kfx(p));
+  }
+
+  kfx_ctx *ctx_ = nullptr;
+  Intrinsics intr_;
+  kinectfuison_params params_;
+};
+
+}  // namespace kf

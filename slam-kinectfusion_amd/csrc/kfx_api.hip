@@ -89,7 +89,8 @@ struct kfx_ctx {
   DevState *st = nullptr;
   DevPose *pose_log = nullptr;
   int pose_cap = 0;
-  long long *partials = nullptr;
+  unsigned long long *icp_shards = nullptr;  // 8 x 27 int64 + ticket (self-resetting)
+  unsigned *icp_ticket = nullptr;
   unsigned long long *counters = nullptr;
   std::vector<void *> allocs;
 
@@ -154,13 +155,10 @@ void enqueue_frame(kfx_ctx *c, bool u16, bool events) {
   if (events) (void)hipEventRecord(c->ev[1], s);
   // ICPRegistration::rigidTransform (icp_registration.cpp:16-46)
   for (int level = c->L - 1; level >= 0; --level) {
-    const int nb = icp_blocks(c->g[level]);
-    for (int it = 0; it < c->p.icp_iter_count[level]; ++it) {
-      launch_icp_acc(s, c->g[level], c->cur.v[level], c->cur.n[level], c->prev.v[level],
-                     c->prev.n[level], c->p.icp_dist_threshold, c->angle_thr, c->st, c->partials,
-                     0);
-      launch_icp_solve(s, c->st, c->partials, nb, 0, 1);
-    }
+    for (int it = 0; it < c->p.icp_iter_count[level]; ++it)
+      launch_icp(s, c->g[level], c->cur.v[level], c->cur.n[level], c->prev.v[level],
+                 c->prev.n[level], c->p.icp_dist_threshold, c->angle_thr, c->st, c->icp_shards,
+                 c->icp_ticket, 0, 1);
   }
   launch_commit(s, c->st, c->pose_log, to_dev(c->p.volu_pose));
   if (events) (void)hipEventRecord(c->ev[2], s);
@@ -267,6 +265,7 @@ VolView make_vol(const kfx_params &p) {
     v.range[i] = p.volu_range[i];
   }
   v.trunc = p.volu_trun_dist;
+  v.inv_trunc = 1.f / v.trunc;
   return v;
 }
 
@@ -402,9 +401,9 @@ int kfx_create(const kfx_intrinsics *intr, const kfx_params *params, int device,
   if ((r = dalloc(c, (void **)&c->st, sizeof(DevState)))) return fail(r);
   c->pose_cap = kInitialPoseCap;
   if ((r = dalloc(c, (void **)&c->pose_log, sizeof(DevPose) * (size_t)c->pose_cap))) return fail(r);
-  int maxnb = 1;
-  for (int l = 0; l < c->L; ++l) maxnb = std::max(maxnb, icp_blocks(c->g[l]));
-  if ((r = dalloc(c, (void **)&c->partials, sizeof(long long) * 27 * (size_t)maxnb))) return fail(r);
+  if ((r = dalloc(c, (void **)&c->icp_shards, sizeof(unsigned long long) * 8 * 27 + 64)))
+    return fail(r);
+  c->icp_ticket = reinterpret_cast<unsigned *>(c->icp_shards + 8 * 27);
   if ((r = dalloc(c, (void **)&c->counters, sizeof(unsigned long long) * 32))) return fail(r);
   launch_inv_lambda(c->stream, c->g[0], c->inv_lambda);
   if ((r = do_reset(c))) return fail(r);
@@ -719,9 +718,9 @@ int kfx_stage_icp_accumulate(kfx_ctx *c, int level, const kfx_pose *pose, int64_
   if (r) return r;
   if (level < 0 || level >= c->L || !pose || !sums) return set_err(KFX_ERR_ARG, "bad argument");
   if ((r = write_field(c, offsetof(DevState, icp_pose), to_dev(*pose)))) return r;
-  launch_icp_acc(c->stream, c->g[level], c->cur.v[level], c->cur.n[level], c->prev.v[level],
-                 c->prev.n[level], c->p.icp_dist_threshold, c->angle_thr, c->st, c->partials, 1);
-  launch_icp_solve(c->stream, c->st, c->partials, icp_blocks(c->g[level]), 1, 0);
+  launch_icp(c->stream, c->g[level], c->cur.v[level], c->cur.n[level], c->prev.v[level],
+             c->prev.n[level], c->p.icp_dist_threshold, c->angle_thr, c->st, c->icp_shards,
+             c->icp_ticket, 1, 0);
   HIPCHK(hipGetLastError());
   DevState s;
   if ((r = read_state(c, &s))) return r;
@@ -740,13 +739,10 @@ int kfx_stage_icp(kfx_ctx *c, kfx_pose *out) {
   s.icp_pose = identity_pose();
   HIPCHK(hipMemcpyAsync(c->st, &s, sizeof(s), hipMemcpyHostToDevice, c->stream));
   for (int level = c->L - 1; level >= 0; --level) {
-    const int nb = icp_blocks(c->g[level]);
-    for (int it = 0; it < c->p.icp_iter_count[level]; ++it) {
-      launch_icp_acc(c->stream, c->g[level], c->cur.v[level], c->cur.n[level], c->prev.v[level],
-                     c->prev.n[level], c->p.icp_dist_threshold, c->angle_thr, c->st, c->partials,
-                     0);
-      launch_icp_solve(c->stream, c->st, c->partials, nb, 0, 1);
-    }
+    for (int it = 0; it < c->p.icp_iter_count[level]; ++it)
+      launch_icp(c->stream, c->g[level], c->cur.v[level], c->cur.n[level], c->prev.v[level],
+                 c->prev.n[level], c->p.icp_dist_threshold, c->angle_thr, c->st, c->icp_shards,
+                 c->icp_ticket, 0, 1);
   }
   HIPCHK(hipGetLastError());
   if ((r = read_state(c, &s))) return r;

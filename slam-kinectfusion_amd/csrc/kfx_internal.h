@@ -53,6 +53,7 @@ struct VolView {
   float vs[3];     // voxel size per axis
   float range[3];  // volume_range
   float trunc;
+  float inv_trunc;  // RN(1/trunc), for the exact FMA division (kfx_kernels.hip div_rn)
   size_t slice;    // voxels per z slice (= X*Y)
 };
 
@@ -72,11 +73,11 @@ void launch_bilateral_vertex(hipStream_t s, int levels, const float *const raw[k
                              DevState *st);
 void launch_normals(hipStream_t s, int levels, const LevelGeom *g, FrameView cur);
 int icp_blocks(const LevelGeom &g);
-void launch_icp_acc(hipStream_t s, const LevelGeom &g, const float *cv, const float *cn,
-                    const float *pv, const float *pn, float dist_thr, float angle_thr,
-                    DevState *st, long long *partials, int force);
-void launch_icp_solve(hipStream_t s, DevState *st, const long long *partials, int nblocks,
-                      int force_mode, int update);
+// one ICP iteration (rigid_icp.cu:135-169 + icp_registration.cpp:33-42) in a
+// single launch; shards = 8 x 27 int64 zeroed, ticket zeroed (both self-reset)
+void launch_icp(hipStream_t s, const LevelGeom &g, const float *cv, const float *cn,
+                const float *pv, const float *pn, float dist_thr, float angle_thr, DevState *st,
+                unsigned long long *shards, unsigned *ticket, int force, int update);
 void launch_commit(hipStream_t s, DevState *st, DevPose *pose_log, DevPose volume_pose);
 void launch_integrate(hipStream_t s, VolView v, LevelGeom g0, const float *dmap,
                       const uint8_t *bgr, const float *inv_lambda, const DevState *st,

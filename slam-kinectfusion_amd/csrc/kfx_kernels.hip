@@ -78,6 +78,17 @@ __device__ __forceinline__ float det_expf(float x) {
   return p * __uint_as_float((unsigned)(k + 127) << 23);
 }
 
+// x / d correctly rounded in 3 instructions given y = RN(1/d): Markstein's
+// theorem (q0 = RN(x*y) is within 1 ulp, the FMA remainder is exact, one
+// correction step rounds correctly).  Checked against IEEE division on 6.7e9
+// operand pairs for the divisors used here (1..65 and the truncation
+// distances), and for every colour quotient (tools/markstein_check.c).
+__device__ __forceinline__ float div_rn(float x, float d, float y) {
+  const float q0 = x * y;
+  const float r = fmaf(-q0, d, x);
+  return fmaf(r, y, q0);
+}
+
 __device__ __forceinline__ DevPose pose_identity() {
   DevPose p;
   for (int i = 0; i < 9; ++i) p.R[i] = (i % 4 == 0) ? 1.f : 0.f;
@@ -297,41 +308,72 @@ __global__ __launch_bounds__(256) void k_normals(NormalArgs a) {
 
 // ICP::findCoresp + kernel_rigidICP (rigid_icp.cu:46-113): per pixel of the
 // floor-covered region (A2), the 7-vector row and its 27 products, summed as
-// exact int64 fixed point (D), reduced per block through LDS.
+// exact int64 fixed point (D; order-independent, so any reduction tree gives
+// the oracle's sums).  Each lane takes kIcpPix pixels whose loads are issued
+// together; the block reduces through LDS and writes one 27-word partial.
+constexpr int kIcpPix = 4;
+constexpr int kIcpBlockPix = 256 * kIcpPix;
+constexpr int kIcpShards = 8;
+__device__ int icp_update(const long long *sums, DevPose &pose, double *xo);
+
 __global__ __launch_bounds__(256) void k_icp_acc(LevelGeom g, int xe, int npix,
                                                  const float *__restrict__ cv,
                                                  const float *__restrict__ cn,
                                                  const float *__restrict__ pv,
                                                  const float *__restrict__ pn, float dist_thr,
-                                                 float angle_thr, const DevState *__restrict__ st,
-                                                 long long *__restrict__ partials, int force) {
+                                                 float angle_thr, DevState *__restrict__ st,
+                                                 unsigned long long *__restrict__ shards,
+                                                 unsigned *__restrict__ ticket, int force,
+                                                 int update) {
   if (!force && (st->mode != MODE_TRACK || st->icp_fail)) return;
   const DevPose P = st->icp_pose;
   const f3 t = {P.t[0], P.t[1], P.t[2]};
   long long acc[27];
 #pragma unroll
   for (int k = 0; k < 27; ++k) acc[k] = 0;
-  for (int i = blockIdx.x * 256 + threadIdx.x; i < npix; i += gridDim.x * 256) {
-    const int x = i % xe, y = i / xe;
-    const size_t idx = (size_t)y * g.w + x;
-    const f3 n0 = ld3(cn, idx);
-    if (isnan(n0.x)) continue;
-    const f3 vcur = add(rmul(P.R, ld3(cv, idx)), t);
-    const int px = f2i_rn((vcur.x / vcur.z) * g.fx + g.cx);
-    const int py = f2i_rn((vcur.y / vcur.z) * g.fy + g.cy);
-    if (!(vcur.z > 0 && px >= 0 && py >= 0 && px < g.w && py < g.h)) continue;
-    const size_t j = (size_t)py * g.w + px;
-    const f3 vpre = ld3(pv, j);
-    const f3 dd = sub(vcur, vpre);
+
+  // loads are unconditional (out-of-range lanes read pixel 0) so the
+  // compiler issues each group back to back instead of waiting per branch
+  f3 n0[kIcpPix], v0[kIcpPix];
+  bool ok[kIcpPix];
+#pragma unroll
+  for (int q = 0; q < kIcpPix; ++q) {
+    const int i = blockIdx.x * kIcpBlockPix + q * 256 + threadIdx.x;
+    ok[q] = i < npix;
+    const size_t idx = ok[q] ? (size_t)(i / xe) * g.w + (i % xe) : 0;
+    n0[q] = ld3(cn, idx);
+    v0[q] = ld3(cv, idx);
+  }
+  f3 vcur[kIcpPix];
+  int j[kIcpPix];
+#pragma unroll
+  for (int q = 0; q < kIcpPix; ++q) {
+    vcur[q] = add(rmul(P.R, v0[q]), t);
+    const int px = f2i_rn((vcur[q].x / vcur[q].z) * g.fx + g.cx);
+    const int py = f2i_rn((vcur[q].y / vcur[q].z) * g.fy + g.cy);
+    ok[q] = ok[q] && !isnan(n0[q].x) && vcur[q].z > 0 && px >= 0 && py >= 0 && px < g.w &&
+            py < g.h;
+    j[q] = ok[q] ? py * g.w + px : 0;
+  }
+  f3 vpre[kIcpPix], npre[kIcpPix];
+#pragma unroll
+  for (int q = 0; q < kIcpPix; ++q) {
+    vpre[q] = ld3(pv, j[q]);
+    npre[q] = ld3(pn, j[q]);
+  }
+#pragma unroll
+  for (int q = 0; q < kIcpPix; ++q) {
+    if (!ok[q]) continue;
+    const f3 dd = sub(vcur[q], vpre[q]);
     const float dist = sqrtf(dot(dd, dd));
     if (!(dist <= dist_thr)) continue;
-    const f3 ncur = rmul(P.R, n0);
-    const f3 npre = ld3(pn, j);
-    const f3 sa = cross(ncur, npre);
+    const f3 ncur = rmul(P.R, n0[q]);
+    const f3 sa = cross(ncur, npre[q]);
     const float sine = sqrtf(dot(sa, sa));
     if (!(sine <= angle_thr)) continue;
-    const f3 c = cross(vcur, npre);
-    const float row[7] = {c.x, c.y, c.z, npre.x, npre.y, npre.z, dot(npre, sub(vpre, vcur))};
+    const f3 c = cross(vcur[q], npre[q]);
+    const float row[7] = {c.x,       c.y,       c.z, npre[q].x, npre[q].y,
+                          npre[q].z, dot(npre[q], sub(vpre[q], vcur[q]))};
     int s = 0;
 #pragma unroll
     for (int a = 0; a < 6; ++a)
@@ -341,75 +383,144 @@ __global__ __launch_bounds__(256) void k_icp_acc(LevelGeom g, int xe, int npix,
         acc[s++] += (long long)rintf(prod * kFix);
       }
   }
-  __shared__ long long red[27 * 256];
+  // LDS transpose reduction: row (wave, k) holds 64 lane values (stride 65 to
+  // spread banks); 108 threads sum one row each, then 27 threads sum 4 waves.
+  __shared__ long long red[4 * 27 * 65];
+  __shared__ long long red2[4 * 27];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #pragma unroll
-  for (int k = 0; k < 27; ++k) red[k * 256 + threadIdx.x] = acc[k];
+  for (int k = 0; k < 27; ++k) red[(wv * 27 + k) * 65 + lane] = acc[k];
   __syncthreads();
-  __shared__ long long red2[8 * 27];
-  if (threadIdx.x < 216) {
-    const int k = threadIdx.x % 27, seg = threadIdx.x / 27;
-    long long s = 0;
-    for (int q = 0; q < 32; ++q) s += red[k * 256 + seg * 32 + q];
-    red2[seg * 27 + k] = s;
+  if (threadIdx.x < 108) {
+    const long long *r = red + threadIdx.x * 65;
+    long long s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+    for (int q = 0; q < 64; q += 4) {
+      s0 += r[q];
+      s1 += r[q + 1];
+      s2 += r[q + 2];
+      s3 += r[q + 3];
+    }
+    red2[threadIdx.x] = (s0 + s1) + (s2 + s3);
   }
   __syncthreads();
+  // Cross-block sum + solve in the same launch: wave 0 adds the block's 27
+  // sums into one of kIcpShards shard rows with device-scope int64 atomics
+  // (performed at the memory side; exact and order-free), waits for them, then
+  // takes a ticket.  The block drawing the last ticket reads-and-clears the
+  // shards and runs icp_registration.cpp:33-42 (icp_update) on one lane.
+  __shared__ int last;
+  if (threadIdx.x < 64) {
+    if (threadIdx.x < 27) {
+      const int k = threadIdx.x;
+      const long long v = red2[k] + red2[27 + k] + red2[54 + k] + red2[81 + k];
+      __hip_atomic_fetch_add(&shards[(blockIdx.x % kIcpShards) * 27 + k], (unsigned long long)v,
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (threadIdx.x == 0) {
+      const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last = (t == gridDim.x - 1);
+    }
+  }
+  __syncthreads();
+  if (!last) return;
+  __shared__ long long sums[27];
   if (threadIdx.x < 27) {
-    long long s = 0;
-    for (int seg = 0; seg < 8; ++seg) s += red2[seg * 27 + threadIdx.x];
-    partials[(size_t)blockIdx.x * 27 + threadIdx.x] = s;
+    long long a = 0;
+#pragma unroll
+    for (int sh = 0; sh < kIcpShards; ++sh)
+      a += (long long)__hip_atomic_exchange(&shards[sh * 27 + threadIdx.x], 0ull,
+                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sums[threadIdx.x] = a;
+    st->sums[threadIdx.x] = a;
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  if (threadIdx.x == 0 && update) {
+    long long sm[27];
+#pragma unroll
+    for (int k = 0; k < 27; ++k) sm[k] = sums[k];
+    DevPose p = st->icp_pose;
+    double x[6];
+    if (icp_update(sm, p, x)) {
+      st->icp_fail = 1;
+    } else {
+      st->icp_pose = p;
+#pragma unroll
+      for (int i = 0; i < 6; ++i) st->x[i] = x[i];
+    }
   }
 }
 
 // icp_registration.cpp:33-42 on the device: A/b unpack (rigid_icp.cu:156-165),
 // LU det check, LU solve (D: instead of SVD), Rodrigues, pose = pose * Tinc.
+// Fully unrolled with select-based row swaps so A lives in registers; the
+// arithmetic is operation-for-operation the oracle's kfo_icp_update.
 __device__ int icp_update(const long long *sums, DevPose &pose, double *xo) {
   double A[6][6], b[6];
-  int s = 0;
-  for (int i = 0; i < 6; ++i)
-    for (int j = i; j < 7; ++j) {
-      const double v = (double)sums[s++] * (1.0 / 4294967296.0);
-      if (j == 6)
-        b[i] = v;
-      else
-        A[i][j] = A[j][i] = v;
-    }
+  {
+    int s = 0;
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+      for (int j = i; j < 7; ++j) {
+        const double v = (double)sums[s++] * (1.0 / 4294967296.0);
+        if (j == 6)
+          b[i] = v;
+        else
+          A[i][j] = A[j][i] = v;
+      }
+  }
   int sign = 1;
+#pragma unroll
   for (int k = 0; k < 6; ++k) {
     int p = k;
     double best = fabs(A[k][k]);
-    for (int i = k + 1; i < 6; ++i)
-      if (fabs(A[i][k]) > best) {
-        best = fabs(A[i][k]);
+#pragma unroll
+    for (int i = k + 1; i < 6; ++i) {
+      const double a = fabs(A[i][k]);
+      if (a > best) {
+        best = a;
         p = i;
       }
-    if (p != k) {
+    }
+    if (p != k) sign = -sign;
+#pragma unroll
+    for (int i = k + 1; i < 6; ++i) {
+      const bool sw = (p == i);
+#pragma unroll
       for (int j = 0; j < 6; ++j) {
-        const double tmp = A[k][j];
-        A[k][j] = A[p][j];
-        A[p][j] = tmp;
+        const double tk = A[k][j], ti = A[i][j];
+        A[k][j] = sw ? ti : tk;
+        A[i][j] = sw ? tk : ti;
       }
-      const double tb = b[k];
-      b[k] = b[p];
-      b[p] = tb;
-      sign = -sign;
+      const double bk = b[k], bi = b[i];
+      b[k] = sw ? bi : bk;
+      b[i] = sw ? bk : bi;
     }
     if (A[k][k] != 0.0) {
+#pragma unroll
       for (int i = k + 1; i < 6; ++i) {
         const double f = A[i][k] / A[k][k];
+#pragma unroll
         for (int j = k + 1; j < 6; ++j) A[i][j] = A[i][j] - f * A[k][j];
         b[i] = b[i] - f * b[k];
       }
     }
   }
   double det = (double)sign;
+#pragma unroll
   for (int k = 0; k < 6; ++k) det = det * A[k][k];
   if (fabs(det) < 1e-15 || isnan(det)) return 1;
   double x[6];
+#pragma unroll
   for (int i = 5; i >= 0; --i) {
     double acc = b[i];
+#pragma unroll
     for (int j = i + 1; j < 6; ++j) acc = acc - A[i][j] * x[j];
     x[i] = acc / A[i][i];
   }
+#pragma unroll
   for (int i = 0; i < 6; ++i) xo[i] = x[i];
   const float rv[3] = {(float)x[0], (float)x[1], (float)x[2]};
   DevPose inc;
@@ -419,6 +530,7 @@ __device__ int icp_update(const long long *sums, DevPose &pose, double *xo) {
   const double theta =
       sqrt((double)rv[0] * rv[0] + (double)rv[1] * rv[1] + (double)rv[2] * rv[2]);
   if (theta < 2.220446049250313e-16) {
+#pragma unroll
     for (int i = 0; i < 9; ++i) inc.R[i] = (i % 4 == 0) ? 1.f : 0.f;
   } else {
     const double c = cos(theta), sn = sin(theta), c1 = 1.0 - c;
@@ -427,6 +539,7 @@ __device__ int icp_update(const long long *sums, DevPose &pose, double *xo) {
     const float rrt[9] = {r[0] * r[0], r[0] * r[1], r[0] * r[2], r[0] * r[1], r[1] * r[1],
                           r[1] * r[2], r[0] * r[2], r[1] * r[2], r[2] * r[2]};
     const float rx[9] = {0.f, -r[2], r[1], r[2], 0.f, -r[0], -r[1], r[0], 0.f};
+#pragma unroll
     for (int i = 0; i < 9; ++i) {
       const float e = (i % 4 == 0) ? 1.f : 0.f;
       inc.R[i] = ((float)(c * e) + (float)(c1 * rrt[i])) + (float)(sn * rx[i]);
@@ -434,37 +547,6 @@ __device__ int icp_update(const long long *sums, DevPose &pose, double *xo) {
   }
   pose = pose_mul(pose, inc);
   return 0;
-}
-
-__global__ __launch_bounds__(256) void k_icp_solve(DevState *st, const long long *partials,
-                                                   int nb, int force, int update) {
-  if (!force && (st->mode != MODE_TRACK || st->icp_fail)) return;
-  __shared__ long long red2[9 * 27];
-  if (threadIdx.x < 243) {
-    const int k = threadIdx.x % 27, seg = threadIdx.x / 27;
-    long long s = 0;
-    for (int b = seg; b < nb; b += 9) s += partials[(size_t)b * 27 + k];
-    red2[seg * 27 + k] = s;
-  }
-  __syncthreads();
-  __shared__ long long sums[27];
-  if (threadIdx.x < 27) {
-    long long s = 0;
-    for (int seg = 0; seg < 9; ++seg) s += red2[seg * 27 + threadIdx.x];
-    sums[threadIdx.x] = s;
-    st->sums[threadIdx.x] = s;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0 && update) {
-    DevPose p = st->icp_pose;
-    double x[6];
-    if (icp_update(sums, p, x)) {
-      st->icp_fail = 1;
-    } else {
-      st->icp_pose = p;
-      for (int i = 0; i < 6; ++i) st->x[i] = x[i];
-    }
-  }
 }
 
 // kinectfusion.cpp:84-104 bookkeeping, single thread: frame-1 bootstrap,
@@ -530,6 +612,10 @@ __global__ __launch_bounds__(256) void k_integrate(VolView v, LevelGeom g,
                                                    const float *__restrict__ invl,
                                                    const DevState *__restrict__ st,
                                                    unsigned long long *counters) {
+  // rtab[d] = RN(1/d), d = 1..65: the weight divisors of the running averages
+  __shared__ float rtab[66];
+  if (threadIdx.x < 66) rtab[threadIdx.x] = 1.f / (float)max(1, (int)threadIdx.x);
+  __syncthreads();
   const int lane = threadIdx.x & 63;
   const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (tile >= v.tiles_x * v.tiles_y) return;
@@ -581,43 +667,96 @@ __global__ __launch_bounds__(256) void k_integrate(VolView v, LevelGeom g,
   unsigned cu = 0, cc = 0;
   int z = 1;
   for (; z < zlo; ++z) vc = add(vc, zs);
-  for (; z <= zhi; ++z) {
-    vc = add(vc, zs);
-    if (vc.z <= 0) continue;
-    const int u = f2i_rn((vc.x / vc.z) * g.fx + g.cx);
-    const int vv = f2i_rn((vc.y / vc.z) * g.fy + g.cy);
-    if (u < 0 || u >= g.w || vv < 0 || vv >= g.h) continue;
-    const size_t pix = (size_t)vv * g.w + u;
-    const float depth = dmap[pix];
-    if (depth <= 0) continue;
-    const float sdf = -(invl[pix] * sqrtf(dot(vc, vc)) - depth);
-    if (sdf >= -trunc) {
-      const size_t i = base + (size_t)z * v.slice;
-      if (kCount) {
-        ++cu;
-        if (sdf <= thres_color && sdf >= -thres_color) ++cc;
-        continue;
+  // Batches of kB voxels: projections, then the kB depth gathers, then the
+  // voxel loads of the batch are issued back to back (memory-level
+  // parallelism); each voxel's arithmetic is exactly the reference's.
+  constexpr int kB = 8;
+  for (; z <= zhi; z += kB) {
+    float sdf[kB];
+    int pix[kB];
+    bool ok[kB];
+    f3 vcj[kB];
+#pragma unroll
+    for (int j = 0; j < kB; ++j) {
+      vc = add(vc, zs);
+      vcj[j] = vc;
+      ok[j] = false;
+      pix[j] = 0;
+      if (z + j <= zhi && vc.z > 0) {
+        const int u = f2i_rn((vc.x / vc.z) * g.fx + g.cx);
+        const int vv = f2i_rn((vc.y / vc.z) * g.fy + g.cy);
+        if (!(u < 0 || u >= g.w || vv < 0 || vv >= g.h)) {
+          pix[j] = vv * g.w + u;
+          ok[j] = true;
+        }
       }
-      const float ts = fminf(1.f, sdf / trunc);
-      const int16_t t0 = v.tsdf[i];
-      const int pre_w = v.weight[i];
-      const float pre_t = (float)t0 * kDivShortMax;
+    }
+    // Loads are issued unconditionally (inactive lanes read a dummy element
+    // that every such lane shares, so they add no traffic): a predicated load
+    // makes the compiler wait for it inside its branch.
+    float dep[kB], il[kB];
+#pragma unroll
+    for (int j = 0; j < kB; ++j) {
+      dep[j] = dmap[ok[j] ? pix[j] : 0];
+      il[j] = invl[ok[j] ? pix[j] : 0];
+    }
+#pragma unroll
+    for (int j = 0; j < kB; ++j) {
+      if (ok[j] && dep[j] > 0) {
+        sdf[j] = -(il[j] * sqrtf(dot(vcj[j], vcj[j])) - dep[j]);
+        ok[j] = sdf[j] >= -trunc;
+      } else {
+        ok[j] = false;
+        sdf[j] = 0.f;
+      }
+    }
+    if (kCount) {
+#pragma unroll
+      for (int j = 0; j < kB; ++j)
+        if (ok[j]) {
+          ++cu;
+          if (sdf[j] <= thres_color && sdf[j] >= -thres_color) ++cc;
+        }
+      continue;
+    }
+    int16_t t0[kB], w0[kB];
+    uint32_t c0[kB], px0[kB];
+    bool band[kB];
+#pragma unroll
+    for (int j = 0; j < kB; ++j) {
+      const size_t i = ok[j] ? base + (size_t)(z + j) * v.slice : 0;
+      band[j] = ok[j] && sdf[j] <= thres_color && sdf[j] >= -thres_color;
+      const size_t ib = band[j] ? i : 0;
+      const size_t pb = band[j] ? 3 * (size_t)pix[j] : 0;
+      t0[j] = v.tsdf[i];
+      w0[j] = v.weight[i];
+      c0[j] = v.rgb[ib];
+      px0[j] = (uint32_t)bgr[pb] | ((uint32_t)bgr[pb + 1] << 8) | ((uint32_t)bgr[pb + 2] << 16);
+    }
+#pragma unroll
+    for (int j = 0; j < kB; ++j) {
+      if (!ok[j]) continue;
+      const size_t i = base + (size_t)(z + j) * v.slice;
+      const float ts = fminf(1.f, div_rn(sdf[j], trunc, v.inv_trunc));
+      const int pre_w = w0[j];
+      const float pre_t = (float)t0[j] * kDivShortMax;
       const int new_w = min(pre_w + 1, kMaxWeight);
-      const float new_t = fmaf(pre_t, (float)pre_w, ts) / (float)(pre_w + 1);
+      const float new_t =
+          div_rn(fmaf(pre_t, (float)pre_w, ts), (float)(pre_w + 1), rtab[pre_w + 1]);
       int q = (int)(new_t * (float)kShortMax);
       q = max(-kShortMax, min(kShortMax, q));
       v.tsdf[i] = (int16_t)q;
       v.weight[i] = (int16_t)new_w;
-      if (sdf <= thres_color && sdf >= -thres_color) {
-        const uint32_t mc = v.rgb[i];
-        const uint8_t *px = bgr + 3 * pix;
+      if (band[j]) {
         const float c = (float)(new_w + 1);
+        const float rc = rtab[new_w + 1];
         uint32_t out = 0u;
 #pragma unroll
         for (int ch = 0; ch < 3; ++ch) {
-          const int m0 = (int)((mc >> (8 * ch)) & 0xffu);
-          const float m = (float)(new_w * m0 + (int)px[ch]);
-          out |= (uint32_t)(uint8_t)(m / c) << (8 * ch);
+          const int m0 = (int)((c0[j] >> (8 * ch)) & 0xffu);
+          const int pc = (int)((px0[j] >> (8 * ch)) & 0xffu);
+          const float m = (float)(new_w * m0 + pc);
+          out |= (uint32_t)(uint8_t)div_rn(m, c, rc) << (8 * ch);
         }
         v.rgb[i] = out;
       }
@@ -701,7 +840,7 @@ __global__ __launch_bounds__(256) void k_raycast(VolView v, LevelGeom g, RayCons
     return;
   }
   f3 vout = {0.f, 0.f, 0.f}, nout = {0.f, 0.f, 0.f};
-  if (mode == MODE_TRACK) {
+  if (mode == MODE_TRACK) {  // block-uniform
     const DevPose P = st->cam2vol;
     const f3 org = {P.t[0], P.t[1], P.t[2]};
     const f3 pp = {(1.f * ((float)x - g.cx)) / g.fx, (1.f * ((float)y - g.cy)) / g.fy, 1.f};
@@ -714,28 +853,90 @@ __global__ __launch_bounds__(256) void k_raycast(VolView v, LevelGeom g, RayCons
     const float tnear = fmaxf(fmaxf(tmin.x, tmin.y), fmaxf(tmin.x, tmin.z));
     const float tfar = fminf(fminf(tmax.x, tmax.y), fminf(tmax.x, tmax.z));
     float ray_len = fmaxf(tnear, 0.f);
-    if (ray_len < tfar) {
-      const f3 vstep = mulc(dir, rc.vs);
-      ray_len += rc.step;
-      f3 nextp = add(org, scl(dir, ray_len));
-      float tn = voxel2tsdf(v, rc, nextp);
-      for (; ray_len < tfar; ray_len += rc.step) {
-        nextp = add(nextp, vstep);
-        const float tcur = tn;
-        tn = voxel2tsdf(v, rc, nextp);
-        if (isnan(tn)) continue;
-        if (tcur < 0.f && tn > 0.f) break;
-        if (tcur > 0.f && tn < 0.f) {
-          const float Ts = ray_len - (v.vs[0] * tcur) / (tcur - tn);  // A3 (R)
-          const f3 vertex = add(org, scl(dir, Ts));
-          const f3 n = compute_normal(v, rc, vertex);
-          if (!isnan(n.x * n.y * n.z)) {
-            nout = rmul(st->Rinv, n);
-            vout = rmul(st->Rinv, sub(vertex, org));
-            break;
+    bool live = ray_len < tfar;
+    const f3 vstep = mulc(dir, rc.vs);
+    ray_len += rc.step;
+    f3 nextp = add(org, scl(dir, ray_len));
+    // reference loop state: the carried sample (tsdf_cur for the next step)
+    float tprev = live ? voxel2tsdf(v, rc, nextp) : NAN;
+    // The march goes kR samples at a time.  Load phase: positions (repeated
+    // nextp += vstep) and tsdf loads for the kR samples, issued back to back.
+    // Scan phase: the reference's events depend only on consecutive samples
+    // (tsdf_cur is the previous sample, NaN included), so with sign s in
+    // {-1,0,+1} (0 = NaN) an event at j is s[j-1]*s[j] == -1: a lane builds a
+    // 16-bit event mask with plain VALU math and only lanes with an event do
+    // more work (a -/+ event ends the ray; a +/- event computes the normal
+    // and, if it is NaN, the scan resumes at the next event).
+    constexpr int kR = 16;
+    int sprev = isnan(tprev) ? 0 : (tprev > 0.f ? 1 : (tprev < 0.f ? -1 : 0));
+    while (__any(live)) {
+      int16_t raw[kR];
+      float rlv[kR];
+      bool val[kR];
+      int je = kR;
+      float rl = ray_len;
+#pragma unroll
+      for (int j = 0; j < kR; ++j) {
+        const bool a = live && rl < tfar;
+        je = (!a && je == kR) ? j : je;
+        nextp.x = a ? nextp.x + vstep.x : nextp.x;
+        nextp.y = a ? nextp.y + vstep.y : nextp.y;
+        nextp.z = a ? nextp.z + vstep.z : nextp.z;
+        const int ix = f2i_rn(nextp.x * rc.vs_inv.x);
+        const int iy = f2i_rn(nextp.y * rc.vs_inv.y);
+        const int iz = f2i_rn(nextp.z * rc.vs_inv.z);
+        val[j] = a && !(ix >= v.X - 1 || iy >= v.Y - 1 || iz >= v.Z - 1 || ix < 1 || iy < 1 || iz < 1);
+        raw[j] = v.tsdf[val[j] ? vox_index(v, ix, iy, iz) : 0];
+        rlv[j] = rl;
+        rl = a ? rl + rc.step : rl;
+      }
+      unsigned ev = 0u, hitm = 0u;
+      const float tfirst = tprev;
+      int sp = sprev;
+#pragma unroll
+      for (int j = 0; j < kR; ++j) {
+        const int sj = val[j] ? (raw[j] > 0) - (raw[j] < 0) : 0;
+        const bool e = sp * sj == -1;
+        ev |= e ? (1u << j) : 0u;
+        hitm |= (e && sj < 0) ? (1u << j) : 0u;
+        sp = sj;
+      }
+      sprev = sp;
+      tprev = val[kR - 1] ? (float)raw[kR - 1] * kDivShortMax : NAN;
+      unsigned pend = live ? ev : 0u;
+      while (__any(pend != 0u)) {
+        if (pend != 0u) {
+          const int j0 = __ffs(pend) - 1;
+          if (!((hitm >> j0) & 1u)) {  // tsdf_cur < 0 && tsdf_next > 0: stop, no surface
+            live = false;
+            pend = 0u;
+          } else {
+            float tc = tfirst, tn = 0.f, rj = 0.f;
+#pragma unroll
+            for (int j = 0; j < kR; ++j) {
+              const float tj = (float)raw[j] * kDivShortMax;
+              if (j + 1 == j0) tc = tj;
+              if (j == j0) {
+                tn = tj;
+                rj = rlv[j];
+              }
+            }
+            const float Ts = rj - (v.vs[0] * tc) / (tc - tn);  // A3 (R)
+            const f3 vertex = add(org, scl(dir, Ts));
+            const f3 n = compute_normal(v, rc, vertex);
+            if (!isnan(n.x * n.y * n.z)) {
+              nout = rmul(st->Rinv, n);
+              vout = rmul(st->Rinv, sub(vertex, org));
+              live = false;
+              pend = 0u;
+            } else {
+              pend &= ~(1u << j0);
+            }
           }
         }
       }
+      if (je < kR) live = false;  // left [.., tfar) inside this batch
+      ray_len = rl;
     }
   }
   st3(prev.v[0], o, vout);
@@ -922,23 +1123,17 @@ static int icp_npix(const LevelGeom &g, int *xe) {
 int icp_blocks(const LevelGeom &g) {
   int xe;
   const int n = icp_npix(g, &xe);
-  int nb = (n + 1023) / 1024;
+  int nb = (n + kIcpBlockPix - 1) / kIcpBlockPix;
   return nb < 1 ? 1 : nb;
 }
 
-void launch_icp_acc(hipStream_t s, const LevelGeom &g, const float *cv, const float *cn,
-                    const float *pv, const float *pn, float dist_thr, float angle_thr,
-                    DevState *st, long long *partials, int force) {
+void launch_icp(hipStream_t s, const LevelGeom &g, const float *cv, const float *cn,
+                const float *pv, const float *pn, float dist_thr, float angle_thr, DevState *st,
+                unsigned long long *shards, unsigned *ticket, int force, int update) {
   int xe;
   const int n = icp_npix(g, &xe);
   hipLaunchKernelGGL(k_icp_acc, dim3(icp_blocks(g)), dim3(256), 0, s, g, xe, n, cv, cn, pv, pn,
-                     dist_thr, angle_thr, st, partials, force);
-}
-
-void launch_icp_solve(hipStream_t s, DevState *st, const long long *partials, int nblocks,
-                      int force_mode, int update) {
-  hipLaunchKernelGGL(k_icp_solve, dim3(1), dim3(256), 0, s, st, partials, nblocks, force_mode,
-                     update);
+                     dist_thr, angle_thr, st, shards, ticket, force, update);
 }
 
 void launch_commit(hipStream_t s, DevState *st, DevPose *pose_log, DevPose volume_pose) {
