@@ -353,6 +353,10 @@ int kfx_create(const kfx_intrinsics *intr, const kfx_params *params, int device,
       return set_err(KFX_ERR_ARG, "volume dims must be >= 8 and range > 0");
   if (p.volu_dims[0] % 8 || p.volu_dims[1] % 8)
     return set_err(KFX_ERR_ARG, "volume dims x,y must be multiples of 8 (8x8 slice tiles)");
+  // keeps every in-block ICP fixed-point sum an integer below 2^53 (exact fp64
+  // accumulation in k_icp_acc): |point| stays below ~45 m
+  if (!(p.dfilter_dist > 0.f && p.dfilter_dist <= 30.f))
+    return set_err(KFX_ERR_ARG, "dfilter_dist must be in (0, 30] m");
   if (p.bfilter_kernel_size < 1 || p.bfilter_kernel_size > 15)
     return set_err(KFX_ERR_ARG, "bfilter_kernel_size must be 1..15");
   for (int l = 0; l < p.pyramid_height; ++l)

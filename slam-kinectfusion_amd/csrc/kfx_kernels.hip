@@ -6,6 +6,7 @@
 // Every float expression follows the reference's evaluation order (file:line
 // cited per kernel) and the file is compiled with -ffp-contract=off, so results
 // are bit-identical to the CPU oracle (oracle/kfx_oracle.cpp) on the same inputs.
+#include <algorithm>
 #include <climits>
 
 #include "kfx_internal.h"
@@ -328,9 +329,13 @@ __global__ __launch_bounds__(256) void k_icp_acc(LevelGeom g, int xe, int npix,
   if (!force && (st->mode != MODE_TRACK || st->icp_fail)) return;
   const DevPose P = st->icp_pose;
   const f3 t = {P.t[0], P.t[1], P.t[2]};
-  long long acc[27];
+  // Every product is rounded to an integer multiple of 2^-32 (rintf(prod *
+  // 2^32)); within a block the running sums are integers below 2^49 (|prod|
+  // < 2^7, <= 2^10 products per 27-slot), so fp64 adds are exact and equal the
+  // oracle's int64 sums; the block total converts to int64 exactly.
+  double acc[27];
 #pragma unroll
-  for (int k = 0; k < 27; ++k) acc[k] = 0;
+  for (int k = 0; k < 27; ++k) acc[k] = 0.0;
 
   // loads are unconditional (out-of-range lanes read pixel 0) so the
   // compiler issues each group back to back instead of waiting per branch
@@ -380,20 +385,20 @@ __global__ __launch_bounds__(256) void k_icp_acc(LevelGeom g, int xe, int npix,
 #pragma unroll
       for (int b = a; b < 7; ++b) {
         const float prod = row[a] * row[b];
-        acc[s++] += (long long)rintf(prod * kFix);
+        acc[s++] += (double)rintf(prod * kFix);
       }
   }
   // LDS transpose reduction: row (wave, k) holds 64 lane values (stride 65 to
   // spread banks); 108 threads sum one row each, then 27 threads sum 4 waves.
-  __shared__ long long red[4 * 27 * 65];
-  __shared__ long long red2[4 * 27];
+  __shared__ double red[4 * 27 * 65];
+  __shared__ double red2[4 * 27];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #pragma unroll
   for (int k = 0; k < 27; ++k) red[(wv * 27 + k) * 65 + lane] = acc[k];
   __syncthreads();
   if (threadIdx.x < 108) {
-    const long long *r = red + threadIdx.x * 65;
-    long long s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+    const double *r = red + threadIdx.x * 65;
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
     for (int q = 0; q < 64; q += 4) {
       s0 += r[q];
       s1 += r[q + 1];
@@ -412,7 +417,7 @@ __global__ __launch_bounds__(256) void k_icp_acc(LevelGeom g, int xe, int npix,
   if (threadIdx.x < 64) {
     if (threadIdx.x < 27) {
       const int k = threadIdx.x;
-      const long long v = red2[k] + red2[27 + k] + red2[54 + k] + red2[81 + k];
+      const long long v = (long long)(red2[k] + red2[27 + k] + red2[54 + k] + red2[81 + k]);
       __hip_atomic_fetch_add(&shards[(blockIdx.x % kIcpShards) * 27 + k], (unsigned long long)v,
                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -603,6 +608,10 @@ __device__ __forceinline__ void clip_lin(double alpha, double beta, double &lo, 
   }
 }
 
+// Work split: a wave owns an 8x8 tile of columns and one of gridDim.y z-chunks
+// of every column's in-range interval (more waves per SIMD to hide latency);
+// each lane replays the vc adds up to its chunk start, so every voxel's vc is
+// the reference's bit for bit.
 // kCount: count-only variant (no voxel traffic) giving N_upd / N_col, the
 // algorithmic-byte inputs of the roofline.
 template <bool kCount>
@@ -619,13 +628,16 @@ __global__ __launch_bounds__(256) void k_integrate(VolView v, LevelGeom g,
   const int lane = threadIdx.x & 63;
   const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (tile >= v.tiles_x * v.tiles_y) return;
+  const int chunk = blockIdx.y, nchunk = gridDim.y;
   const int x = (tile % v.tiles_x) * 8 + (lane & 7);
   const int y = (tile / v.tiles_x) * 8 + (lane >> 3);
   const size_t base = (size_t)tile * 64 + lane;
   const int mode = st->mode;
   if (mode == MODE_FAIL) {  // reset(): whole volume zeroed (A5 D)
     if (kCount) return;
-    for (int z = 0; z < v.Z; ++z) {
+    const int z0 = (int)((long long)v.Z * chunk / nchunk);
+    const int z1 = (int)((long long)v.Z * (chunk + 1) / nchunk);
+    for (int z = z0; z < z1; ++z) {
       const size_t i = base + (size_t)z * v.slice;
       v.tsdf[i] = 0;
       v.weight[i] = 0;
@@ -661,35 +673,36 @@ __global__ __launch_bounds__(256) void k_integrate(VolView v, LevelGeom g,
   const int zlo = max(1, (int)floor(lo) - 2);
   const int zhi = min(v.Z - 1, (int)ceil(hi) + 2);
   if (zhi < zlo) return;
+  const int len = zhi - zlo + 1;
+  const int za = zlo + (int)((long long)len * chunk / nchunk);
+  const int zb = zlo + (int)((long long)len * (chunk + 1) / nchunk) - 1;
+  if (zb < za) return;
 
   const float trunc = v.trunc;
   const float thres_color = trunc / 2;
   unsigned cu = 0, cc = 0;
   int z = 1;
-  for (; z < zlo; ++z) vc = add(vc, zs);
+#pragma unroll 8
+  for (; z < za; ++z) vc = add(vc, zs);
   // Batches of kB voxels: projections, then the kB depth gathers, then the
   // voxel loads of the batch are issued back to back (memory-level
   // parallelism); each voxel's arithmetic is exactly the reference's.
-  constexpr int kB = 8;
-  for (; z <= zhi; z += kB) {
-    float sdf[kB];
+  constexpr int kB = 4;
+  for (; z <= zb; z += kB) {
+    float sdf[kB], n2[kB];
     int pix[kB];
     bool ok[kB];
-    f3 vcj[kB];
+    // Branch-free: both projections, the depth gathers and sdf are computed
+    // for every voxel of the batch (results of voxels the reference skips are
+    // discarded by ok[]), so the kB division chains interleave.
 #pragma unroll
     for (int j = 0; j < kB; ++j) {
       vc = add(vc, zs);
-      vcj[j] = vc;
-      ok[j] = false;
-      pix[j] = 0;
-      if (z + j <= zhi && vc.z > 0) {
-        const int u = f2i_rn((vc.x / vc.z) * g.fx + g.cx);
-        const int vv = f2i_rn((vc.y / vc.z) * g.fy + g.cy);
-        if (!(u < 0 || u >= g.w || vv < 0 || vv >= g.h)) {
-          pix[j] = vv * g.w + u;
-          ok[j] = true;
-        }
-      }
+      n2[j] = dot(vc, vc);
+      const int u = f2i_rn((vc.x / vc.z) * g.fx + g.cx);
+      const int vv = f2i_rn((vc.y / vc.z) * g.fy + g.cy);
+      ok[j] = (z + j <= zb) & (vc.z > 0) & (u >= 0) & (u < g.w) & (vv >= 0) & (vv < g.h);
+      pix[j] = ok[j] ? vv * g.w + u : 0;
     }
     // Loads are issued unconditionally (inactive lanes read a dummy element
     // that every such lane shares, so they add no traffic): a predicated load
@@ -697,18 +710,13 @@ __global__ __launch_bounds__(256) void k_integrate(VolView v, LevelGeom g,
     float dep[kB], il[kB];
 #pragma unroll
     for (int j = 0; j < kB; ++j) {
-      dep[j] = dmap[ok[j] ? pix[j] : 0];
-      il[j] = invl[ok[j] ? pix[j] : 0];
+      dep[j] = dmap[pix[j]];
+      il[j] = invl[pix[j]];
     }
 #pragma unroll
     for (int j = 0; j < kB; ++j) {
-      if (ok[j] && dep[j] > 0) {
-        sdf[j] = -(il[j] * sqrtf(dot(vcj[j], vcj[j])) - dep[j]);
-        ok[j] = sdf[j] >= -trunc;
-      } else {
-        ok[j] = false;
-        sdf[j] = 0.f;
-      }
+      sdf[j] = -(il[j] * sqrtf(n2[j]) - dep[j]);
+      ok[j] = ok[j] & (dep[j] > 0) & (sdf[j] >= -trunc);
     }
     if (kCount) {
 #pragma unroll
@@ -720,18 +728,11 @@ __global__ __launch_bounds__(256) void k_integrate(VolView v, LevelGeom g,
       continue;
     }
     int16_t t0[kB], w0[kB];
-    uint32_t c0[kB], px0[kB];
-    bool band[kB];
 #pragma unroll
     for (int j = 0; j < kB; ++j) {
       const size_t i = ok[j] ? base + (size_t)(z + j) * v.slice : 0;
-      band[j] = ok[j] && sdf[j] <= thres_color && sdf[j] >= -thres_color;
-      const size_t ib = band[j] ? i : 0;
-      const size_t pb = band[j] ? 3 * (size_t)pix[j] : 0;
       t0[j] = v.tsdf[i];
       w0[j] = v.weight[i];
-      c0[j] = v.rgb[ib];
-      px0[j] = (uint32_t)bgr[pb] | ((uint32_t)bgr[pb + 1] << 8) | ((uint32_t)bgr[pb + 2] << 16);
     }
 #pragma unroll
     for (int j = 0; j < kB; ++j) {
@@ -745,25 +746,28 @@ __global__ __launch_bounds__(256) void k_integrate(VolView v, LevelGeom g,
           div_rn(fmaf(pre_t, (float)pre_w, ts), (float)(pre_w + 1), rtab[pre_w + 1]);
       int q = (int)(new_t * (float)kShortMax);
       q = max(-kShortMax, min(kShortMax, q));
-      v.tsdf[i] = (int16_t)q;
-      v.weight[i] = (int16_t)new_w;
-      if (band[j]) {
+      // saturated voxels (w = 64 at a tsdf fixed point) keep their values:
+      // skipping those stores changes nothing and saves write bandwidth
+      if (q != t0[j]) v.tsdf[i] = (int16_t)q;
+      if (new_w != pre_w) v.weight[i] = (int16_t)new_w;
+      if (sdf[j] <= thres_color && sdf[j] >= -thres_color) {  // colour band (rare)
+        const uint32_t c0 = v.rgb[i];
+        const uint8_t *px = bgr + 3 * (size_t)pix[j];
         const float c = (float)(new_w + 1);
         const float rc = rtab[new_w + 1];
         uint32_t out = 0u;
 #pragma unroll
         for (int ch = 0; ch < 3; ++ch) {
-          const int m0 = (int)((c0[j] >> (8 * ch)) & 0xffu);
-          const int pc = (int)((px0[j] >> (8 * ch)) & 0xffu);
-          const float m = (float)(new_w * m0 + pc);
+          const int m0 = (int)((c0 >> (8 * ch)) & 0xffu);
+          const float m = (float)(new_w * m0 + (int)px[ch]);
           out |= (uint32_t)(uint8_t)div_rn(m, c, rc) << (8 * ch);
         }
-        v.rgb[i] = out;
+        if (out != c0) v.rgb[i] = out;
       }
     }
   }
   if (kCount) {
-    const int sh = blockIdx.x % 16;
+    const int sh = (blockIdx.x + blockIdx.y) % 16;
     atomicAdd(&counters[2 * sh], (unsigned long long)cu);
     atomicAdd(&counters[2 * sh + 1], (unsigned long long)cc);
   }
@@ -825,7 +829,7 @@ __device__ f3 compute_normal(const VolView &v, const RayConsts &rc, f3 p) {
 
 // One wave = an 8x8 pixel tile (rays of a wave sample neighbouring voxels).
 // BOOT frames copy the measured level-0 maps instead (kinectfusion.cpp:88-89).
-__global__ __launch_bounds__(256) void k_raycast(VolView v, LevelGeom g, RayConsts rc,
+__global__ __launch_bounds__(256, 5) void k_raycast(VolView v, LevelGeom g, RayConsts rc,
                                                  FrameView cur, FrameView prev,
                                                  const DevState *__restrict__ st) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -871,7 +875,6 @@ __global__ __launch_bounds__(256) void k_raycast(VolView v, LevelGeom g, RayCons
     int sprev = isnan(tprev) ? 0 : (tprev > 0.f ? 1 : (tprev < 0.f ? -1 : 0));
     while (__any(live)) {
       int16_t raw[kR];
-      float rlv[kR];
       bool val[kR];
       int je = kR;
       float rl = ray_len;
@@ -887,7 +890,6 @@ __global__ __launch_bounds__(256) void k_raycast(VolView v, LevelGeom g, RayCons
         const int iz = f2i_rn(nextp.z * rc.vs_inv.z);
         val[j] = a && !(ix >= v.X - 1 || iy >= v.Y - 1 || iz >= v.Z - 1 || ix < 1 || iy < 1 || iz < 1);
         raw[j] = v.tsdf[val[j] ? vox_index(v, ix, iy, iz) : 0];
-        rlv[j] = rl;
         rl = a ? rl + rc.step : rl;
       }
       unsigned ev = 0u, hitm = 0u;
@@ -911,15 +913,15 @@ __global__ __launch_bounds__(256) void k_raycast(VolView v, LevelGeom g, RayCons
             live = false;
             pend = 0u;
           } else {
-            float tc = tfirst, tn = 0.f, rj = 0.f;
+            // sample j0's ray_len: replay the batch's adds (event samples
+            // always lie before je, where every step added rc.step)
+            float tc = tfirst, tn = 0.f, rj = ray_len;
 #pragma unroll
             for (int j = 0; j < kR; ++j) {
               const float tj = (float)raw[j] * kDivShortMax;
               if (j + 1 == j0) tc = tj;
-              if (j == j0) {
-                tn = tj;
-                rj = rlv[j];
-              }
+              if (j == j0) tn = tj;
+              if (j < j0) rj += rc.step;
             }
             const float Ts = rj - (v.vs[0] * tc) / (tc - tn);  // A3 (R)
             const f3 vertex = add(org, scl(dir, Ts));
@@ -1144,7 +1146,9 @@ void launch_integrate(hipStream_t s, VolView v, LevelGeom g0, const float *dmap,
                       const uint8_t *bgr, const float *inv_lambda, const DevState *st,
                       unsigned long long *counters) {
   const int tiles = v.tiles_x * v.tiles_y;
-  dim3 grd((tiles + 3) / 4);
+  // z-chunks so that >= 16 waves per SIMD exist (16384 waves on 1024 SIMDs)
+  const int nchunk = std::max(1, std::min(8, (16384 + tiles - 1) / tiles));
+  dim3 grd((tiles + 3) / 4, nchunk);
   if (counters)
     hipLaunchKernelGGL(k_integrate<true>, grd, dim3(256), 0, s, v, g0, dmap, bgr, inv_lambda, st,
                        counters);

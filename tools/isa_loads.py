@@ -10,7 +10,7 @@ for m in re.finditer(r"^(_ZN3kfx\S+):\s", s, re.M):
     name = m.group(1)
     if not any(p in name for p in pats):
         continue
-    body = s[m.end():s.find("s_endpgm", m.end())]
+    body = s[m.end():s.find(".Lfunc_end", m.end())]
     lines = [l.strip() for l in body.splitlines() if l.startswith("\t") and not l.strip().startswith((".", ";"))]
     seq = []
     for l in lines:
