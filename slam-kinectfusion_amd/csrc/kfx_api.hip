@@ -92,6 +92,7 @@ struct kfx_ctx {
   unsigned long long *icp_shards = nullptr;  // 8 x 27 int64 + ticket (self-resetting)
   unsigned *icp_ticket = nullptr;
   unsigned long long *counters = nullptr;
+  float *xpose = nullptr;  // explicit stage poses (21 floats: pose R,t + Rinv)
   std::vector<void *> allocs;
 
   float *staged_depth = nullptr;
@@ -100,7 +101,9 @@ struct kfx_ctx {
 
   bool graph_mode = true;
   bool profiling = false;
-  hipGraphExec_t graph[2] = {nullptr, nullptr};  // [u16 input]
+  hipGraphExec_t graph[2] = {nullptr, nullptr};  // [u16 input], inputs in raw[0]/bgr
+  std::vector<hipGraphExec_t> staged_graph;       // one per staged frame (reads it in place)
+  const uint8_t *last_bgr = nullptr;              // colour the last frame integrated
   hipEvent_t ev[5]{};
   float stage_ms[5]{};
   int pending = 0;      // frames enqueued since the last host sync
@@ -132,26 +135,39 @@ void destroy_graphs(kfx_ctx *c) {
       (void)hipGraphExecDestroy(gx);
       gx = nullptr;
     }
+  for (auto &gx : c->staged_graph)
+    if (gx) {
+      (void)hipGraphExecDestroy(gx);
+      gx = nullptr;
+    }
 }
+
+// Frame input: depth (f32 mm, or u16 mm) and BGR8 colour, in device memory.
+struct FrameInput {
+  const float *d32;
+  const uint16_t *d16;
+  const uint8_t *bgr;
+};
 
 // The per-frame launch sequence (kinectfusion.cpp:78-127 with the frame-1 and
 // failure branches resolved on the device).  ev != nullptr records stage events.
-void enqueue_frame(kfx_ctx *c, bool u16, bool events) {
+void enqueue_frame(kfx_ctx *c, FrameInput in, bool events) {
   hipStream_t s = c->stream;
   if (events) (void)hipEventRecord(c->ev[0], s);
   // imageProcess (kinectfusion.cpp:48-76)
+  const float *raw[kMaxLevels];
+  for (int l = 0; l < kMaxLevels; ++l) raw[l] = c->raw[l];
+  raw[0] = in.d32;
   if (c->L > 1) {
-    launch_pyr_down(s, c->raw[0], u16 ? c->raw0_u16 : nullptr, c->g[0].w, c->g[0].h, c->raw[1],
-                    c->st);
+    launch_pyr_down(s, in.d32, in.d16, c->g[0].w, c->g[0].h, c->raw[1], c->st);
     for (int l = 2; l < c->L; ++l)
       launch_pyr_down(s, c->raw[l - 1], nullptr, c->g[l - 1].w, c->g[l - 1].h, c->raw[l], nullptr);
   } else {
     launch_frame_begin(s, c->st);
   }
-  launch_bilateral_vertex(s, c->L, c->raw, u16 ? c->raw0_u16 : nullptr, c->g, c->cur,
-                          c->p.bfilter_kernel_size, c->p.bfilter_color_sigma,
-                          c->p.bfilter_spatial_sigma, c->p.dfilter_dist, c->st);
-  launch_normals(s, c->L, c->g, c->cur);
+  launch_preprocess_maps(s, c->L, raw, in.d16, c->g, c->cur, c->p.bfilter_kernel_size,
+                         c->p.bfilter_color_sigma, c->p.bfilter_spatial_sigma, c->p.dfilter_dist,
+                         c->st);
   if (events) (void)hipEventRecord(c->ev[1], s);
   // ICPRegistration::rigidTransform (icp_registration.cpp:16-46)
   for (int level = c->L - 1; level >= 0; --level) {
@@ -160,21 +176,21 @@ void enqueue_frame(kfx_ctx *c, bool u16, bool events) {
                  c->prev.n[level], c->p.icp_dist_threshold, c->angle_thr, c->st, c->icp_shards,
                  c->icp_ticket, 0, 1);
   }
-  launch_commit(s, c->st, c->pose_log, to_dev(c->p.volu_pose));
   if (events) (void)hipEventRecord(c->ev[2], s);
-  launch_integrate(s, c->vol, c->g[0], c->cur.d[0], c->bgr, c->inv_lambda, c->st, nullptr);
+  launch_integrate(s, c->vol, c->g[0], c->cur.d[0], in.bgr, c->inv_lambda, c->st, c->pose_log,
+                   to_dev(c->p.volu_pose), nullptr, nullptr);
   if (events) (void)hipEventRecord(c->ev[3], s);
-  launch_raycast(s, c->vol, c->g[0], c->cur, c->prev, c->st);
-  launch_resize(s, c->L, c->g, c->cur, c->prev, c->st);
+  launch_raycast(s, c->vol, c->L, c->g, c->cur, c->prev, c->st, c->pose_log,
+                 to_dev(c->p.volu_pose), nullptr);
   if (events) (void)hipEventRecord(c->ev[4], s);
 }
 
-int build_graph(kfx_ctx *c, bool u16) {
+int build_graph(kfx_ctx *c, FrameInput in, hipGraphExec_t *out) {
   hipGraph_t graph = nullptr;
   HIPCHK(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-  enqueue_frame(c, u16, false);
+  enqueue_frame(c, in, false);
   HIPCHK(hipStreamEndCapture(c->stream, &graph));
-  hipError_t e = hipGraphInstantiate(&c->graph[u16 ? 1 : 0], graph, nullptr, nullptr, 0);
+  hipError_t e = hipGraphInstantiate(out, graph, nullptr, nullptr, 0);
   (void)hipGraphDestroy(graph);
   if (e != hipSuccess) return set_err(KFX_ERR_HIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(e));
   return KFX_OK;
@@ -216,29 +232,30 @@ int ensure_pose_capacity(kfx_ctx *c, int more) {
   c->pose_cap = ncap;
   r = write_field(c, offsetof(DevState, pose_cap), ncap);
   if (r) return r;
-  destroy_graphs(c);  // the commit node holds the old pointer
+  destroy_graphs(c);  // the integrate/raycast nodes hold the old pointer
   return KFX_OK;
 }
 
-int run_frame(kfx_ctx *c, bool u16) {
+// graph: the cached executable for this input (built on first use), or null
+int run_frame(kfx_ctx *c, FrameInput in, hipGraphExec_t *graph) {
   int r = ensure_pose_capacity(c, 1);
   if (r) return r;
+  c->last_bgr = in.bgr;
   if (c->profiling) {
-    enqueue_frame(c, u16, true);
+    enqueue_frame(c, in, true);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventSynchronize(c->ev[4]));
     for (int i = 0; i < 4; ++i) HIPCHK(hipEventElapsedTime(&c->stage_ms[i], c->ev[i], c->ev[i + 1]));
     HIPCHK(hipEventElapsedTime(&c->stage_ms[4], c->ev[0], c->ev[4]));
     // stage order in the events: preprocess, icp(+commit), integrate, raycast(+resize)
-  } else if (c->graph_mode) {
-    hipGraphExec_t &gx = c->graph[u16 ? 1 : 0];
-    if (!gx) {
-      r = build_graph(c, u16);
+  } else if (c->graph_mode && graph) {
+    if (!*graph) {
+      r = build_graph(c, in, graph);
       if (r) return r;
     }
-    HIPCHK(hipGraphLaunch(gx, c->stream));
+    HIPCHK(hipGraphLaunch(*graph, c->stream));
   } else {
-    enqueue_frame(c, u16, false);
+    enqueue_frame(c, in, false);
     HIPCHK(hipGetLastError());
   }
   c->pending += 1;
@@ -249,7 +266,7 @@ int finish_frame(kfx_ctx *c) {
   DevState s;
   int r = read_state(c, &s);
   if (r) return r;
-  return s.mode == MODE_FAIL ? KFX_TRACKING_LOST : KFX_OK;
+  return s.last_fail ? KFX_TRACKING_LOST : KFX_OK;
 }
 
 VolView make_vol(const kfx_params &p) {
@@ -360,6 +377,9 @@ int kfx_create(const kfx_intrinsics *intr, const kfx_params *params, int device,
   if (p.bfilter_kernel_size < 1 || p.bfilter_kernel_size > 15)
     return set_err(KFX_ERR_ARG, "bfilter_kernel_size must be 1..15");
   for (int l = 0; l < p.pyramid_height; ++l)
+    if ((intr->width >> l) <= p.bfilter_kernel_size / 2 || (intr->height >> l) <= p.bfilter_kernel_size / 2)
+      return set_err(KFX_ERR_ARG, "pyramid level smaller than the bilateral radius");
+  for (int l = 0; l < p.pyramid_height; ++l)
     if (p.icp_iter_count[l] < 0) return set_err(KFX_ERR_ARG, "negative icp_iter_count");
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
@@ -409,6 +429,7 @@ int kfx_create(const kfx_intrinsics *intr, const kfx_params *params, int device,
     return fail(r);
   c->icp_ticket = reinterpret_cast<unsigned *>(c->icp_shards + 8 * 27);
   if ((r = dalloc(c, (void **)&c->counters, sizeof(unsigned long long) * 32))) return fail(r);
+  if ((r = dalloc(c, (void **)&c->xpose, sizeof(float) * 32))) return fail(r);
   launch_inv_lambda(c->stream, c->g[0], c->inv_lambda);
   if ((r = do_reset(c))) return fail(r);
   *out = c;
@@ -442,7 +463,7 @@ int kfx_pipeline(kfx_ctx *c, const uint8_t *bgr, const float *depth_mm) {
   const size_t np = (size_t)c->intr.width * c->intr.height;
   HIPCHK(hipMemcpyAsync(c->raw[0], depth_mm, np * 4, hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipMemcpyAsync(c->bgr, bgr, np * 3, hipMemcpyHostToDevice, c->stream));
-  if ((r = run_frame(c, false))) return r;
+  if ((r = run_frame(c, {c->raw[0], nullptr, c->bgr}, &c->graph[0]))) return r;
   return finish_frame(c);
 }
 
@@ -453,7 +474,7 @@ int kfx_pipeline_u16(kfx_ctx *c, const uint8_t *bgr, const uint16_t *depth_mm) {
   const size_t np = (size_t)c->intr.width * c->intr.height;
   HIPCHK(hipMemcpyAsync(c->raw0_u16, depth_mm, np * 2, hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipMemcpyAsync(c->bgr, bgr, np * 3, hipMemcpyHostToDevice, c->stream));
-  if ((r = run_frame(c, true))) return r;
+  if ((r = run_frame(c, {c->raw[0], c->raw0_u16, c->bgr}, &c->graph[1]))) return r;
   return finish_frame(c);
 }
 
@@ -471,6 +492,8 @@ int kfx_stage_frames(kfx_ctx *c, int n, const uint8_t *bgr, const float *depth_m
   c->staged_depth = nullptr;
   c->staged_bgr = nullptr;
   c->n_staged = 0;
+  destroy_graphs(c);
+  c->staged_graph.assign(n, nullptr);
   if ((r = dalloc(c, (void **)&c->staged_depth, np * 4 * (size_t)n))) return r;
   if ((r = dalloc(c, (void **)&c->staged_bgr, np * 3 * (size_t)n))) return r;
   HIPCHK(hipMemcpyAsync(c->staged_depth, depth_mm, np * 4 * (size_t)n, hipMemcpyHostToDevice,
@@ -486,11 +509,9 @@ int kfx_pipeline_staged(kfx_ctx *c, int idx) {
   if (r) return r;
   if (idx < 0 || idx >= c->n_staged) return set_err(KFX_ERR_ARG, "staged frame index out of range");
   const size_t np = (size_t)c->intr.width * c->intr.height;
-  HIPCHK(hipMemcpyAsync(c->raw[0], c->staged_depth + np * idx, np * 4, hipMemcpyDeviceToDevice,
-                        c->stream));
-  HIPCHK(hipMemcpyAsync(c->bgr, c->staged_bgr + np * 3 * idx, np * 3, hipMemcpyDeviceToDevice,
-                        c->stream));
-  return run_frame(c, false);
+  // the captured graph for this staged frame reads it in place (no copy)
+  return run_frame(c, {c->staged_depth + np * idx, nullptr, c->staged_bgr + np * 3 * idx},
+                   &c->staged_graph[idx]);
 }
 
 int kfx_synchronize(kfx_ctx *c) {
@@ -703,15 +724,15 @@ int kfx_stage_preprocess(kfx_ctx *c, const uint8_t *bgr, const float *depth_mm) 
   const size_t np = (size_t)c->intr.width * c->intr.height;
   HIPCHK(hipMemcpyAsync(c->raw[0], depth_mm, np * 4, hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipMemcpyAsync(c->bgr, bgr, np * 3, hipMemcpyHostToDevice, c->stream));
+  c->last_bgr = c->bgr;
   HIPCHK(hipMemsetAsync(reinterpret_cast<char *>(c->st) + offsetof(DevState, dmax_bits), 0,
                         sizeof(((DevState *)nullptr)->dmax_bits), c->stream));
   for (int l = 1; l < c->L; ++l)
     launch_pyr_down(c->stream, c->raw[l - 1], nullptr, c->g[l - 1].w, c->g[l - 1].h, c->raw[l],
                     nullptr);
-  launch_bilateral_vertex(c->stream, c->L, c->raw, nullptr, c->g, c->cur, c->p.bfilter_kernel_size,
-                          c->p.bfilter_color_sigma, c->p.bfilter_spatial_sigma, c->p.dfilter_dist,
-                          c->st);
-  launch_normals(c->stream, c->L, c->g, c->cur);
+  launch_preprocess_maps(c->stream, c->L, c->raw, nullptr, c->g, c->cur,
+                         c->p.bfilter_kernel_size, c->p.bfilter_color_sigma,
+                         c->p.bfilter_spatial_sigma, c->p.dfilter_dist, c->st);
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(c->stream));
   return KFX_OK;
@@ -757,10 +778,10 @@ int kfx_stage_icp(kfx_ctx *c, kfx_pose *out) {
   return failed ? KFX_TRACKING_LOST : KFX_OK;
 }
 
-static int integrate_counts_impl(kfx_ctx *c, int64_t *nu, int64_t *nc) {
+static int integrate_counts_impl(kfx_ctx *c, int64_t *nu, int64_t *nc, const float *xpose) {
   HIPCHK(hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * 32, c->stream));
-  launch_integrate(c->stream, c->vol, c->g[0], c->cur.d[0], c->bgr, c->inv_lambda, c->st,
-                   c->counters);
+  launch_integrate(c->stream, c->vol, c->g[0], c->cur.d[0], c->last_bgr ? c->last_bgr : c->bgr,
+                   c->inv_lambda, c->st, c->pose_log, to_dev(c->p.volu_pose), xpose, c->counters);
   HIPCHK(hipGetLastError());
   unsigned long long h[32];
   HIPCHK(hipMemcpyAsync(h, c->counters, sizeof(h), hipMemcpyDeviceToHost, c->stream));
@@ -779,17 +800,15 @@ int kfx_stage_integrate(kfx_ctx *c, const kfx_pose *vol2cam, int64_t *nu, int64_
   int r = check_ctx(c);
   if (r) return r;
   if (!vol2cam) return set_err(KFX_ERR_ARG, "null pose");
-  DevState s0;
-  if ((r = read_state(c, &s0))) return r;
-  DevState s = s0;
-  s.mode = MODE_TRACK;
-  s.vol2cam = to_dev(*vol2cam);
-  HIPCHK(hipMemcpyAsync(c->st, &s, sizeof(s), hipMemcpyHostToDevice, c->stream));
+  float xp[12];
+  std::memcpy(xp, vol2cam->R, sizeof(float) * 9);
+  std::memcpy(xp + 9, vol2cam->t, sizeof(float) * 3);
+  HIPCHK(hipMemcpyAsync(c->xpose, xp, sizeof(xp), hipMemcpyHostToDevice, c->stream));
   if (nu || nc)
-    if ((r = integrate_counts_impl(c, nu, nc))) return r;
-  launch_integrate(c->stream, c->vol, c->g[0], c->cur.d[0], c->bgr, c->inv_lambda, c->st, nullptr);
+    if ((r = integrate_counts_impl(c, nu, nc, c->xpose))) return r;
+  launch_integrate(c->stream, c->vol, c->g[0], c->cur.d[0], c->bgr, c->inv_lambda, c->st,
+                   c->pose_log, to_dev(c->p.volu_pose), c->xpose, nullptr);
   HIPCHK(hipGetLastError());
-  HIPCHK(hipMemcpyAsync(c->st, &s0, sizeof(s0), hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   return KFX_OK;
 }
@@ -797,24 +816,21 @@ int kfx_stage_integrate(kfx_ctx *c, const kfx_pose *vol2cam, int64_t *nu, int64_
 int kfx_integrate_counts(kfx_ctx *c, int64_t *nu, int64_t *nc) {
   int r = check_ctx(c);
   if (r) return r;
-  return integrate_counts_impl(c, nu, nc);
+  return integrate_counts_impl(c, nu, nc, nullptr);
 }
 
 int kfx_stage_raycast(kfx_ctx *c, const kfx_pose *cam2vol, const float Rinv[9]) {
   int r = check_ctx(c);
   if (r) return r;
   if (!cam2vol || !Rinv) return set_err(KFX_ERR_ARG, "null argument");
-  DevState s0;
-  if ((r = read_state(c, &s0))) return r;
-  DevState s = s0;
-  s.mode = MODE_TRACK;
-  s.cam2vol = to_dev(*cam2vol);
-  std::memcpy(s.Rinv, Rinv, sizeof(s.Rinv));
-  HIPCHK(hipMemcpyAsync(c->st, &s, sizeof(s), hipMemcpyHostToDevice, c->stream));
-  launch_raycast(c->stream, c->vol, c->g[0], c->cur, c->prev, c->st);
-  launch_resize(c->stream, c->L, c->g, c->cur, c->prev, c->st);
+  float xp[21];
+  std::memcpy(xp, cam2vol->R, sizeof(float) * 9);
+  std::memcpy(xp + 9, cam2vol->t, sizeof(float) * 3);
+  std::memcpy(xp + 12, Rinv, sizeof(float) * 9);
+  HIPCHK(hipMemcpyAsync(c->xpose, xp, sizeof(xp), hipMemcpyHostToDevice, c->stream));
+  launch_raycast(c->stream, c->vol, c->L, c->g, c->cur, c->prev, c->st, c->pose_log,
+                 to_dev(c->p.volu_pose), c->xpose);
   HIPCHK(hipGetLastError());
-  HIPCHK(hipMemcpyAsync(c->st, &s0, sizeof(s0), hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   return KFX_OK;
 }

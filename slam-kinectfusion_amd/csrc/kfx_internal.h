@@ -26,13 +26,10 @@ struct DevState {
   int n_poses;          // pose_record.size()
   int pose_cap;         // capacity of the pose log
   int pose_overflow;
-  int pad0[2];
+  int n_base;           // n_poses at frame start (read-only during the frame)
+  int last_fail;        // 1 if the last frame hit the ICP det check (reset applied)
   unsigned dmax_bits[16];  // max valid level-0 depth of this frame (float bits), sharded
   DevPose icp_pose;     // camera_pose inside rigidTransform
-  DevPose vol2cam;      // TSDFVolume::integrate pose (tsdf_volume.cpp:50)
-  DevPose cam2vol;      // TSDFVolume::raycast pose (tsdf_volume.cpp:59)
-  float Rinv[9];        // cam2vol.rotation().inv() (D: transpose)
-  float pad1[3];
   long long sums[27];   // last ICP sums (test seam)
   double x[6];          // last ICP increment
 };
@@ -67,25 +64,29 @@ struct FrameView {
 void launch_frame_begin(hipStream_t s, DevState *st);
 void launch_pyr_down(hipStream_t s, const float *src, const uint16_t *src16, int w, int h,
                      float *dst, DevState *st_begin);
-void launch_bilateral_vertex(hipStream_t s, int levels, const float *const raw[kMaxLevels],
-                             const uint16_t *raw0_u16, const LevelGeom *g, FrameView cur,
-                             int ksz, float sigma_color, float sigma_spatial, float max_dist,
-                             DevState *st);
-void launch_normals(hipStream_t s, int levels, const LevelGeom *g, FrameView cur);
+// bilateral + truncation + vertex + normal maps, all levels (raw[l] = raw mm)
+void launch_preprocess_maps(hipStream_t s, int levels, const float *const raw[kMaxLevels],
+                            const uint16_t *raw0_u16, const LevelGeom *g, FrameView cur, int ksz,
+                            float sigma_color, float sigma_spatial, float max_dist, DevState *st);
 int icp_blocks(const LevelGeom &g);
 // one ICP iteration (rigid_icp.cu:135-169 + icp_registration.cpp:33-42) in a
 // single launch; shards = 8 x 27 int64 zeroed, ticket zeroed (both self-reset)
 void launch_icp(hipStream_t s, const LevelGeom &g, const float *cv, const float *cn,
                 const float *pv, const float *pn, float dist_thr, float angle_thr, DevState *st,
                 unsigned long long *shards, unsigned *ticket, int force, int update);
-void launch_commit(hipStream_t s, DevState *st, DevPose *pose_log, DevPose volume_pose);
+// The frame's global pose, the integrate/raycast poses and the
+// kinectfusion.cpp:84-104 bookkeeping are derived inside these kernels from
+// DevState + pose log (no separate commit launch).  `xpose` (device, 12 or 21
+// floats: pose [, Rinv]) overrides them for the stage seams; bookkeeping is
+// then skipped.
 void launch_integrate(hipStream_t s, VolView v, LevelGeom g0, const float *dmap,
-                      const uint8_t *bgr, const float *inv_lambda, const DevState *st,
+                      const uint8_t *bgr, const float *inv_lambda, DevState *st, DevPose *log,
+                      DevPose vpose, const float *xpose,
                       unsigned long long *counters /* non-null: count-only, 32 words */);
-void launch_raycast(hipStream_t s, VolView v, LevelGeom g0, FrameView cur, FrameView prev,
-                    const DevState *st);
-void launch_resize(hipStream_t s, int levels, const LevelGeom *g, FrameView cur, FrameView prev,
-                   const DevState *st);
+// raycast of level 0 + resizePointsNormals of levels >= 1 in one launch
+void launch_raycast(hipStream_t s, VolView v, int levels, const LevelGeom *g, FrameView cur,
+                    FrameView prev, const DevState *st, const DevPose *log, DevPose vpose,
+                    const float *xpose);
 void launch_inv_lambda(hipStream_t s, LevelGeom g0, float *inv_lambda);
 void launch_export_records(hipStream_t s, VolView v, int z0, int nz, uint64_t *dst);
 void launch_import_records(hipStream_t s, VolView v, int z0, int nz, const uint64_t *src);

@@ -127,6 +127,7 @@ __device__ DevPose pose_inv(const DevPose &a) {
 __device__ __forceinline__ void frame_begin(DevState *st) {
   st->mode = (st->frame_count == 1) ? MODE_BOOT : MODE_TRACK;
   st->icp_fail = 0;
+  st->n_base = st->n_poses;
   st->icp_pose = pose_identity();
   for (int i = 0; i < kDmaxShards; ++i) st->dmax_bits[i] = 0u;
 }
@@ -210,6 +211,7 @@ struct BilatArgs {
   const uint16_t *raw0_u16;
   float *d[kMaxLevels];
   float *v[kMaxLevels];
+  float *n[kMaxLevels];
   int ksz;
   float s_half, c_half;
   float max_dist;
@@ -217,51 +219,94 @@ struct BilatArgs {
 
 // cv::cuda::bilateralFilter (kinectfusion.cpp:57-65, A1 D: out of place) +
 // kernal_depthTruncation (image_process.cu:8-17) + kernel_getVertexmap
-// (image_process.cu:29-43), fused, all levels in one launch.  Level 0 also
-// reduces the frame's max depth (conservative integrate bound).
-__global__ __launch_bounds__(256) void k_bilateral_vertex(BilatArgs a, DevState *st) {
+// (image_process.cu:29-43) + kernel_getNormalmap (image_process.cu:57-84),
+// fused, all levels in one launch.  A block owns a 16x16 tile: it stages the
+// raw tile with a (r+1)-pixel halo in LDS (halo coordinates reflect-101
+// mapped, exactly the taps the filter reads), filters the 18x18 ring the
+// normals need, then computes normals of the 16x16 core from LDS.  Border
+// normals are written 0 (the value Frame::reset leaves, types.hpp:53-62).
+// Level 0 also reduces the frame's max depth (conservative integrate bound).
+constexpr int kPreMaxR = 7;                    // ksz <= 15
+constexpr int kPreRaw = 16 + 2 * (kPreMaxR + 1);  // 32
+__global__ __launch_bounds__(256) void k_preprocess_maps(BilatArgs a, DevState *st) {
   const int l = find_level(a.t, blockIdx.x);
   const int local = blockIdx.x - a.t.off[l];
   const LevelGeom g = a.t.g[l];
-  const int x = (local % a.t.nbx[l]) * 16 + (threadIdx.x & 15);
-  const int y = (local / a.t.nbx[l]) * 16 + (threadIdx.x >> 4);
-  float dval = 0.f;
-  const bool in = x < g.w && y < g.h;
-  if (in) {
-    const float *src = a.raw[l];
-    const uint16_t *src16 = (l == 0) ? a.raw0_u16 : nullptr;
-    auto rd = [&](size_t i) -> float { return src16 ? (float)src16[i] : src[i]; };
-    const float center = rd((size_t)y * g.w + x);
-    const int r = a.ksz / 2;
-    const float r2 = (float)(r * r);
-    float sum1 = 0.f, sum2 = 0.f;
-    for (int cy = y - r; cy < y - r + a.ksz; ++cy) {
-      const size_t row = (size_t)reflect101(cy, g.h) * g.w;
-      for (int cx = x - r; cx < x - r + a.ksz; ++cx) {
-        const float space2 = (float)((x - cx) * (x - cx) + (y - cy) * (y - cy));
-        if (space2 > r2) continue;
-        const float vv = rd(row + reflect101(cx, g.w));
-        const float dd = fabsf(vv - center);
-        const float wgt = det_expf(space2 * a.s_half + (dd * dd) * a.c_half);
-        sum1 = sum1 + wgt * vv;
-        sum2 = sum2 + wgt;
+  const int X0 = (local % a.t.nbx[l]) * 16, Y0 = (local / a.t.nbx[l]) * 16;
+  const int r = a.ksz / 2, H = r + 1, side = 16 + 2 * H;
+  __shared__ float sraw[kPreRaw * kPreRaw];
+  __shared__ float sd[18 * 18];
+  __shared__ f3 sv[18 * 18];
+  const float *src = a.raw[l];
+  const uint16_t *src16 = (l == 0) ? a.raw0_u16 : nullptr;
+  for (int i = threadIdx.x; i < side * side; i += 256) {
+    // taps of in-image pixels reflect once (create checks r < level size);
+    // the clamp only keeps halo cells no output reads inside the image
+    const int yy = min(max(reflect101(Y0 - H + i / side, g.h), 0), g.h - 1);
+    const int xx = min(max(reflect101(X0 - H + i % side, g.w), 0), g.w - 1);
+    const size_t o = (size_t)yy * g.w + xx;
+    sraw[i] = src16 ? (float)src16[o] : src[o];
+  }
+  __syncthreads();
+  // filtered depth + vertex on the 18x18 ring (pixels inside the image)
+  const float r2 = (float)(r * r);
+  for (int i = threadIdx.x; i < 18 * 18; i += 256) {
+    const int py = i / 18, px = i % 18;
+    const int x = X0 - 1 + px, y = Y0 - 1 + py;
+    float dval = 0.f;
+    f3 vtx = {0.f, 0.f, 0.f};
+    if (x >= 0 && x < g.w && y >= 0 && y < g.h) {
+      const int cyl = py + (H - 1), cxl = px + (H - 1);  // this pixel in sraw
+      const float center = sraw[cyl * side + cxl];
+      float sum1 = 0.f, sum2 = 0.f;
+      for (int cy = y - r; cy < y - r + a.ksz; ++cy) {
+        for (int cx = x - r; cx < x - r + a.ksz; ++cx) {
+          const float space2 = (float)((x - cx) * (x - cx) + (y - cy) * (y - cy));
+          if (space2 > r2) continue;
+          const float vv = sraw[(cyl + cy - y) * side + (cxl + cx - x)];
+          const float dd = fabsf(vv - center);
+          const float wgt = det_expf(space2 * a.s_half + (dd * dd) * a.c_half);
+          sum1 = sum1 + wgt * vv;
+          sum2 = sum2 + wgt;
+        }
       }
+      dval = sum1 / sum2;
+      dval *= 0.001f;
+      if (dval > a.max_dist) dval = 0.f;
+      if (isnan(dval))
+        vtx = {0.f, 0.f, 0.f};
+      else
+        vtx = {(dval * ((float)x - g.cx)) / g.fx, (dval * ((float)y - g.cy)) / g.fy, dval};
     }
-    dval = sum1 / sum2;
-    dval *= 0.001f;
-    if (dval > a.max_dist) dval = 0.f;
-    const size_t i = (size_t)y * g.w + x;
-    a.d[l][i] = dval;
-    f3 vtx;
-    if (isnan(dval))
-      vtx = {0.f, 0.f, 0.f};
-    else
-      vtx = {(dval * ((float)x - g.cx)) / g.fx, (dval * ((float)y - g.cy)) / g.fy, dval};
-    st3(a.v[l], i, vtx);
+    sd[i] = dval;
+    sv[i] = vtx;
+  }
+  __syncthreads();
+  const int cx = threadIdx.x & 15, cy = threadIdx.x >> 4;
+  const int x = X0 + cx, y = Y0 + cy;
+  const bool in = x < g.w && y < g.h;
+  const int c = (cy + 1) * 18 + (cx + 1);
+  const float dval = sd[c];
+  if (in) {
+    const size_t o = (size_t)y * g.w + x;
+    a.d[l][o] = dval;
+    st3(a.v[l], o, sv[c]);
+    f3 n = {0.f, 0.f, 0.f};
+    if (x >= 1 && x < g.w - 1 && y >= 1 && y < g.h - 1) {
+      const f3 lf = sv[c - 1], rt = sv[c + 1], up = sv[c - 18], dn = sv[c + 18];
+      if (lf.z == 0 || rt.z == 0 || up.z == 0 || dn.z == 0) {
+        n = {0.f, 0.f, 0.f};
+      } else {
+        n = cross(sub(lf, rt), sub(up, dn));
+        if (n.z > 0) n = scl(n, -1.f);
+      }
+      n = normalized(n);  // 0/0 = NaN when a neighbour is invalid (A8)
+    }
+    st3(a.n[l], o, n);
   }
   if (l == 0) {  // block-uniform
     unsigned m = (in && dval > 0.f) ? __float_as_uint(dval) : 0u;
-    for (int o = 32; o > 0; o >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, o));
+    for (int off = 32; off > 0; off >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, off));
     __shared__ unsigned wm[4];
     if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
     __syncthreads();
@@ -270,38 +315,6 @@ __global__ __launch_bounds__(256) void k_bilateral_vertex(BilatArgs a, DevState 
       if (b) atomicMax(&st->dmax_bits[blockIdx.x % kDmaxShards], b);
     }
   }
-}
-
-struct NormalArgs {
-  LevelTiles t;
-  const float *v[kMaxLevels];
-  float *n[kMaxLevels];
-};
-
-// kernel_getNormalmap (image_process.cu:57-84), all levels; border written 0
-// (the value Frame::reset leaves there, types.hpp:53-62).
-__global__ __launch_bounds__(256) void k_normals(NormalArgs a) {
-  const int l = find_level(a.t, blockIdx.x);
-  const int local = blockIdx.x - a.t.off[l];
-  const LevelGeom g = a.t.g[l];
-  const int x = (local % a.t.nbx[l]) * 16 + (threadIdx.x & 15);
-  const int y = (local / a.t.nbx[l]) * 16 + (threadIdx.x >> 4);
-  if (x >= g.w || y >= g.h) return;
-  const float *vm = a.v[l];
-  const size_t i = (size_t)y * g.w + x;
-  if (x < 1 || x >= g.w - 1 || y < 1 || y >= g.h - 1) {
-    st3(a.n[l], i, {0.f, 0.f, 0.f});
-    return;
-  }
-  const f3 lf = ld3(vm, i - 1), rt = ld3(vm, i + 1), up = ld3(vm, i - g.w), dn = ld3(vm, i + g.w);
-  f3 n;
-  if (lf.z == 0 || rt.z == 0 || up.z == 0 || dn.z == 0) {
-    n = {0.f, 0.f, 0.f};
-  } else {
-    n = cross(sub(lf, rt), sub(up, dn));
-    if (n.z > 0) n = scl(n, -1.f);
-  }
-  st3(a.n[l], i, normalized(n));
 }
 
 // ---------------------------------------------------------------------------
@@ -554,38 +567,36 @@ __device__ int icp_update(const long long *sums, DevPose &pose, double *xo) {
   return 0;
 }
 
-// kinectfusion.cpp:84-104 bookkeeping, single thread: frame-1 bootstrap,
-// tracking failure -> reset() semantics, pose_record push, derived poses for
-// integrate (tsdf_volume.cpp:50) and raycast (tsdf_volume.cpp:59-61).
-__global__ void k_commit(DevState *st, DevPose *log, DevPose vpose) {
-  const int mode = st->mode;
-  if (mode == MODE_BOOT) {
-    const DevPose back = log[st->n_poses - 1];
-    st->vol2cam = pose_mul(pose_inv(back), vpose);
-    st->frame_count += 1;
-  } else if (mode == MODE_TRACK) {
-    if (st->icp_fail) {
-      st->mode = MODE_FAIL;
-      st->frame_count = 1;
-      st->n_poses = 1;
-      log[0] = pose_identity();
+// kinectfusion.cpp:84-104, resolved on the device.  Frame kind: 0 = frame-1
+// bootstrap (integrate at pose_record.back(), copy measured maps), 1 = tracked
+// (pose_record.back() * cam_pose), 2 = ICP failure (reset(), frame dropped).
+__device__ __forceinline__ int frame_kind(const DevState *st) {
+  return st->mode == MODE_BOOT ? 0 : (st->icp_fail ? 2 : 1);
+}
+__device__ __forceinline__ DevPose frame_pose(const DevState *st, const DevPose *log, int kind) {
+  const DevPose back = log[st->n_base - 1];
+  return kind == 0 ? back : pose_mul(back, st->icp_pose);
+}
+// pose_record push / reset (one thread of one block); only fields that no
+// other block of the frame reads are written.
+__device__ void frame_bookkeeping(DevState *st, DevPose *log, int kind, const DevPose &g) {
+  if (kind == 2) {
+    st->frame_count = 1;
+    st->n_poses = 1;
+    log[0] = pose_identity();
+    st->last_fail = 1;
+    return;
+  }
+  if (kind == 1) {
+    if (st->n_base < st->pose_cap) {
+      log[st->n_base] = g;
+      st->n_poses = st->n_base + 1;
     } else {
-      const DevPose g = pose_mul(log[st->n_poses - 1], st->icp_pose);
-      if (st->n_poses < st->pose_cap) {
-        log[st->n_poses] = g;
-        st->n_poses += 1;
-      } else {
-        log[st->pose_cap - 1] = g;
-        st->pose_overflow = 1;
-      }
-      st->vol2cam = pose_mul(pose_inv(g), vpose);
-      const DevPose c2v = pose_mul(pose_inv(vpose), g);
-      st->cam2vol = c2v;
-      for (int i = 0; i < 3; ++i)
-        for (int j = 0; j < 3; ++j) st->Rinv[3 * i + j] = c2v.R[3 * j + i];
-      st->frame_count += 1;
+      st->pose_overflow = 1;
     }
   }
+  st->frame_count += 1;
+  st->last_fail = 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -619,11 +630,30 @@ __global__ __launch_bounds__(256) void k_integrate(VolView v, LevelGeom g,
                                                    const float *__restrict__ dmap,
                                                    const uint8_t *__restrict__ bgr,
                                                    const float *__restrict__ invl,
-                                                   const DevState *__restrict__ st,
+                                                   DevState *__restrict__ st, DevPose *log,
+                                                   DevPose vpose, const float *xpose,
                                                    unsigned long long *counters) {
   // rtab[d] = RN(1/d), d = 1..65: the weight divisors of the running averages
   __shared__ float rtab[66];
+  __shared__ DevPose s_pose;
+  __shared__ int s_kind;
   if (threadIdx.x < 66) rtab[threadIdx.x] = 1.f / (float)max(1, (int)threadIdx.x);
+  if (threadIdx.x == 0) {
+    if (xpose) {  // stage seam: explicit vol2cam
+      s_kind = 1;
+      for (int i = 0; i < 9; ++i) s_pose.R[i] = xpose[i];
+      for (int i = 0; i < 3; ++i) s_pose.t[i] = xpose[9 + i];
+    } else {
+      const int kind = frame_kind(st);
+      s_kind = kind;
+      DevPose gp = pose_identity();
+      if (kind != 2) {
+        gp = frame_pose(st, log, kind);
+        s_pose = pose_mul(pose_inv(gp), vpose);  // tsdf_volume.cpp:50
+      }
+      if (!kCount && blockIdx.x == 0 && blockIdx.y == 0) frame_bookkeeping(st, log, kind, gp);
+    }
+  }
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -632,8 +662,7 @@ __global__ __launch_bounds__(256) void k_integrate(VolView v, LevelGeom g,
   const int x = (tile % v.tiles_x) * 8 + (lane & 7);
   const int y = (tile / v.tiles_x) * 8 + (lane >> 3);
   const size_t base = (size_t)tile * 64 + lane;
-  const int mode = st->mode;
-  if (mode == MODE_FAIL) {  // reset(): whole volume zeroed (A5 D)
+  if (s_kind == 2) {  // reset(): whole volume zeroed (A5 D)
     if (kCount) return;
     const int z0 = (int)((long long)v.Z * chunk / nchunk);
     const int z1 = (int)((long long)v.Z * (chunk + 1) / nchunk);
@@ -645,7 +674,7 @@ __global__ __launch_bounds__(256) void k_integrate(VolView v, LevelGeom g,
     }
     return;
   }
-  const DevPose P = st->vol2cam;
+  const DevPose P = s_pose;
   const f3 vx = {(float)x * v.vs[0], (float)y * v.vs[1], 0.f * v.vs[2]};
   f3 vc = add(rmul(P.R, vx), {P.t[0], P.t[1], P.t[2]});
   const f3 zs = {P.R[2] * v.vs[0], P.R[5] * v.vs[0], P.R[8] * v.vs[0]};
@@ -829,23 +858,73 @@ __device__ f3 compute_normal(const VolView &v, const RayConsts &rc, f3 p) {
 
 // One wave = an 8x8 pixel tile (rays of a wave sample neighbouring voxels).
 // BOOT frames copy the measured level-0 maps instead (kinectfusion.cpp:88-89).
-__global__ __launch_bounds__(256, 5) void k_raycast(VolView v, LevelGeom g, RayConsts rc,
-                                                 FrameView cur, FrameView prev,
-                                                 const DevState *__restrict__ st) {
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int x = blockIdx.x * 16 + (wv & 1) * 8 + (lane & 7);
-  const int y = blockIdx.y * 16 + (wv >> 1) * 8 + (lane >> 3);
-  if (x >= g.w || y >= g.h) return;
-  const size_t o = (size_t)y * g.w + x;
-  const int mode = st->mode;
-  if (mode == MODE_BOOT) {
-    st3(prev.v[0], o, ld3(cur.v[0], o));
-    st3(prev.n[0], o, ld3(cur.n[0], o));
-    return;
+// Blocks are dealt round-robin to the 8 XCDs; remap so that each XCD gets a
+// contiguous band of 16x16 tiles (rays of neighbouring tiles gather the same
+// voxel lines, which then hit in that XCD's L2).  Bijective for any count.
+__device__ __forceinline__ int xcd_remap(int b, int nb) {
+  const int q = nb / 8, r = nb % 8, xcd = b % 8;
+  return xcd * q + min(xcd, r) + b / 8;
+}
+
+template <bool kIdx32>
+__device__ __forceinline__ size_t ray_index(const VolView &v, int x, int y, int z) {
+  if (kIdx32)
+    return (size_t)((unsigned)z * (unsigned)v.slice +
+                    (((unsigned)(y >> 3) * (unsigned)v.tiles_x + (unsigned)(x >> 3)) << 6) +
+                    (unsigned)(((y & 7) << 3) | (x & 7)));
+  return vox_index(v, x, y, z);
+}
+
+struct RayArgs {
+  LevelGeom g[kMaxLevels];
+  int levels;
+};
+
+template <bool kIdx32>
+__global__ __launch_bounds__(256) void k_raycast(VolView v, RayArgs ra, RayConsts rc,
+                                                    FrameView cur, FrameView prev,
+                                                    const DevState *__restrict__ st,
+                                                    const DevPose *__restrict__ log, DevPose vpose,
+                                                    const float *xpose) {
+  // cam2vol = volume_pose^-1 * pose, Rinv = R^T (tsdf_volume.cpp:59-61; D: transpose)
+  __shared__ DevPose s_c2v;
+  __shared__ float s_rinv[9];
+  __shared__ int s_kind;
+  if (threadIdx.x == 0) {
+    if (xpose) {  // stage seam: explicit cam2vol and Rinv
+      s_kind = 1;
+      for (int i = 0; i < 9; ++i) s_c2v.R[i] = xpose[i];
+      for (int i = 0; i < 3; ++i) s_c2v.t[i] = xpose[9 + i];
+      for (int i = 0; i < 9; ++i) s_rinv[i] = xpose[12 + i];
+    } else {
+      const int kind = frame_kind(st);
+      s_kind = kind;
+      if (kind == 1) {
+        const DevPose c2v = pose_mul(pose_inv(vpose), frame_pose(st, log, kind));
+        s_c2v = c2v;
+        for (int i = 0; i < 3; ++i)
+          for (int j = 0; j < 3; ++j) s_rinv[3 * i + j] = c2v.R[3 * j + i];
+      }
+    }
   }
+  __syncthreads();
+  const LevelGeom g = ra.g[0];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int nbx = (g.w + 15) / 16;
+  const int t = xcd_remap(blockIdx.x, gridDim.x);
+  const int tx0 = (t % nbx) * 16, ty0 = (t / nbx) * 16;
+  const int lx = (wv & 1) * 8 + (lane & 7), ly = (wv >> 1) * 8 + (lane >> 3);
+  const int x = tx0 + lx, y = ty0 + ly;
+  const bool inimg = x < g.w && y < g.h;
+  const size_t o = (size_t)y * g.w + x;
+  const int kind = s_kind;
   f3 vout = {0.f, 0.f, 0.f}, nout = {0.f, 0.f, 0.f};
-  if (mode == MODE_TRACK) {  // block-uniform
-    const DevPose P = st->cam2vol;
+  if (kind == 0 && inimg) {  // frame 1: the measured maps become the model maps
+    vout = ld3(cur.v[0], o);
+    nout = ld3(cur.n[0], o);
+  }
+  if (kind == 1) {  // block-uniform
+    const DevPose P = s_c2v;
     const f3 org = {P.t[0], P.t[1], P.t[2]};
     const f3 pp = {(1.f * ((float)x - g.cx)) / g.fx, (1.f * ((float)y - g.cy)) / g.fy, 1.f};
     const f3 dir = normalized(rmul(P.R, pp));
@@ -857,7 +936,7 @@ __global__ __launch_bounds__(256, 5) void k_raycast(VolView v, LevelGeom g, RayC
     const float tnear = fmaxf(fmaxf(tmin.x, tmin.y), fmaxf(tmin.x, tmin.z));
     const float tfar = fminf(fminf(tmax.x, tmax.y), fminf(tmax.x, tmax.z));
     float ray_len = fmaxf(tnear, 0.f);
-    bool live = ray_len < tfar;
+    bool live = inimg && ray_len < tfar;
     const f3 vstep = mulc(dir, rc.vs);
     ray_len += rc.step;
     f3 nextp = add(org, scl(dir, ray_len));
@@ -888,8 +967,10 @@ __global__ __launch_bounds__(256, 5) void k_raycast(VolView v, LevelGeom g, RayC
         const int ix = f2i_rn(nextp.x * rc.vs_inv.x);
         const int iy = f2i_rn(nextp.y * rc.vs_inv.y);
         const int iz = f2i_rn(nextp.z * rc.vs_inv.z);
-        val[j] = a && !(ix >= v.X - 1 || iy >= v.Y - 1 || iz >= v.Z - 1 || ix < 1 || iy < 1 || iz < 1);
-        raw[j] = v.tsdf[val[j] ? vox_index(v, ix, iy, iz) : 0];
+        // 1 <= i <= dim-2 on each axis (tsdf_volume.cu:184-185), as unsigned compares
+        val[j] = a & ((unsigned)(ix - 1) < (unsigned)(v.X - 2)) &
+                 ((unsigned)(iy - 1) < (unsigned)(v.Y - 2)) & ((unsigned)(iz - 1) < (unsigned)(v.Z - 2));
+        raw[j] = v.tsdf[val[j] ? ray_index<kIdx32>(v, ix, iy, iz) : 0];
         rl = a ? rl + rc.step : rl;
       }
       unsigned ev = 0u, hitm = 0u;
@@ -927,8 +1008,14 @@ __global__ __launch_bounds__(256, 5) void k_raycast(VolView v, LevelGeom g, RayC
             const f3 vertex = add(org, scl(dir, Ts));
             const f3 n = compute_normal(v, rc, vertex);
             if (!isnan(n.x * n.y * n.z)) {
-              nout = rmul(st->Rinv, n);
-              vout = rmul(st->Rinv, sub(vertex, org));
+              // Rinv re-read from LDS here (volatile: not held in registers
+              // through the march)
+              float ri[9];
+              const volatile float *vr = s_rinv;
+#pragma unroll
+              for (int q = 0; q < 9; ++q) ri[q] = vr[q];
+              nout = rmul(ri, n);
+              vout = rmul(ri, sub(vertex, org));
               live = false;
               pend = 0u;
             } else {
@@ -941,77 +1028,55 @@ __global__ __launch_bounds__(256, 5) void k_raycast(VolView v, LevelGeom g, RayC
       ray_len = rl;
     }
   }
-  st3(prev.v[0], o, vout);
-  st3(prev.n[0], o, nout);
-}
-
-// kernel_resizePointsNormals (image_process.cu:95-125) for every level >= 1 in
-// one launch: a block owns a 16x16 tile of level 1 and the 8x8 / 4x4 tiles of
-// levels 2 / 3 under it, passing values through LDS (same float ops).
-__device__ __forceinline__ void resize_one(f3 d00, f3 d01, f3 d10, f3 d11, f3 n00, f3 n01,
-                                           f3 n10, f3 n11, f3 &vo, f3 &no) {
-  vo = {0.f, 0.f, 0.f};
-  no = {0.f, 0.f, 0.f};
-  if (!isnan(d00.x * d01.x * d10.x * d11.x)) {
-    vo = scl(add(add(add(d00, d01), d10), d11), 0.25f);
-    no = scl(add(add(add(n00, n01), n10), n11), 0.25f);
+  if (inimg) {
+    st3(prev.v[0], o, vout);
+    st3(prev.n[0], o, nout);
   }
-}
-
-struct ResizeArgs {
-  LevelGeom g[kMaxLevels];
-  int levels;
-};
-
-__global__ __launch_bounds__(256) void k_resize(ResizeArgs a, FrameView cur, FrameView prev,
-                                                const DevState *__restrict__ st) {
-  if (a.levels < 2) return;
-  const int mode = st->mode;
-  __shared__ f3 sv[2][16 * 16], sn[2][16 * 16];
-  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  // kernel_resizePointsNormals (image_process.cu:95-125) for levels >= 1: the
+  // block's 16x16 tile maps onto 8x8 / 4x4 / 2x2 tiles of levels 1 / 2 / 3,
+  // computed from the level below through LDS with the same float ops.
+  if (ra.levels < 2) return;
+  __shared__ f3 sv[2][256], sn[2][256];
+  sv[0][ly * 16 + lx] = vout;
+  sn[0][ly * 16 + lx] = nout;
+  __syncthreads();
   int side = 16;
-  for (int l = 1; l < a.levels; ++l) {
-    const LevelGeom g = a.g[l];
-    const int X = blockIdx.x * side + tx, Y = blockIdx.y * side + ty;
-    const bool act = tx < side && ty < side && X < g.w && Y < g.h;
-    f3 vo = {0.f, 0.f, 0.f}, no = {0.f, 0.f, 0.f};
-    if (act) {
-      const size_t o = (size_t)Y * g.w + X;
-      if (mode == MODE_BOOT) {
-        vo = ld3(cur.v[l], o);
-        no = ld3(cur.n[l], o);
-      } else if (mode == MODE_TRACK) {
-        f3 d[4], n[4];
-        if (l == 1) {
-          const int wb = a.g[0].w;
-          const size_t i00 = (size_t)(2 * Y) * wb + 2 * X;
-          const size_t ii[4] = {i00, i00 + 1, i00 + wb, i00 + wb + 1};
-          for (int q = 0; q < 4; ++q) {
-            d[q] = ld3(prev.v[0], ii[q]);
-            n[q] = ld3(prev.n[0], ii[q]);
-          }
-        } else {
-          const int pb = (l - 1) & 1;
-          const int ps = side * 2;
-          const int i00 = (2 * ty) * ps + 2 * tx;
-          const int ii[4] = {i00, i00 + 1, i00 + ps, i00 + ps + 1};
-          for (int q = 0; q < 4; ++q) {
-            d[q] = sv[pb][ii[q]];
-            n[q] = sn[pb][ii[q]];
-          }
-        }
-        resize_one(d[0], d[1], d[2], d[3], n[0], n[1], n[2], n[3], vo, no);
-      }
-      st3(prev.v[l], o, vo);
-      st3(prev.n[l], o, no);
-    }
-    __syncthreads();
-    if (tx < side && ty < side) {
-      sv[l & 1][ty * side + tx] = vo;
-      sn[l & 1][ty * side + tx] = no;
-    }
-    __syncthreads();
+  for (int l = 1; l < ra.levels; ++l) {
+    const int pb = (l - 1) & 1, cb = l & 1;
+    const int ps = side;
     side >>= 1;
+    const LevelGeom gl = ra.g[l];
+    const int X = (tx0 >> l) + (threadIdx.x % side), Y = (ty0 >> l) + (threadIdx.x / side);
+    const bool act = (int)threadIdx.x < side * side && X < gl.w && Y < gl.h;
+    f3 vo = {0.f, 0.f, 0.f}, no = {0.f, 0.f, 0.f};
+    if ((int)threadIdx.x < side * side) {
+      const int cx = threadIdx.x % side, cy = threadIdx.x / side;
+      if (kind == 0) {
+        if (act) {
+          const size_t ol = (size_t)Y * gl.w + X;
+          vo = ld3(cur.v[l], ol);
+          no = ld3(cur.n[l], ol);
+        }
+      } else if (kind == 1) {
+        const int i00 = (2 * cy) * ps + 2 * cx;
+        const f3 d00 = sv[pb][i00], d01 = sv[pb][i00 + 1], d10 = sv[pb][i00 + ps],
+                 d11 = sv[pb][i00 + ps + 1];
+        if (!isnan(d00.x * d01.x * d10.x * d11.x)) {
+          vo = scl(add(add(add(d00, d01), d10), d11), 0.25f);
+          no = scl(add(add(add(sn[pb][i00], sn[pb][i00 + 1]), sn[pb][i00 + ps]),
+                       sn[pb][i00 + ps + 1]),
+                   0.25f);
+        }
+      }
+      sv[cb][cy * side + cx] = vo;
+      sn[cb][cy * side + cx] = no;
+      if (act) {
+        const size_t ol = (size_t)Y * gl.w + X;
+        st3(prev.v[l], ol, vo);
+        st3(prev.n[l], ol, no);
+      }
+    }
+    __syncthreads();
   }
 }
 
@@ -1088,33 +1153,24 @@ void launch_pyr_down(hipStream_t s, const float *src, const uint16_t *src16, int
     hipLaunchKernelGGL(k_pyr_down<float>, grd, blk, 0, s, src, w, h, dst, dw, dh, st_begin);
 }
 
-void launch_bilateral_vertex(hipStream_t s, int levels, const float *const raw[kMaxLevels],
-                             const uint16_t *raw0_u16, const LevelGeom *g, FrameView cur,
-                             int ksz, float sigma_color, float sigma_spatial, float max_dist,
-                             DevState *st) {
+void launch_preprocess_maps(hipStream_t s, int levels, const float *const raw[kMaxLevels],
+                            const uint16_t *raw0_u16, const LevelGeom *g, FrameView cur, int ksz,
+                            float sigma_color, float sigma_spatial, float max_dist,
+                            DevState *st) {
   BilatArgs a{};
   a.t = make_tiles(levels, g);
   for (int l = 0; l < levels; ++l) {
     a.raw[l] = raw[l];
     a.d[l] = cur.d[l];
     a.v[l] = cur.v[l];
+    a.n[l] = cur.n[l];
   }
   a.raw0_u16 = raw0_u16;
   a.ksz = ksz;
   a.s_half = -0.5f / (sigma_spatial * sigma_spatial);
   a.c_half = -0.5f / (sigma_color * sigma_color);
   a.max_dist = max_dist;
-  hipLaunchKernelGGL(k_bilateral_vertex, dim3(a.t.off[levels]), dim3(256), 0, s, a, st);
-}
-
-void launch_normals(hipStream_t s, int levels, const LevelGeom *g, FrameView cur) {
-  NormalArgs a{};
-  a.t = make_tiles(levels, g);
-  for (int l = 0; l < levels; ++l) {
-    a.v[l] = cur.v[l];
-    a.n[l] = cur.n[l];
-  }
-  hipLaunchKernelGGL(k_normals, dim3(a.t.off[levels]), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_preprocess_maps, dim3(a.t.off[levels]), dim3(256), 0, s, a, st);
 }
 
 static int icp_npix(const LevelGeom &g, int *xe) {
@@ -1138,44 +1194,39 @@ void launch_icp(hipStream_t s, const LevelGeom &g, const float *cv, const float 
                      dist_thr, angle_thr, st, shards, ticket, force, update);
 }
 
-void launch_commit(hipStream_t s, DevState *st, DevPose *pose_log, DevPose volume_pose) {
-  hipLaunchKernelGGL(k_commit, dim3(1), dim3(1), 0, s, st, pose_log, volume_pose);
-}
-
 void launch_integrate(hipStream_t s, VolView v, LevelGeom g0, const float *dmap,
-                      const uint8_t *bgr, const float *inv_lambda, const DevState *st,
-                      unsigned long long *counters) {
+                      const uint8_t *bgr, const float *inv_lambda, DevState *st, DevPose *log,
+                      DevPose vpose, const float *xpose, unsigned long long *counters) {
   const int tiles = v.tiles_x * v.tiles_y;
   // z-chunks so that >= 16 waves per SIMD exist (16384 waves on 1024 SIMDs)
   const int nchunk = std::max(1, std::min(8, (16384 + tiles - 1) / tiles));
   dim3 grd((tiles + 3) / 4, nchunk);
   if (counters)
     hipLaunchKernelGGL(k_integrate<true>, grd, dim3(256), 0, s, v, g0, dmap, bgr, inv_lambda, st,
-                       counters);
+                       log, vpose, xpose, counters);
   else
     hipLaunchKernelGGL(k_integrate<false>, grd, dim3(256), 0, s, v, g0, dmap, bgr, inv_lambda, st,
-                       counters);
+                       log, vpose, xpose, counters);
 }
 
-void launch_raycast(hipStream_t s, VolView v, LevelGeom g0, FrameView cur, FrameView prev,
-                    const DevState *st) {
+void launch_raycast(hipStream_t s, VolView v, int levels, const LevelGeom *g, FrameView cur,
+                    FrameView prev, const DevState *st, const DevPose *log, DevPose vpose,
+                    const float *xpose) {
   RayConsts rc;
   rc.vs = {v.vs[0], v.vs[1], v.vs[2]};
   rc.vs_inv = {1.f / v.vs[0], 1.f / v.vs[1], 1.f / v.vs[2]};
   rc.gd = {v.vs[0] * 0.5f, v.vs[1] * 0.5f, v.vs[2] * 0.5f};
   rc.step = v.vs[0];
-  dim3 grd((g0.w + 15) / 16, (g0.h + 15) / 16);
-  hipLaunchKernelGGL(k_raycast, grd, dim3(256), 0, s, v, g0, rc, cur, prev, st);
-}
-
-void launch_resize(hipStream_t s, int levels, const LevelGeom *g, FrameView cur, FrameView prev,
-                   const DevState *st) {
-  if (levels < 2) return;
-  ResizeArgs a{};
-  a.levels = levels;
-  for (int l = 0; l < levels; ++l) a.g[l] = g[l];
-  dim3 grd((g[1].w + 15) / 16, (g[1].h + 15) / 16);
-  hipLaunchKernelGGL(k_resize, grd, dim3(256), 0, s, a, cur, prev, st);
+  RayArgs ra{};
+  ra.levels = levels;
+  for (int l = 0; l < levels; ++l) ra.g[l] = g[l];
+  dim3 grd(((g[0].w + 15) / 16) * ((g[0].h + 15) / 16));
+  if (v.slice * (size_t)v.Z < (1ull << 32))
+    hipLaunchKernelGGL(k_raycast<true>, grd, dim3(256), 0, s, v, ra, rc, cur, prev, st, log, vpose,
+                       xpose);
+  else
+    hipLaunchKernelGGL(k_raycast<false>, grd, dim3(256), 0, s, v, ra, rc, cur, prev, st, log, vpose,
+                       xpose);
 }
 
 void launch_inv_lambda(hipStream_t s, LevelGeom g0, float *inv_lambda) {
