@@ -106,6 +106,16 @@ int kfx_pipeline_staged(kfx_ctx *ctx, int frame_index);
 int kfx_synchronize(kfx_ctx *ctx);
 /* Use a captured hipGraph for the per-frame launch sequence (default on). */
 int kfx_set_graph_mode(kfx_ctx *ctx, int enabled);
+/* Run all ICP iterations of a frame as one persistent launch (default on; used
+ * only when its grid fits co-resident on the device, else one launch per
+ * iteration).  Returns 1 if the persistent kernel is usable on this context, 0
+ * if not, <0 on error.  Results are identical either way. */
+int kfx_set_icp_persistent(kfx_ctx *ctx, int enabled);
+/* Profiling seam: per ICP iteration of the last persistent-ICP frame, five
+ * s_memrealtime stamps (100 MHz): block 0 start, block 0 arrived, block 0
+ * released from the barrier, block 0 solved, last block arrived.  Returns the
+ * number of iterations written (<= max_iters). */
+int kfx_get_icp_trace(kfx_ctx *ctx, uint64_t *out, int max_iters);
 
 /* kinectfusion::getCurCameraPose() (kinectfusion.cpp:128-132). */
 int kfx_get_cur_camera_pose(kfx_ctx *ctx, kfx_pose *out);

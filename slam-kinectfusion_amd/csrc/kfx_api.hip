@@ -91,6 +91,10 @@ struct kfx_ctx {
   int pose_cap = 0;
   unsigned long long *icp_shards = nullptr;  // 8 x 27 int64 + ticket (self-resetting)
   unsigned *icp_ticket = nullptr;
+  IcpSync *icp_sync = nullptr;  // persistent ICP barrier + per-iteration shard slots
+  IcpPlan icp_plan{};
+  bool icp_persistent = false;  // plan fits and its grid is co-resident
+  bool icp_persistent_enabled = true;
   unsigned long long *counters = nullptr;
   float *xpose = nullptr;  // explicit stage poses (21 floats: pose R,t + Rinv)
   std::vector<void *> allocs;
@@ -170,11 +174,15 @@ void enqueue_frame(kfx_ctx *c, FrameInput in, bool events) {
                          c->st);
   if (events) (void)hipEventRecord(c->ev[1], s);
   // ICPRegistration::rigidTransform (icp_registration.cpp:16-46)
-  for (int level = c->L - 1; level >= 0; --level) {
-    for (int it = 0; it < c->p.icp_iter_count[level]; ++it)
-      launch_icp(s, c->g[level], c->cur.v[level], c->cur.n[level], c->prev.v[level],
-                 c->prev.n[level], c->p.icp_dist_threshold, c->angle_thr, c->st, c->icp_shards,
-                 c->icp_ticket, 0, 1);
+  if (c->icp_persistent && c->icp_persistent_enabled) {
+    launch_icp_track(s, c->icp_plan, c->st, c->icp_sync);
+  } else {
+    for (int level = c->L - 1; level >= 0; --level) {
+      for (int it = 0; it < c->p.icp_iter_count[level]; ++it)
+        launch_icp(s, c->g[level], c->cur.v[level], c->cur.n[level], c->prev.v[level],
+                   c->prev.n[level], c->p.icp_dist_threshold, c->angle_thr, c->st,
+                   c->icp_shards, c->icp_ticket, 0, 1);
+    }
   }
   if (events) (void)hipEventRecord(c->ev[2], s);
   launch_integrate(s, c->vol, c->g[0], c->cur.d[0], in.bgr, c->inv_lambda, c->st, c->pose_log,
@@ -266,6 +274,11 @@ int finish_frame(kfx_ctx *c) {
   DevState s;
   int r = read_state(c, &s);
   if (r) return r;
+  if (s.icp_stalled) {
+    HIPCHK(hipMemsetAsync(c->icp_sync, 0, sizeof(IcpSync), c->stream));
+    r = write_field(c, offsetof(DevState, icp_stalled), 0);
+    return r ? r : set_err(KFX_ERR_HIP, "ICP grid barrier watchdog fired (grid not co-resident)");
+  }
   return s.last_fail ? KFX_TRACKING_LOST : KFX_OK;
 }
 
@@ -428,6 +441,10 @@ int kfx_create(const kfx_intrinsics *intr, const kfx_params *params, int device,
   if ((r = dalloc(c, (void **)&c->icp_shards, sizeof(unsigned long long) * 8 * 27 + 64)))
     return fail(r);
   c->icp_ticket = reinterpret_cast<unsigned *>(c->icp_shards + 8 * 27);
+  if ((r = dalloc(c, (void **)&c->icp_sync, sizeof(IcpSync)))) return fail(r);
+  c->icp_plan = make_icp_plan(c->L, c->g, c->p.icp_iter_count, c->cur, c->prev,
+                              c->p.icp_dist_threshold, c->angle_thr);
+  c->icp_persistent = icp_persistent_ok(c->icp_plan, c->device);
   if ((r = dalloc(c, (void **)&c->counters, sizeof(unsigned long long) * 32))) return fail(r);
   if ((r = dalloc(c, (void **)&c->xpose, sizeof(float) * 32))) return fail(r);
   launch_inv_lambda(c->stream, c->g[0], c->inv_lambda);
@@ -525,6 +542,23 @@ int kfx_set_graph_mode(kfx_ctx *c, int enabled) {
   if (!c) return set_err(KFX_ERR_ARG, "null context");
   c->graph_mode = enabled != 0;
   return KFX_OK;
+}
+
+int kfx_set_icp_persistent(kfx_ctx *c, int enabled) {
+  if (!c) return set_err(KFX_ERR_ARG, "null context");
+  if (c->icp_persistent_enabled != (enabled != 0)) destroy_graphs(c);
+  c->icp_persistent_enabled = enabled != 0;
+  return c->icp_persistent ? 1 : 0;
+}
+
+int kfx_get_icp_trace(kfx_ctx *c, uint64_t *out, int max_iters) {
+  int r = check_ctx(c);
+  if (r) return r;
+  if (!out || max_iters < 0) return set_err(KFX_ERR_ARG, "null argument");
+  const int n = std::min(max_iters, c->icp_plan.slots);
+  HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(hipMemcpy(out, c->icp_sync->trace, sizeof(uint64_t) * 12 * (size_t)n, hipMemcpyDeviceToHost));
+  return n;
 }
 
 int kfx_set_profiling(kfx_ctx *c, int enabled) {
@@ -763,14 +797,24 @@ int kfx_stage_icp(kfx_ctx *c, kfx_pose *out) {
   s.icp_fail = 0;
   s.icp_pose = identity_pose();
   HIPCHK(hipMemcpyAsync(c->st, &s, sizeof(s), hipMemcpyHostToDevice, c->stream));
-  for (int level = c->L - 1; level >= 0; --level) {
-    for (int it = 0; it < c->p.icp_iter_count[level]; ++it)
-      launch_icp(c->stream, c->g[level], c->cur.v[level], c->cur.n[level], c->prev.v[level],
-                 c->prev.n[level], c->p.icp_dist_threshold, c->angle_thr, c->st, c->icp_shards,
-                 c->icp_ticket, 0, 1);
+  if (c->icp_persistent && c->icp_persistent_enabled) {
+    launch_icp_track(c->stream, c->icp_plan, c->st, c->icp_sync);
+  } else {
+    for (int level = c->L - 1; level >= 0; --level) {
+      for (int it = 0; it < c->p.icp_iter_count[level]; ++it)
+        launch_icp(c->stream, c->g[level], c->cur.v[level], c->cur.n[level], c->prev.v[level],
+                   c->prev.n[level], c->p.icp_dist_threshold, c->angle_thr, c->st,
+                   c->icp_shards, c->icp_ticket, 0, 1);
+    }
   }
   HIPCHK(hipGetLastError());
   if ((r = read_state(c, &s))) return r;
+  if (s.icp_stalled) {
+    HIPCHK(hipMemsetAsync(c->icp_sync, 0, sizeof(IcpSync), c->stream));
+    HIPCHK(hipMemcpyAsync(c->st, &s0, sizeof(s0), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return set_err(KFX_ERR_HIP, "ICP grid barrier watchdog fired (grid not co-resident)");
+  }
   if (out) *out = to_api(s.icp_pose);
   const int failed = s.icp_fail;
   HIPCHK(hipMemcpyAsync(c->st, &s0, sizeof(s0), hipMemcpyHostToDevice, c->stream));

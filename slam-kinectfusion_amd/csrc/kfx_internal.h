@@ -32,11 +32,38 @@ struct DevState {
   DevPose icp_pose;     // camera_pose inside rigidTransform
   long long sums[27];   // last ICP sums (test seam)
   double x[6];          // last ICP increment
+  int icp_stalled;      // persistent ICP barrier watchdog fired (reported as KFX_ERR_HIP)
 };
 
 struct LevelGeom {
   int w, h;
   float fx, fy, cx, cy;
+};
+
+constexpr int kIcpShards = 8;
+constexpr int kIcpMaxSlots = 64;  // ICP iterations per frame in the persistent kernel
+
+// Per-frame plan of the persistent ICP kernel (all levels, all iterations).
+struct IcpPlan {
+  int levels, nblocks, slots;
+  LevelGeom g[kMaxLevels];
+  int xe[kMaxLevels], npix[kMaxLevels], groups[kMaxLevels], iters[kMaxLevels];
+  const float *cv[kMaxLevels], *cn[kMaxLevels], *pv[kMaxLevels], *pn[kMaxLevels];
+  float dist_thr, angle_thr;
+};
+
+// Device workspace of the persistent ICP kernel; zero between launches
+// (the kernel's last block restores that).
+struct IcpSync {
+  unsigned arrive, pad0[31];   // arrivals, all iterations (own 128-B line)
+  unsigned exit, pad1[31];
+  struct {
+    unsigned v, pad[31];
+  } release[8];                // iterations released so far; 8 copies polled by block % 8
+  unsigned long long sums[kIcpMaxSlots * kIcpShards * 27];
+  // s_memrealtime stamps of the last frame, per iteration: block 0 start /
+  // arrived / released / solved, last block arrived (kfx_get_icp_trace)
+  unsigned long long trace[kIcpMaxSlots][12];
 };
 
 // SoA TSDF volume.  Each z slice is tiled in 8x8 (x,y) tiles; voxel (x,y,z)
@@ -71,6 +98,10 @@ void launch_preprocess_maps(hipStream_t s, int levels, const float *const raw[kM
 int icp_blocks(const LevelGeom &g);
 // one ICP iteration (rigid_icp.cu:135-169 + icp_registration.cpp:33-42) in a
 // single launch; shards = 8 x 27 int64 zeroed, ticket zeroed (both self-reset)
+IcpPlan make_icp_plan(int levels, const LevelGeom *g, const int *iters, FrameView cur,
+                      FrameView prev, float dist_thr, float angle_thr);
+bool icp_persistent_ok(const IcpPlan &pl, int device);  // grid co-resident + slots fit
+void launch_icp_track(hipStream_t s, const IcpPlan &pl, DevState *st, IcpSync *sync);
 void launch_icp(hipStream_t s, const LevelGeom &g, const float *cv, const float *cn,
                 const float *pv, const float *pn, float dist_thr, float angle_thr, DevState *st,
                 unsigned long long *shards, unsigned *ticket, int force, int update);

@@ -8,6 +8,7 @@
 // are bit-identical to the CPU oracle (oracle/kfx_oracle.cpp) on the same inputs.
 #include <algorithm>
 #include <climits>
+#include <type_traits>
 
 #include "kfx_internal.h"
 
@@ -89,6 +90,19 @@ __device__ __forceinline__ float div_rn(float x, float d, float y) {
   const float r = fmaf(-q0, d, x);
   return fmaf(r, y, q0);
 }
+
+// Pixel coordinate rn((a / d) * f + c) as a float, with a / d from one
+// reciprocal y = RN(1/d) shared by both image axes: div_rn(a, d, y) is the
+// correctly rounded quotient (Markstein; checked on 2e10 random general pairs,
+// tools/markstein_general.c).  |d| below 2^-100 (1/d near overflow) takes the
+// IEEE division.
+__device__ __forceinline__ float proj_rn(float a, float d, float y, float f, float c) {
+  const float q = (fabsf(d) >= 7.8886091e-31f) ? div_rn(a, d, y) : a / d;
+  return rintf(q * f + c);
+}
+// f2i_rn(v) in [0, n) tested on the rounded float (exact: integers, n < 2^24);
+// NaN fails both compares like the INT_MIN of f2i_rn.
+__device__ __forceinline__ bool in_range(float r, int n) { return r >= 0.f && r < (float)n; }
 
 __device__ __forceinline__ DevPose pose_identity() {
   DevPose p;
@@ -327,52 +341,38 @@ __global__ __launch_bounds__(256) void k_preprocess_maps(BilatArgs a, DevState *
 // together; the block reduces through LDS and writes one 27-word partial.
 constexpr int kIcpPix = 4;
 constexpr int kIcpBlockPix = 256 * kIcpPix;
-constexpr int kIcpShards = 8;
+constexpr unsigned long long kIcpWatchdogTicks = 20000000ull;  // >= 0.2 s of s_memrealtime
 __device__ int icp_update(const long long *sums, DevPose &pose, double *xo);
 
-__global__ __launch_bounds__(256) void k_icp_acc(LevelGeom g, int xe, int npix,
-                                                 const float *__restrict__ cv,
-                                                 const float *__restrict__ cn,
-                                                 const float *__restrict__ pv,
-                                                 const float *__restrict__ pn, float dist_thr,
-                                                 float angle_thr, DevState *__restrict__ st,
-                                                 unsigned long long *__restrict__ shards,
-                                                 unsigned *__restrict__ ticket, int force,
-                                                 int update) {
-  if (!force && (st->mode != MODE_TRACK || st->icp_fail)) return;
-  const DevPose P = st->icp_pose;
+// Per-lane part of one ICP iteration: kIcpPix pixels whose current-frame
+// vertex/normal (n0, v0, validity ok0) are already in registers; gathers the
+// previous frame's maps at the projections and accumulates the 27 products.
+// Every product is rounded to an integer multiple of 2^-32 (rintf(prod *
+// 2^32)); within a block the running sums are integers below 2^49 (|prod| <
+// 2^7, <= 2^10 products per 27-slot), so fp64 adds are exact and equal the
+// oracle's int64 sums; the block total converts to int64 exactly.
+__device__ __forceinline__ void icp_lane(const LevelGeom &g, const DevPose &P,
+                                         const f3 (&n0)[kIcpPix], const f3 (&v0)[kIcpPix],
+                                         const bool (&ok0)[kIcpPix], const float *__restrict__ pv,
+                                         const float *__restrict__ pn, float dist_thr,
+                                         float angle_thr, double (&acc)[27]) {
   const f3 t = {P.t[0], P.t[1], P.t[2]};
-  // Every product is rounded to an integer multiple of 2^-32 (rintf(prod *
-  // 2^32)); within a block the running sums are integers below 2^49 (|prod|
-  // < 2^7, <= 2^10 products per 27-slot), so fp64 adds are exact and equal the
-  // oracle's int64 sums; the block total converts to int64 exactly.
-  double acc[27];
 #pragma unroll
   for (int k = 0; k < 27; ++k) acc[k] = 0.0;
-
-  // loads are unconditional (out-of-range lanes read pixel 0) so the
-  // compiler issues each group back to back instead of waiting per branch
-  f3 n0[kIcpPix], v0[kIcpPix];
-  bool ok[kIcpPix];
-#pragma unroll
-  for (int q = 0; q < kIcpPix; ++q) {
-    const int i = blockIdx.x * kIcpBlockPix + q * 256 + threadIdx.x;
-    ok[q] = i < npix;
-    const size_t idx = ok[q] ? (size_t)(i / xe) * g.w + (i % xe) : 0;
-    n0[q] = ld3(cn, idx);
-    v0[q] = ld3(cv, idx);
-  }
   f3 vcur[kIcpPix];
   int j[kIcpPix];
+  bool ok[kIcpPix];
 #pragma unroll
   for (int q = 0; q < kIcpPix; ++q) {
     vcur[q] = add(rmul(P.R, v0[q]), t);
     const int px = f2i_rn((vcur[q].x / vcur[q].z) * g.fx + g.cx);
     const int py = f2i_rn((vcur[q].y / vcur[q].z) * g.fy + g.cy);
-    ok[q] = ok[q] && !isnan(n0[q].x) && vcur[q].z > 0 && px >= 0 && py >= 0 && px < g.w &&
+    ok[q] = ok0[q] && !isnan(n0[q].x) && vcur[q].z > 0 && px >= 0 && py >= 0 && px < g.w &&
             py < g.h;
     j[q] = ok[q] ? py * g.w + px : 0;
   }
+  // loads are unconditional (rejected lanes read pixel 0) so the compiler
+  // issues each group back to back instead of waiting per branch
   f3 vpre[kIcpPix], npre[kIcpPix];
 #pragma unroll
   for (int q = 0; q < kIcpPix; ++q) {
@@ -401,26 +401,75 @@ __global__ __launch_bounds__(256) void k_icp_acc(LevelGeom g, int xe, int npix,
         acc[s++] += (double)rintf(prod * kFix);
       }
   }
-  // LDS transpose reduction: row (wave, k) holds 64 lane values (stride 65 to
-  // spread banks); 108 threads sum one row each, then 27 threads sum 4 waves.
-  __shared__ double red[4 * 27 * 65];
-  __shared__ double red2[4 * 27];
+}
+
+// Current-frame vertex/normal of the lane's pixels of pixel group grp.
+__device__ __forceinline__ void icp_load_cur(const LevelGeom &g, int xe, int npix, int grp,
+                                             const float *__restrict__ cv,
+                                             const float *__restrict__ cn, f3 (&n0)[kIcpPix],
+                                             f3 (&v0)[kIcpPix], bool (&ok)[kIcpPix]) {
+#pragma unroll
+  for (int q = 0; q < kIcpPix; ++q) {
+    const int i = grp * kIcpBlockPix + q * 256 + threadIdx.x;
+    ok[q] = i < npix;
+    const size_t idx = ok[q] ? (size_t)(i / xe) * g.w + (i % xe) : 0;
+    n0[q] = ld3(cn, idx);
+    v0[q] = ld3(cv, idx);
+  }
+}
+
+// LDS transpose reduction of the block's 256 x 27 lane sums: row (wave, k)
+// holds 64 lane values (stride 65 to spread banks); 108 threads sum one row
+// each.  Returns, in threads 0..26, the block's sum of product k as int64.
+struct IcpRed {
+  double red[4 * 27 * 65];
+  double red2[kIcpShards * 27];  // >= 4 * 27; also stages the shard reads
+};
+__device__ __forceinline__ long long icp_block_reduce(IcpRed &r, const double (&acc)[27]) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #pragma unroll
-  for (int k = 0; k < 27; ++k) red[(wv * 27 + k) * 65 + lane] = acc[k];
+  for (int k = 0; k < 27; ++k) r.red[(wv * 27 + k) * 65 + lane] = acc[k];
   __syncthreads();
   if (threadIdx.x < 108) {
-    const double *r = red + threadIdx.x * 65;
+    const double *row = r.red + threadIdx.x * 65;
     double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
     for (int q = 0; q < 64; q += 4) {
-      s0 += r[q];
-      s1 += r[q + 1];
-      s2 += r[q + 2];
-      s3 += r[q + 3];
+      s0 += row[q];
+      s1 += row[q + 1];
+      s2 += row[q + 2];
+      s3 += row[q + 3];
     }
-    red2[threadIdx.x] = (s0 + s1) + (s2 + s3);
+    r.red2[threadIdx.x] = (s0 + s1) + (s2 + s3);
   }
   __syncthreads();
+  long long v = 0;
+  if (threadIdx.x < 27) {
+    const int k = threadIdx.x;
+    v = (long long)(r.red2[k] + r.red2[27 + k] + r.red2[54 + k] + r.red2[81 + k]);
+  }
+  return v;
+}
+
+// One ICP iteration per launch (stage API seam and the fallback when the
+// persistent kernel's grid cannot be co-resident).
+__global__ __launch_bounds__(256) void k_icp_acc(LevelGeom g, int xe, int npix,
+                                                 const float *__restrict__ cv,
+                                                 const float *__restrict__ cn,
+                                                 const float *__restrict__ pv,
+                                                 const float *__restrict__ pn, float dist_thr,
+                                                 float angle_thr, DevState *__restrict__ st,
+                                                 unsigned long long *__restrict__ shards,
+                                                 unsigned *__restrict__ ticket, int force,
+                                                 int update) {
+  if (!force && (st->mode != MODE_TRACK || st->icp_fail)) return;
+  const DevPose P = st->icp_pose;
+  f3 n0[kIcpPix], v0[kIcpPix];
+  bool ok[kIcpPix];
+  icp_load_cur(g, xe, npix, blockIdx.x, cv, cn, n0, v0, ok);
+  double acc[27];
+  icp_lane(g, P, n0, v0, ok, pv, pn, dist_thr, angle_thr, acc);
+  __shared__ IcpRed red;
+  const long long bsum = icp_block_reduce(red, acc);
   // Cross-block sum + solve in the same launch: wave 0 adds the block's 27
   // sums into one of kIcpShards shard rows with device-scope int64 atomics
   // (performed at the memory side; exact and order-free), waits for them, then
@@ -428,12 +477,9 @@ __global__ __launch_bounds__(256) void k_icp_acc(LevelGeom g, int xe, int npix,
   // shards and runs icp_registration.cpp:33-42 (icp_update) on one lane.
   __shared__ int last;
   if (threadIdx.x < 64) {
-    if (threadIdx.x < 27) {
-      const int k = threadIdx.x;
-      const long long v = (long long)(red2[k] + red2[27 + k] + red2[54 + k] + red2[81 + k]);
-      __hip_atomic_fetch_add(&shards[(blockIdx.x % kIcpShards) * 27 + k], (unsigned long long)v,
-                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    if (threadIdx.x < 27)
+      __hip_atomic_fetch_add(&shards[(blockIdx.x % kIcpShards) * 27 + threadIdx.x],
+                             (unsigned long long)bsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (threadIdx.x == 0) {
       const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -443,103 +489,249 @@ __global__ __launch_bounds__(256) void k_icp_acc(LevelGeom g, int xe, int npix,
   __syncthreads();
   if (!last) return;
   __shared__ long long sums[27];
+  // one read-and-clear per thread (a thread's atomics serialise)
+  if (threadIdx.x < kIcpShards * 27)
+    red.red2[threadIdx.x] = __longlong_as_double((long long)__hip_atomic_exchange(
+        &shards[threadIdx.x], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  if (threadIdx.x == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
   if (threadIdx.x < 27) {
     long long a = 0;
 #pragma unroll
-    for (int sh = 0; sh < kIcpShards; ++sh)
-      a += (long long)__hip_atomic_exchange(&shards[sh * 27 + threadIdx.x], 0ull,
-                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int sh = 0; sh < kIcpShards; ++sh) a += __double_as_longlong(red.red2[sh * 27 + threadIdx.x]);
     sums[threadIdx.x] = a;
     st->sums[threadIdx.x] = a;
   }
-  if (threadIdx.x == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
-  if (threadIdx.x == 0 && update) {
-    long long sm[27];
-#pragma unroll
-    for (int k = 0; k < 27; ++k) sm[k] = sums[k];
+  if (threadIdx.x < 64 && update) {  // wave 0 solves
     DevPose p = st->icp_pose;
     double x[6];
-    if (icp_update(sm, p, x)) {
-      st->icp_fail = 1;
-    } else {
-      st->icp_pose = p;
+    const int f = icp_update(sums, p, x);
+    if (threadIdx.x == 0) {
+      if (f) {
+        st->icp_fail = 1;
+      } else {
+        st->icp_pose = p;
 #pragma unroll
-      for (int i = 0; i < 6; ++i) st->x[i] = x[i];
+        for (int i = 0; i < 6; ++i) st->x[i] = x[i];
+      }
     }
   }
 }
 
-// icp_registration.cpp:33-42 on the device: A/b unpack (rigid_icp.cu:156-165),
-// LU det check, LU solve (D: instead of SVD), Rodrigues, pose = pose * Tinc.
-// Fully unrolled with select-based row swaps so A lives in registers; the
-// arithmetic is operation-for-operation the oracle's kfo_icp_update.
-__device__ int icp_update(const long long *sums, DevPose &pose, double *xo) {
-  double A[6][6], b[6];
-  {
-    int s = 0;
-#pragma unroll
-    for (int i = 0; i < 6; ++i)
-#pragma unroll
-      for (int j = i; j < 7; ++j) {
-        const double v = (double)sums[s++] * (1.0 / 4294967296.0);
-        if (j == 6)
-          b[i] = v;
-        else
-          A[i][j] = A[j][i] = v;
+// ICPRegistration::rigidTransform (icp_registration.cpp:16-46) as ONE
+// persistent launch: every iteration of every level, separated by a
+// grid-wide arrival counter instead of a kernel boundary.  The grid (one
+// block per 1024-pixel group of the largest level) is checked co-resident on
+// the host (icp_persistent_ok).  Per iteration, the blocks that own pixels at
+// that level add their int64 partials into the iteration's own shard slot and
+// arrive; EVERY block then waits for the arrivals, reads the slot and runs the
+// same solve (identical inputs and code => identical pose in every block, no
+// broadcast step).  Current-frame maps stay in registers across a level's
+// iterations.  A wall-clock watchdog turns a stalled barrier into a reported
+// error instead of a hang.
+__global__ __launch_bounds__(256, 2) void k_icp_track(IcpPlan pl, DevState *__restrict__ st,
+                                                   IcpSync *__restrict__ sy) {
+  if (st->mode != MODE_TRACK || st->icp_fail) return;  // uniform across the grid
+  __shared__ IcpRed red;
+  __shared__ long long sums[27];
+  __shared__ DevPose spose;
+  __shared__ int sfail, sstall;
+  DevPose P = st->icp_pose;
+  int fail = 0;
+  unsigned target = 0;
+  int slot = 0;
+  for (int l = pl.levels - 1; l >= 0 && !fail; --l) {
+    const LevelGeom g = pl.g[l];
+    const bool mine = (int)blockIdx.x < pl.groups[l];
+    f3 n0[kIcpPix], v0[kIcpPix];
+    bool ok[kIcpPix];
+    if (mine) icp_load_cur(g, pl.xe[l], pl.npix[l], blockIdx.x, pl.cv[l], pl.cn[l], n0, v0, ok);
+    for (int it = 0; it < pl.iters[l] && !fail; ++it, ++slot) {
+      unsigned long long *sh = sy->sums + (size_t)slot * kIcpShards * 27;
+      target += pl.groups[l];
+      const bool tr = threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x - 1);
+      if (tr && blockIdx.x == 0) sy->trace[slot][0] = wall_clock64();
+      if (mine) {
+        double acc[27];
+        icp_lane(g, P, n0, v0, ok, pl.pv[l], pl.pn[l], pl.dist_thr, pl.angle_thr, acc);
+        if (tr && blockIdx.x == 0) sy->trace[slot][8] = wall_clock64() + (acc[3] == -1.5 ? 1 : 0);
+        const long long bsum = icp_block_reduce(red, acc);
+        if (tr && blockIdx.x == 0) sy->trace[slot][9] = wall_clock64() + (bsum == -7 ? 1 : 0);
+        if (threadIdx.x < 64) {
+          if (threadIdx.x < 27)
+            __hip_atomic_fetch_add(&sh[(blockIdx.x % kIcpShards) * 27 + threadIdx.x],
+                                   (unsigned long long)bsum, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+          // the partial adds are device-scope atomics (performed past the
+          // non-coherent L2s); waiting for their completion orders them before
+          // the arrival, and every read of them below is a coherent atomic
+          // load, so no L2 writeback/invalidate fence is needed
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          if (tr && blockIdx.x == 0) sy->trace[slot][10] = wall_clock64();
+          if (threadIdx.x == 0) {
+            // the last arriver releases the iteration: spinners poll 8 flag
+            // copies instead of the contended arrival counter
+            const unsigned n =
+                __hip_atomic_fetch_add(&sy->arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (n == target - 1)
+              for (int k = 0; k < 8; ++k)
+                __hip_atomic_store(&sy->release[k].v, (unsigned)(slot + 1), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+          }
+        }
       }
+      if (tr) sy->trace[slot][blockIdx.x == 0 ? 1 : 4] = wall_clock64();
+      if (threadIdx.x == 0) {
+        const unsigned long long t0 = wall_clock64();
+        int stalled = 0;
+        const unsigned *flag = &sy->release[blockIdx.x & 7].v;
+        while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)(slot + 1)) {
+          __builtin_amdgcn_s_sleep(1);
+          if (wall_clock64() - t0 > kIcpWatchdogTicks) {
+            stalled = 1;
+            break;
+          }
+        }
+        if (stalled) st->icp_stalled = 1;  // host reports it after the frame
+        sstall = stalled;
+        if (tr && blockIdx.x == 0) sy->trace[slot][2] = wall_clock64();
+      }
+      __syncthreads();
+      // one coherent load per thread (a thread's atomic loads serialise)
+      if (threadIdx.x < kIcpShards * 27)
+        red.red2[threadIdx.x] = __longlong_as_double((long long)__hip_atomic_load(
+            &sh[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      __syncthreads();
+      if (threadIdx.x < 27) {
+        long long a = 0;
+#pragma unroll
+        for (int k = 0; k < kIcpShards; ++k) a += __double_as_longlong(red.red2[k * 27 + threadIdx.x]);
+        sums[threadIdx.x] = a;
+      }
+      __syncthreads();
+      if (tr && blockIdx.x == 0) sy->trace[slot][5] = wall_clock64();
+      if (threadIdx.x < 64) {  // wave 0 solves (every block, identical result)
+        DevPose p = P;
+        double x[6];
+        int f = icp_update(sums, p, x);
+        if (tr && blockIdx.x == 0) sy->trace[slot][6] = __builtin_amdgcn_readfirstlane((int)x[0]) + wall_clock64();
+        if (sstall) f = 1;  // a stalled block stops; the others stall at the next barrier
+        if (threadIdx.x < 27 && blockIdx.x == 0) st->sums[threadIdx.x] = sums[threadIdx.x];
+        if (threadIdx.x == 0) {
+          sfail = f;
+          if (!f) spose = p;
+        }
+        if (threadIdx.x == 0 && blockIdx.x == 0) {
+          if (f) {
+            st->icp_fail = 1;
+          } else {
+#pragma unroll
+            for (int i = 0; i < 6; ++i) st->x[i] = x[i];
+          }
+        }
+      }
+      __syncthreads();
+      if (tr && blockIdx.x == 0) sy->trace[slot][3] = wall_clock64();
+      fail = __builtin_amdgcn_readfirstlane(sfail);
+      if (!fail) {  // block-uniform: keep the pose in SGPRs
+#pragma unroll
+        for (int k = 0; k < 9; ++k) P.R[k] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(spose.R[k])));
+#pragma unroll
+        for (int k = 0; k < 3; ++k) P.t[k] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(spose.t[k])));
+      }
+      __syncthreads();  // spose/sums/red are rewritten next iteration
+    }
+  }
+  if (threadIdx.x == 0) {
+    if (blockIdx.x == 0) st->icp_pose = P;
+    // exit ticket: the last block out clears the slots and the counters
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    const unsigned t = __hip_atomic_fetch_add(&sy->exit, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sfail = (t == gridDim.x - 1);  // sfail is free after the loop's last barrier
+  }
+  __syncthreads();
+  if (sfail) {  // this block drew the last exit ticket
+    const int n = slot * kIcpShards * 27;
+    for (int i = threadIdx.x; i < n; i += 256)
+      __hip_atomic_store(&sy->sums[i], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) {
+      __hip_atomic_store(&sy->arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&sy->exit, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (threadIdx.x < 8)
+      __hip_atomic_store(&sy->release[threadIdx.x].v, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// Broadcast of a double from a (wave-uniform) lane through SGPRs.
+__device__ __forceinline__ double bcast(double v, int src) {
+  const long long u = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(u & 0xffffffff), src);
+  const int hi = __builtin_amdgcn_readlane((int)(u >> 32), src);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+// icp_registration.cpp:33-42 on the device, run by one whole wave: A/b unpack
+// (rigid_icp.cu:156-165), partial-pivot LU with det check, LU solve (D:
+// instead of SVD), Rodrigues, pose = pose * Tinc.  Lane 7*i+j holds A[i][j]
+// (j == 6: b[i]); each elimination step updates all (i > k, j > k) elements
+// at once with exactly the oracle's per-element operation
+// A[i][j] - (A[i][k] / A[k][k]) * A[k][j] (kfo_icp_update), so the result is
+// bit-identical to the sequential loop.  Everything after the LU is computed
+// redundantly by every lane (uniform results).  sums: 27 int64 (any memory).
+__device__ int icp_update(const long long *sums, DevPose &pose, double *xo) {
+  const int lane = threadIdx.x & 63;
+  const int i = lane / 7, j = lane - 7 * (lane / 7);
+  const bool live = lane < 42;
+  double a = 0.0;
+  if (live) {
+    const int r = (j == 6 || i <= j) ? i : j, c = (j == 6 || i <= j) ? j : i;
+    a = (double)sums[7 * r - r * (r - 1) / 2 + (c - r)] * (1.0 / 4294967296.0);
   }
   int sign = 1;
 #pragma unroll
   for (int k = 0; k < 6; ++k) {
     int p = k;
-    double best = fabs(A[k][k]);
+    double best = fabs(bcast(a, 7 * k + k));
 #pragma unroll
-    for (int i = k + 1; i < 6; ++i) {
-      const double a = fabs(A[i][k]);
-      if (a > best) {
-        best = a;
-        p = i;
+    for (int r = k + 1; r < 6; ++r) {
+      const double t = fabs(bcast(a, 7 * r + k));
+      if (t > best) {
+        best = t;
+        p = r;
       }
     }
-    if (p != k) sign = -sign;
-#pragma unroll
-    for (int i = k + 1; i < 6; ++i) {
-      const bool sw = (p == i);
-#pragma unroll
-      for (int j = 0; j < 6; ++j) {
-        const double tk = A[k][j], ti = A[i][j];
-        A[k][j] = sw ? ti : tk;
-        A[i][j] = sw ? tk : ti;
-      }
-      const double bk = b[k], bi = b[i];
-      b[k] = sw ? bi : bk;
-      b[i] = sw ? bk : bi;
+    if (p != k) {  // wave-uniform
+      const int src = (i == k) ? 7 * p + j : ((i == p) ? 7 * k + j : lane);
+      a = __shfl(a, src);
+      sign = -sign;
     }
-    if (A[k][k] != 0.0) {
-#pragma unroll
-      for (int i = k + 1; i < 6; ++i) {
-        const double f = A[i][k] / A[k][k];
-#pragma unroll
-        for (int j = k + 1; j < 6; ++j) A[i][j] = A[i][j] - f * A[k][j];
-        b[i] = b[i] - f * b[k];
+    const double akk = bcast(a, 7 * k + k);
+    if (akk != 0.0) {
+      const double aik = __shfl(a, live ? 7 * i + k : lane);
+      const double akj = __shfl(a, live ? 7 * k + j : lane);
+      if (live && i > k && j > k) {
+        const double f = aik / akk;
+        a = a - f * akj;
       }
     }
   }
   double det = (double)sign;
 #pragma unroll
-  for (int k = 0; k < 6; ++k) det = det * A[k][k];
+  for (int k = 0; k < 6; ++k) det = det * bcast(a, 7 * k + k);
   if (fabs(det) < 1e-15 || isnan(det)) return 1;
   double x[6];
 #pragma unroll
-  for (int i = 5; i >= 0; --i) {
-    double acc = b[i];
+  for (int r = 5; r >= 0; --r) {
+    double acc = bcast(a, 7 * r + 6);
 #pragma unroll
-    for (int j = i + 1; j < 6; ++j) acc = acc - A[i][j] * x[j];
-    x[i] = acc / A[i][i];
+    for (int c = r + 1; c < 6; ++c) acc = acc - bcast(a, 7 * r + c) * x[c];
+    x[r] = acc / bcast(a, 7 * r + r);
   }
 #pragma unroll
-  for (int i = 0; i < 6; ++i) xo[i] = x[i];
+  for (int r = 0; r < 6; ++r) xo[r] = x[r];
+  // cv::Affine3f(Vec3f rvec, Vec3f t): the Vec3d arguments narrow to float.
   const float rv[3] = {(float)x[0], (float)x[1], (float)x[2]};
   DevPose inc;
   inc.t[0] = (float)x[3];
@@ -549,7 +741,7 @@ __device__ int icp_update(const long long *sums, DevPose &pose, double *xo) {
       sqrt((double)rv[0] * rv[0] + (double)rv[1] * rv[1] + (double)rv[2] * rv[2]);
   if (theta < 2.220446049250313e-16) {
 #pragma unroll
-    for (int i = 0; i < 9; ++i) inc.R[i] = (i % 4 == 0) ? 1.f : 0.f;
+    for (int q = 0; q < 9; ++q) inc.R[q] = (q % 4 == 0) ? 1.f : 0.f;
   } else {
     const double c = cos(theta), sn = sin(theta), c1 = 1.0 - c;
     const double it = 1.0 / theta;
@@ -558,9 +750,9 @@ __device__ int icp_update(const long long *sums, DevPose &pose, double *xo) {
                           r[1] * r[2], r[0] * r[2], r[1] * r[2], r[2] * r[2]};
     const float rx[9] = {0.f, -r[2], r[1], r[2], 0.f, -r[0], -r[1], r[0], 0.f};
 #pragma unroll
-    for (int i = 0; i < 9; ++i) {
-      const float e = (i % 4 == 0) ? 1.f : 0.f;
-      inc.R[i] = ((float)(c * e) + (float)(c1 * rrt[i])) + (float)(sn * rx[i]);
+    for (int q = 0; q < 9; ++q) {
+      const float e = (q % 4 == 0) ? 1.f : 0.f;
+      inc.R[q] = ((float)(c * e) + (float)(c1 * rrt[q])) + (float)(sn * rx[q]);
     }
   }
   pose = pose_mul(pose, inc);
@@ -625,7 +817,7 @@ __device__ __forceinline__ void clip_lin(double alpha, double beta, double &lo, 
 // the reference's bit for bit.
 // kCount: count-only variant (no voxel traffic) giving N_upd / N_col, the
 // algorithmic-byte inputs of the roofline.
-template <bool kCount>
+template <bool kCount, bool kIdx32>
 __global__ __launch_bounds__(256) void k_integrate(VolView v, LevelGeom g,
                                                    const float *__restrict__ dmap,
                                                    const uint8_t *__restrict__ bgr,
@@ -713,6 +905,11 @@ __global__ __launch_bounds__(256) void k_integrate(VolView v, LevelGeom g,
   int z = 1;
 #pragma unroll 8
   for (; z < za; ++z) vc = add(vc, zs);
+  // voxel index of (x, y, z), advanced by one slice per z (32-bit when the
+  // volume has < 2^30 voxels, so byte offsets of the u32 colour fit too)
+  using Idx = typename std::conditional<kIdx32, unsigned, size_t>::type;
+  const Idx slice = (Idx)v.slice;
+  Idx iz = (Idx)base + (Idx)za * slice;
   // Batches of kB voxels: projections, then the kB depth gathers, then the
   // voxel loads of the batch are issued back to back (memory-level
   // parallelism); each voxel's arithmetic is exactly the reference's.
@@ -728,10 +925,11 @@ __global__ __launch_bounds__(256) void k_integrate(VolView v, LevelGeom g,
     for (int j = 0; j < kB; ++j) {
       vc = add(vc, zs);
       n2[j] = dot(vc, vc);
-      const int u = f2i_rn((vc.x / vc.z) * g.fx + g.cx);
-      const int vv = f2i_rn((vc.y / vc.z) * g.fy + g.cy);
-      ok[j] = (z + j <= zb) & (vc.z > 0) & (u >= 0) & (u < g.w) & (vv >= 0) & (vv < g.h);
-      pix[j] = ok[j] ? vv * g.w + u : 0;
+      const float y = 1.f / vc.z;
+      const float uf = proj_rn(vc.x, vc.z, y, g.fx, g.cx);
+      const float vf = proj_rn(vc.y, vc.z, y, g.fy, g.cy);
+      ok[j] = (z + j <= zb) & (vc.z > 0) & (int)in_range(uf, g.w) & (int)in_range(vf, g.h);
+      pix[j] = ok[j] ? (int)vf * g.w + (int)uf : 0;
     }
     // Loads are issued unconditionally (inactive lanes read a dummy element
     // that every such lane shares, so they add no traffic): a predicated load
@@ -748,6 +946,7 @@ __global__ __launch_bounds__(256) void k_integrate(VolView v, LevelGeom g,
       ok[j] = ok[j] & (dep[j] > 0) & (sdf[j] >= -trunc);
     }
     if (kCount) {
+      iz += (Idx)kB * slice;
 #pragma unroll
       for (int j = 0; j < kB; ++j)
         if (ok[j]) {
@@ -757,16 +956,19 @@ __global__ __launch_bounds__(256) void k_integrate(VolView v, LevelGeom g,
       continue;
     }
     int16_t t0[kB], w0[kB];
+    Idx vi[kB];
 #pragma unroll
     for (int j = 0; j < kB; ++j) {
-      const size_t i = ok[j] ? base + (size_t)(z + j) * v.slice : 0;
+      vi[j] = iz + (Idx)j * slice;
+      const Idx i = ok[j] ? vi[j] : 0;
       t0[j] = v.tsdf[i];
       w0[j] = v.weight[i];
     }
+    iz += (Idx)kB * slice;
 #pragma unroll
     for (int j = 0; j < kB; ++j) {
       if (!ok[j]) continue;
-      const size_t i = base + (size_t)(z + j) * v.slice;
+      const Idx i = vi[j];
       const float ts = fminf(1.f, div_rn(sdf[j], trunc, v.inv_trunc));
       const int pre_w = w0[j];
       const float pre_t = (float)t0[j] * kDivShortMax;
@@ -1185,6 +1387,42 @@ int icp_blocks(const LevelGeom &g) {
   return nb < 1 ? 1 : nb;
 }
 
+IcpPlan make_icp_plan(int levels, const LevelGeom *g, const int *iters, FrameView cur,
+                      FrameView prev, float dist_thr, float angle_thr) {
+  IcpPlan pl{};
+  pl.levels = levels;
+  pl.dist_thr = dist_thr;
+  pl.angle_thr = angle_thr;
+  for (int l = 0; l < levels; ++l) {
+    pl.g[l] = g[l];
+    pl.npix[l] = icp_npix(g[l], &pl.xe[l]);
+    pl.groups[l] = (pl.npix[l] + kIcpBlockPix - 1) / kIcpBlockPix;
+    pl.iters[l] = iters[l];
+    pl.cv[l] = cur.v[l];
+    pl.cn[l] = cur.n[l];
+    pl.pv[l] = prev.v[l];
+    pl.pn[l] = prev.n[l];
+    pl.nblocks = std::max(pl.nblocks, pl.groups[l]);
+    pl.slots += iters[l];
+  }
+  pl.nblocks = std::max(pl.nblocks, 1);
+  return pl;
+}
+
+bool icp_persistent_ok(const IcpPlan &pl, int device) {
+  if (pl.slots > kIcpMaxSlots) return false;
+  int per_cu = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_icp_track, 256, 0) != hipSuccess)
+    return false;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
+    return false;
+  return (long long)per_cu * cus >= pl.nblocks;
+}
+
+void launch_icp_track(hipStream_t s, const IcpPlan &pl, DevState *st, IcpSync *sync) {
+  hipLaunchKernelGGL(k_icp_track, dim3(pl.nblocks), dim3(256), 0, s, pl, st, sync);
+}
+
 void launch_icp(hipStream_t s, const LevelGeom &g, const float *cv, const float *cn,
                 const float *pv, const float *pn, float dist_thr, float angle_thr, DevState *st,
                 unsigned long long *shards, unsigned *ticket, int force, int update) {
@@ -1201,12 +1439,16 @@ void launch_integrate(hipStream_t s, VolView v, LevelGeom g0, const float *dmap,
   // z-chunks so that >= 16 waves per SIMD exist (16384 waves on 1024 SIMDs)
   const int nchunk = std::max(1, std::min(8, (16384 + tiles - 1) / tiles));
   dim3 grd((tiles + 3) / 4, nchunk);
+  const bool idx32 = v.slice * (size_t)v.Z < (1ull << 30);
   if (counters)
-    hipLaunchKernelGGL(k_integrate<true>, grd, dim3(256), 0, s, v, g0, dmap, bgr, inv_lambda, st,
-                       log, vpose, xpose, counters);
+    hipLaunchKernelGGL((k_integrate<true, false>), grd, dim3(256), 0, s, v, g0, dmap, bgr,
+                       inv_lambda, st, log, vpose, xpose, counters);
+  else if (idx32)
+    hipLaunchKernelGGL((k_integrate<false, true>), grd, dim3(256), 0, s, v, g0, dmap, bgr,
+                       inv_lambda, st, log, vpose, xpose, counters);
   else
-    hipLaunchKernelGGL(k_integrate<false>, grd, dim3(256), 0, s, v, g0, dmap, bgr, inv_lambda, st,
-                       log, vpose, xpose, counters);
+    hipLaunchKernelGGL((k_integrate<false, false>), grd, dim3(256), 0, s, v, g0, dmap, bgr,
+                       inv_lambda, st, log, vpose, xpose, counters);
 }
 
 void launch_raycast(hipStream_t s, VolView v, int levels, const LevelGeom *g, FrameView cur,

@@ -28,7 +28,7 @@ LIB_PATH = os.path.join(_PKG, "lib", "libkfx.so")
 EXPORTS = [
     "kfx_abi_version", "kfx_last_error", "kfx_default_params", "kfx_create", "kfx_destroy", "kfx_reset",
     "kfx_pipeline", "kfx_pipeline_u16", "kfx_stage_frames", "kfx_pipeline_staged", "kfx_synchronize",
-    "kfx_set_graph_mode", "kfx_get_cur_camera_pose", "kfx_get_frame_count", "kfx_get_pose_record",
+    "kfx_set_graph_mode", "kfx_set_icp_persistent", "kfx_get_icp_trace", "kfx_get_cur_camera_pose", "kfx_get_frame_count", "kfx_get_pose_record",
     "kfx_write_poses_txt", "kfx_get_frame_maps", "kfx_set_frame_maps", "kfx_download_tsdf",
     "kfx_upload_tsdf", "kfx_download_volume_soa", "kfx_stage_preprocess", "kfx_stage_icp_accumulate",
     "kfx_stage_icp", "kfx_stage_integrate", "kfx_stage_raycast", "kfx_set_profiling", "kfx_get_stage_ms",
@@ -71,6 +71,8 @@ def lib():
         "kfx_pipeline_staged": ([vp, i], i),
         "kfx_synchronize": ([vp], i),
         "kfx_set_graph_mode": ([vp, i], i),
+        "kfx_set_icp_persistent": ([vp, i], i),
+        "kfx_get_icp_trace": ([vp, P(C.c_uint64), i], i),
         "kfx_get_cur_camera_pose": ([vp, P(Pose)], i),
         "kfx_get_frame_count": ([vp, P(i)], i),
         "kfx_get_pose_record": ([vp, P(Pose), i, P(i)], i),
@@ -182,6 +184,20 @@ class KinectFusion:
 
     def set_graph_mode(self, on: bool):
         _check(lib().kfx_set_graph_mode(self._h, int(on)), "kfx_set_graph_mode")
+
+    def set_icp_persistent(self, on: bool) -> bool:
+        """Toggle the one-launch persistent ICP kernel; returns whether it is usable here."""
+        r = lib().kfx_set_icp_persistent(self._h, int(on))
+        _check(min(r, 0), "kfx_set_icp_persistent")
+        return bool(r)
+
+    def icp_trace(self):
+        """(iterations, 5) s_memrealtime stamps of the last persistent-ICP frame."""
+        import numpy as np
+        out = np.zeros((64, 12), np.uint64)
+        n = _check(lib().kfx_get_icp_trace(self._h, out.ctypes.data_as(C.POINTER(C.c_uint64)), 64),
+                   "kfx_get_icp_trace", ok=tuple(range(65)))
+        return out[:n]
 
     def set_profiling(self, on: bool):
         _check(lib().kfx_set_profiling(self._h, int(on)), "kfx_set_profiling")

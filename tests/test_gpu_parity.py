@@ -241,14 +241,17 @@ def test_pipeline_matches_oracle(which, seq_qvga, seq_vga):
 
 
 def test_pipeline_modes_and_inputs_identical(seq_qvga):
-    """graph / eager / profiled launches and u16 / f32 / staged inputs all give
-    the same poses and volume."""
+    """graph / eager / profiled launches, u16 / f32 / staged inputs and the
+    persistent vs per-iteration ICP launches all give the same poses and volume."""
     bgr, dep, gt = seq_qvga
     intr = synth.Intrinsics.qvga()
     res = []
-    for mode in ("graph", "eager", "profile", "u16", "staged"):
+    for mode in ("graph", "eager", "profile", "u16", "staged", "icp_per_iter"):
         kf, p = make(intr, dims=64)
         if mode == "eager":
+            kf.set_graph_mode(False)
+        if mode == "icp_per_iter":
+            assert kf.set_icp_persistent(False)  # persistent path was the one in use
             kf.set_graph_mode(False)
         if mode == "profile":
             kf.set_profiling(True)

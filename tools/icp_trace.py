@@ -1,0 +1,33 @@
+#!/usr/bin/env python3
+"""Phase timing of the persistent ICP kernel on a VGA 512^3 run (GPU box)."""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "slam-kinectfusion_amd"))
+import kfx  # noqa: E402
+from kfx import synth  # noqa: E402
+from kfx.abi import default_params  # noqa: E402
+
+intr = synth.Intrinsics.vga()
+kf = kfx.KinectFusion(intr, default_params())
+bgr, dep, _ = synth.sequence(8, intr)
+for k in range(len(dep)):
+    kf.pipeline(bgr[k], dep[k].astype(np.float32))
+kf.synchronize()
+tr = kf.icp_trace().astype(np.int64)
+t0 = tr[0, 0]
+print("iter  start  b0_arrive  last_arrive  release  solved   (us from frame ICP start; 100 MHz)")
+for i, r in enumerate(tr):
+    f = lambda v: (v - t0) / 100.0
+    print(f"{i:3d} {f(r[0]):7.2f} {f(r[1]):9.2f} {f(r[4]):11.2f} {f(r[2]):8.2f} {f(r[3]):7.2f}")
+print("per-iteration (release-start):", np.round((tr[:, 2] - tr[:, 0]) / 100.0, 2))
+print("lane (load+gather+products):", np.round((tr[:, 8] - tr[:, 0]) / 100.0, 2))
+print("block reduce:", np.round((tr[:, 9] - tr[:, 8]) / 100.0, 2))
+print("atomics:", np.round((tr[:, 10] - tr[:, 9]) / 100.0, 2))
+print("arrive:", np.round((tr[:, 1] - tr[:, 10]) / 100.0, 2))
+print("sums read:", np.round((tr[:, 5] - tr[:, 2]) / 100.0, 2))
+print("solve:", np.round((tr[:, 6] - tr[:, 5]) / 100.0, 2))
+print("post-solve:", np.round((tr[:, 3] - tr[:, 6]) / 100.0, 2))
