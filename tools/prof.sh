@@ -1,0 +1,31 @@
+#!/bin/bash
+# One profiling session on the GPU box (run from the repo root through gpurun):
+#   1. rocprofv3 --kernel-trace --stats of a short bench run  -> gpurun_out/prof/stats
+#   2. FETCH_SIZE / WRITE_SIZE calibration streams             -> gpurun_out/prof/calib
+#   3. FETCH_SIZE and WRITE_SIZE passes over the same bench    -> gpurun_out/prof/pmc
+# Every rocprofv3 run is its own process under its own time limit; counters are
+# never combined with trace domains (MI355X_MICROARCH.md, rocprofv3 section).
+# usage: tools/prof.sh [bench args...]
+set -o pipefail
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
+cd /tmp && export TMPDIR=/tmp
+ARGS=${@:-"--steps 100 --warmup 20 --profile-frames 4 --cpu-frames 0"}
+OUT="$ROOT/gpurun_out/prof"
+mkdir -p "$OUT"
+run() {  # name, timeout, rocprof args...
+  local name=$1 secs=$2
+  shift 2
+  echo "=== $name"
+  timeout -k 10 "$secs" rocprofv3 "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "rc=$rc"
+  [ $rc -eq 0 ] || { tail -20 "$OUT/$name.log"; exit $rc; }
+}
+run stats 240 --kernel-trace --stats --output-format csv -d "$OUT/stats" -o run -- python3 "$ROOT/bench.py" $ARGS
+if [ -x "$ROOT/tools/build/pmc_calib" ]; then
+  run calib_fetch 90 --pmc FETCH_SIZE --output-format csv -d "$OUT/calib/FETCH_SIZE" -- "$ROOT/tools/build/pmc_calib"
+  run calib_write 90 --pmc WRITE_SIZE --output-format csv -d "$OUT/calib/WRITE_SIZE" -- "$ROOT/tools/build/pmc_calib"
+fi
+run pmc_fetch 240 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc/FETCH_SIZE" -- python3 "$ROOT/bench.py" $ARGS
+run pmc_write 240 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc/WRITE_SIZE" -- python3 "$ROOT/bench.py" $ARGS
+python3 "$ROOT/tools/traffic.py" "$OUT"

@@ -1,0 +1,86 @@
+#!/usr/bin/env python3
+"""Per-launch HBM traffic of the kfx kernels from rocprofv3 PMC passes.
+
+Input: the directory tools/prof.sh writes (gpurun_out/prof):
+  calib/{FETCH_SIZE,WRITE_SIZE}/**/counter_collection.csv  known-byte streams (tools/pmc_calib.hip)
+  pmc/{FETCH_SIZE,WRITE_SIZE}/**/counter_collection.csv    the bench run
+  stats/**/*kernel_stats.csv                               rocprofv3 --stats summary
+
+FETCH_SIZE / WRITE_SIZE are converted to bytes with the calibration factors of
+the 2-byte streams (the width of the tsdf/weight arrays that dominate integrate
+and raycast): factor = counter value per dispatch / bytes the stream moved
+(MI355X_MICROARCH.md: only 16-B/lane streams are calibrated there, other widths
+must be calibrated on a known byte count).  Output: <dir>/traffic.json, and
+profiles/integrate_pmc.json when --commit is given (bench.py reads that file
+for roofline.traffic).
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+CALIB_BYTES = 512 << 20  # each calibration kernel streams 512 MiB once
+
+
+def short(name):
+    name = name.replace("void ", "")
+    for p in ("kfx::(anonymous namespace)::", "kfx::"):
+        name = name.replace(p, "")
+    return name.split("(")[0].strip()
+
+
+def per_kernel(root):
+    agg = collections.defaultdict(list)
+    for f in glob.glob(f"{root}/**/*counter_collection.csv", recursive=True):
+        for r in csv.DictReader(open(f)):
+            agg[short(r.get("Kernel_Name", "?"))].append(float(r["Counter_Value"]))
+    return {k: (sum(v) / len(v), len(v)) for k, v in agg.items()}
+
+
+def main():
+    root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/prof"
+    commit = "--commit" in sys.argv
+    out = {"calibration": {}, "kernels": {}}
+    fac = {}
+    for c in ("FETCH_SIZE", "WRITE_SIZE"):
+        cal = per_kernel(f"{root}/calib/{c}")
+        want = "k_read<unsigned short>" if c == "FETCH_SIZE" else "k_write<unsigned short>"
+        for k, (v, n) in cal.items():
+            out["calibration"][f"{c}:{k}"] = {"per_dispatch": v, "units_per_byte": v / CALIB_BYTES}
+        hit = [v for k, (v, n) in cal.items() if k.startswith(want)]
+        fac[c] = (hit[0] / CALIB_BYTES) if hit else None
+    out["factor_units_per_byte"] = fac
+    fetch = per_kernel(f"{root}/pmc/FETCH_SIZE")
+    write = per_kernel(f"{root}/pmc/WRITE_SIZE")
+    for k in sorted(set(fetch) | set(write)):
+        f, nf = fetch.get(k, (None, 0))
+        w, nw = write.get(k, (None, 0))
+        rec = {"FETCH_SIZE": f, "WRITE_SIZE": w, "dispatches": max(nf, nw)}
+        if f is not None and fac.get("FETCH_SIZE"):
+            rec["read_bytes"] = f / fac["FETCH_SIZE"]
+        if w is not None and fac.get("WRITE_SIZE"):
+            rec["write_bytes"] = w / fac["WRITE_SIZE"]
+        if "read_bytes" in rec and "write_bytes" in rec:
+            rec["hbm_bytes_per_launch"] = rec["read_bytes"] + rec["write_bytes"]
+        out["kernels"][k] = rec
+    json.dump(out, open(f"{root}/traffic.json", "w"), indent=1)
+    for k, r in out["kernels"].items():
+        if k.startswith("k_"):
+            print(f"{k:40s} n={r['dispatches']:5d} hbm/launch={r.get('hbm_bytes_per_launch', float('nan')) / 1e6:10.2f} MB")
+    if commit:
+        integ = [r for k, r in out["kernels"].items()
+                 if k.startswith("k_integrate<false") and "hbm_bytes_per_launch" in r]
+        if integ:
+            r = max(integ, key=lambda r: r["dispatches"])
+            prof = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles")
+            json.dump({"kernel": "k_integrate", "hbm_bytes_per_launch": int(r["hbm_bytes_per_launch"]),
+                       "read_bytes": int(r["read_bytes"]), "write_bytes": int(r["write_bytes"]),
+                       "dispatches": r["dispatches"], "factor_units_per_byte": fac,
+                       "source": "tools/prof.sh FETCH_SIZE/WRITE_SIZE passes, 2-byte stream calibration"},
+                      open(os.path.join(prof, "integrate_pmc.json"), "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
