@@ -39,6 +39,9 @@ extern "C" {
 #define KFX_ERR_OOM (-3)
 #define KFX_ERR_STATE (-4)
 #define KFX_ERR_NO_DEVICE (-5)
+#define KFX_ERR_COMM (-6)
+
+#define KFX_COMM_ID_BYTES 128
 
 /* kf::Intrinsics (types.hpp:13-29).  `c` (types.hpp:17) is unused on the path. */
 typedef struct kfx_intrinsics {
@@ -175,6 +178,29 @@ int kfx_get_stage_ms(kfx_ctx *ctx, float out_ms[5]);
  * updated and those whose colour was also blended.  Count-only kernel, the
  * volume is not touched. */
 int kfx_integrate_counts(kfx_ctx *ctx, int64_t *n_updated, int64_t *n_colored);
+
+/* ---- Z-slab sharding (new; the reference is single-GPU) -------------------
+ * One kf::kinectfusion stream split over `world` GPUs: slab
+ * `rank` owns global z slices [Z*rank/world, Z*(rank+1)/world) of the volume
+ * and stores 4 halo slices on each side, which it integrates itself.
+ * Preprocess and ICP run on every slab (identical results, no collective);
+ * raycast events are combined across slabs each frame (all-reduce MIN of the
+ * per-pixel event sample index, then all-reduce MAX of the winner's map bits),
+ * so every slab ends each frame with the same poses and model maps as a
+ * single-GPU kfx_create context, bit for bit. */
+int kfx_create_slab(const kfx_intrinsics *intr, const kfx_params *params, int device,
+                    int rank, int world, kfx_ctx **out);
+/* stored slices [zb, zb+zn), owned slices [own0, own1) */
+int kfx_slab_info(kfx_ctx *ctx, int *zb, int *zn, int *own0, int *own1);
+/* One process per GPU: rank 0 creates the id, every rank passes it to
+ * kfx_comm_init (RCCL over xGMI); kfx_pipeline* then combine through RCCL. */
+int kfx_comm_get_unique_id(uint8_t id[KFX_COMM_ID_BYTES]);
+int kfx_comm_init(kfx_ctx *ctx, const uint8_t id[KFX_COMM_ID_BYTES]);
+/* One process driving all slabs (members k = slab k of n, no communicator; on
+ * one GPU or on several with peer access): one pipeline() frame. */
+int kfx_pipeline_group(kfx_ctx **ctxs, int n, const uint8_t *bgr, const float *depth_mm);
+/* kfx_download_tsdf / kfx_download_volume_soa on a slab write its owned slices
+ * only (at their global offsets); kfx_upload_tsdf reads its stored slices. */
 
 #ifdef __cplusplus
 }

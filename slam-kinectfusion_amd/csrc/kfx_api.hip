@@ -11,6 +11,8 @@
 #include <string>
 #include <vector>
 
+#include <rccl/rccl.h>
+
 #include "../../include/kfx.h"
 #include "kfx_internal.h"
 
@@ -112,6 +114,13 @@ struct kfx_ctx {
   float stage_ms[5]{};
   int pending = 0;      // frames enqueued since the last host sync
   int known_poses = 1;  // n_poses at the last sync
+
+  // Z-slab sharding: this context owns slab `rank` of `world`
+  bool slab = false;
+  int rank = 0, world = 1;
+  uint32_t *key_local = nullptr;  // per-pixel sample index of this slab's decisive event
+  uint32_t *key_min = nullptr;    // all-reduce MIN of key_local over the slabs
+  ncclComm_t comm = nullptr;      // RCCL communicator over the slab ranks (one process per GPU)
 };
 
 namespace {
@@ -131,7 +140,7 @@ int dalloc(kfx_ctx *c, void **p, size_t bytes) {
   return KFX_OK;
 }
 
-size_t nvox(const kfx_ctx *c) { return c->vol.slice * (size_t)c->vol.Z; }
+size_t nvox(const kfx_ctx *c) { return c->vol.local_voxels(); }
 
 void destroy_graphs(kfx_ctx *c) {
   for (auto &gx : c->graph)
@@ -154,8 +163,44 @@ struct FrameInput {
 };
 
 // The per-frame launch sequence (kinectfusion.cpp:78-127 with the frame-1 and
-// failure branches resolved on the device).  ev != nullptr records stage events.
-void enqueue_frame(kfx_ctx *c, FrameInput in, bool events) {
+// failure branches resolved on the device).  `events` records stage events.
+// Slab contexts stop after their local raycast (enqueue_local) and then
+// combine the slabs' raycast results (enqueue_combine).
+void enqueue_local(kfx_ctx *c, FrameInput in, bool events);
+int enqueue_combine(kfx_ctx *c);
+
+int enqueue_frame(kfx_ctx *c, FrameInput in, bool events) {
+  enqueue_local(c, in, events);
+  int r = KFX_OK;
+  if (c->slab) r = enqueue_combine(c);
+  if (events) (void)hipEventRecord(c->ev[4], c->stream);
+  return r;
+}
+
+#define NCCLCHK(expr)                                                                      \
+  do {                                                                                     \
+    ncclResult_t e_ = (expr);                                                              \
+    if (e_ != ncclSuccess)                                                                 \
+      return set_err(KFX_ERR_COMM, std::string(#expr) + ": " + ncclGetErrorString(e_));    \
+  } while (0)
+
+// Cross-slab raycast combine: all-reduce MIN of the per-pixel
+// event keys, each slab clears the pixels it lost, all-reduce MAX of the map
+// bits (level-0 vmap and nmap are one contiguous buffer), then the pyramid.
+int enqueue_combine(kfx_ctx *c) {
+  hipStream_t s = c->stream;
+  const size_t np = (size_t)c->g[0].w * c->g[0].h;
+  if (c->world > 1 || c->comm) {
+    if (!c->comm) return set_err(KFX_ERR_STATE, "slab context without a communicator (kfx_comm_init, or kfx_pipeline_group)");
+    NCCLCHK(ncclAllReduce(c->key_local, c->key_min, np, ncclUint32, ncclMin, c->comm, s));
+    launch_slab_mask(s, c->key_local, c->key_min, c->prev.v[0], c->prev.n[0], (int)np);
+    NCCLCHK(ncclAllReduce(c->prev.v[0], c->prev.v[0], 6 * np, ncclUint32, ncclMax, c->comm, s));
+  }
+  launch_resize(s, c->L, c->g, c->cur, c->prev, c->st, nullptr);
+  return KFX_OK;
+}
+
+void enqueue_local(kfx_ctx *c, FrameInput in, bool events) {
   hipStream_t s = c->stream;
   if (events) (void)hipEventRecord(c->ev[0], s);
   // imageProcess (kinectfusion.cpp:48-76)
@@ -189,15 +234,19 @@ void enqueue_frame(kfx_ctx *c, FrameInput in, bool events) {
                    to_dev(c->p.volu_pose), nullptr, nullptr);
   if (events) (void)hipEventRecord(c->ev[3], s);
   launch_raycast(s, c->vol, c->L, c->g, c->cur, c->prev, c->st, c->pose_log,
-                 to_dev(c->p.volu_pose), nullptr);
-  if (events) (void)hipEventRecord(c->ev[4], s);
+                 to_dev(c->p.volu_pose), nullptr, c->slab ? c->key_local : nullptr);
 }
 
 int build_graph(kfx_ctx *c, FrameInput in, hipGraphExec_t *out) {
   hipGraph_t graph = nullptr;
   HIPCHK(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-  enqueue_frame(c, in, false);
-  HIPCHK(hipStreamEndCapture(c->stream, &graph));
+  const int r = enqueue_frame(c, in, false);
+  const hipError_t ec = hipStreamEndCapture(c->stream, &graph);
+  if (r) {
+    if (graph) (void)hipGraphDestroy(graph);
+    return r;
+  }
+  if (ec != hipSuccess) return set_err(KFX_ERR_HIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(ec));
   hipError_t e = hipGraphInstantiate(out, graph, nullptr, nullptr, 0);
   (void)hipGraphDestroy(graph);
   if (e != hipSuccess) return set_err(KFX_ERR_HIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(e));
@@ -250,20 +299,31 @@ int run_frame(kfx_ctx *c, FrameInput in, hipGraphExec_t *graph) {
   if (r) return r;
   c->last_bgr = in.bgr;
   if (c->profiling) {
-    enqueue_frame(c, in, true);
+    if ((r = enqueue_frame(c, in, true))) return r;
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventSynchronize(c->ev[4]));
     for (int i = 0; i < 4; ++i) HIPCHK(hipEventElapsedTime(&c->stage_ms[i], c->ev[i], c->ev[i + 1]));
     HIPCHK(hipEventElapsedTime(&c->stage_ms[4], c->ev[0], c->ev[4]));
-    // stage order in the events: preprocess, icp(+commit), integrate, raycast(+resize)
+    // stage order in the events: preprocess, icp(+commit), integrate,
+    // raycast(+slab combine, +resize)
   } else if (c->graph_mode && graph) {
     if (!*graph) {
       r = build_graph(c, in, graph);
+      if (r && c->comm) {
+        // RCCL calls that refuse stream capture: run this context eagerly
+        (void)hipGetLastError();
+        c->graph_mode = false;
+        destroy_graphs(c);
+        if ((r = enqueue_frame(c, in, false))) return r;
+        HIPCHK(hipGetLastError());
+        c->pending += 1;
+        return KFX_OK;
+      }
       if (r) return r;
     }
     HIPCHK(hipGraphLaunch(*graph, c->stream));
   } else {
-    enqueue_frame(c, in, false);
+    if ((r = enqueue_frame(c, in, false))) return r;
     HIPCHK(hipGetLastError());
   }
   c->pending += 1;
@@ -282,11 +342,22 @@ int finish_frame(kfx_ctx *c) {
   return s.last_fail ? KFX_TRACKING_LOST : KFX_OK;
 }
 
-VolView make_vol(const kfx_params &p) {
+// Slab `rank` of `world` owns global slices [Z*rank/world, Z*(rank+1)/world)
+// and stores kSlabHalo more on each side (clipped to the volume).
+VolView make_vol(const kfx_params &p, int rank, int world) {
   VolView v{};
   v.X = p.volu_dims[0];
   v.Y = p.volu_dims[1];
   v.Z = p.volu_dims[2];
+  v.own0 = (int)((long long)v.Z * rank / world);
+  v.own1 = (int)((long long)v.Z * (rank + 1) / world);
+  if (world > 1) {
+    v.zb = std::max(0, v.own0 - kSlabHalo);
+    v.zn = std::min(v.Z, v.own1 + kSlabHalo) - v.zb;
+  } else {
+    v.zb = 0;
+    v.zn = v.Z;
+  }
   v.tiles_x = v.X / 8;
   v.tiles_y = v.Y / 8;
   v.slice = (size_t)v.X * v.Y;
@@ -369,7 +440,23 @@ int kfx_default_params(kfx_params *p) {
   return KFX_OK;
 }
 
+static int create_impl(const kfx_intrinsics *intr, const kfx_params *params, int device,
+                       int rank, int world, bool slab, kfx_ctx **out);
+
 int kfx_create(const kfx_intrinsics *intr, const kfx_params *params, int device, kfx_ctx **out) {
+  return create_impl(intr, params, device, 0, 1, false, out);
+}
+
+int kfx_create_slab(const kfx_intrinsics *intr, const kfx_params *params, int device, int rank,
+                    int world, kfx_ctx **out) {
+  if (world < 1 || rank < 0 || rank >= world) return set_err(KFX_ERR_ARG, "bad rank/world");
+  if (params && params->volu_dims[2] < 2 * world)
+    return set_err(KFX_ERR_ARG, "fewer than 2 slices per slab");
+  return create_impl(intr, params, device, rank, world, true, out);
+}
+
+static int create_impl(const kfx_intrinsics *intr, const kfx_params *params, int device,
+                       int rank, int world, bool slab, kfx_ctx **out) {
   if (!intr || !params || !out) return set_err(KFX_ERR_ARG, "null argument");
   *out = nullptr;
   const kfx_params &p = *params;
@@ -401,6 +488,9 @@ int kfx_create(const kfx_intrinsics *intr, const kfx_params *params, int device,
 
   kfx_ctx *c = new kfx_ctx();
   c->device = device;
+  c->slab = slab;
+  c->rank = rank;
+  c->world = world;
   c->intr = *intr;
   c->p = p;
   c->L = p.pyramid_height;
@@ -423,14 +513,19 @@ int kfx_create(const kfx_intrinsics *intr, const kfx_params *params, int device,
     if ((r = dalloc(c, (void **)&c->cur.d[l], np * 4))) return fail(r);
     if ((r = dalloc(c, (void **)&c->cur.v[l], np * 12))) return fail(r);
     if ((r = dalloc(c, (void **)&c->cur.n[l], np * 12))) return fail(r);
-    if ((r = dalloc(c, (void **)&c->prev.v[l], np * 12))) return fail(r);
-    if ((r = dalloc(c, (void **)&c->prev.n[l], np * 12))) return fail(r);
+    // prev vmap|nmap of a level are one buffer (one collective in the slab combine)
+    if ((r = dalloc(c, (void **)&c->prev.v[l], np * 24))) return fail(r);
+    c->prev.n[l] = c->prev.v[l] + 3 * np;
   }
   const size_t np0 = (size_t)intr->width * intr->height;
+  if (slab) {
+    if ((r = dalloc(c, (void **)&c->key_local, np0 * 4))) return fail(r);
+    if ((r = dalloc(c, (void **)&c->key_min, np0 * 4))) return fail(r);
+  }
   if ((r = dalloc(c, (void **)&c->raw0_u16, np0 * 2))) return fail(r);
   if ((r = dalloc(c, (void **)&c->bgr, np0 * 3))) return fail(r);
   if ((r = dalloc(c, (void **)&c->inv_lambda, np0 * 4))) return fail(r);
-  c->vol = make_vol(p);
+  c->vol = make_vol(p, rank, world);
   const size_t n = nvox(c);
   if ((r = dalloc(c, (void **)&c->vol.tsdf, n * 2))) return fail(r);
   if ((r = dalloc(c, (void **)&c->vol.weight, n * 2))) return fail(r);
@@ -458,6 +553,7 @@ int kfx_destroy(kfx_ctx *c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   destroy_graphs(c);
+  if (c->comm) (void)ncclCommDestroy(c->comm);
   for (void *a : c->allocs) (void)hipFree(a);
   for (auto &e : c->ev)
     if (e) (void)hipEventDestroy(e);
@@ -682,8 +778,8 @@ int kfx_download_tsdf(kfx_ctx *c, void *dst) {
   const int nz = slab_z(c, 8);
   uint64_t *tmp = nullptr;
   HIPCHK(hipMalloc(&tmp, c->vol.slice * 8 * (size_t)nz));
-  for (int z0 = 0; z0 < c->vol.Z; z0 += nz) {
-    const int k = std::min(nz, c->vol.Z - z0);
+  for (int z0 = c->vol.own0; z0 < c->vol.own1; z0 += nz) {  // owned slices only
+    const int k = std::min(nz, c->vol.own1 - z0);
     launch_export_records(c->stream, c->vol, z0, k, tmp);
     hipError_t e = hipMemcpyAsync((char *)dst + c->vol.slice * 8 * (size_t)z0, tmp,
                                   c->vol.slice * 8 * (size_t)k, hipMemcpyDeviceToHost, c->stream);
@@ -705,8 +801,9 @@ int kfx_upload_tsdf(kfx_ctx *c, const void *src) {
   const int nz = slab_z(c, 8);
   uint64_t *tmp = nullptr;
   HIPCHK(hipMalloc(&tmp, c->vol.slice * 8 * (size_t)nz));
-  for (int z0 = 0; z0 < c->vol.Z; z0 += nz) {
-    const int k = std::min(nz, c->vol.Z - z0);
+  const int zend = c->vol.zb + c->vol.zn;
+  for (int z0 = c->vol.zb; z0 < zend; z0 += nz) {  // stored slices, halo included
+    const int k = std::min(nz, zend - z0);
     hipError_t e = hipMemcpyAsync(tmp, (const char *)src + c->vol.slice * 8 * (size_t)z0,
                                   c->vol.slice * 8 * (size_t)k, hipMemcpyHostToDevice, c->stream);
     if (e == hipSuccess) {
@@ -732,8 +829,8 @@ int kfx_download_volume_soa(kfx_ctx *c, int16_t *t, int16_t *w, uint8_t *rgba) {
   int16_t *dt = (int16_t *)tmp;
   int16_t *dw = (int16_t *)(tmp + cap * 2);
   uint32_t *dc = (uint32_t *)(tmp + cap * 4);
-  for (int z0 = 0; z0 < c->vol.Z; z0 += nz) {
-    const int k = std::min(nz, c->vol.Z - z0);
+  for (int z0 = c->vol.own0; z0 < c->vol.own1; z0 += nz) {  // owned slices only
+    const int k = std::min(nz, c->vol.own1 - z0);
     const size_t cnt = c->vol.slice * (size_t)k, off = c->vol.slice * (size_t)z0;
     launch_export_soa(c->stream, c->vol, z0, k, dt, dw, dc);
     hipError_t e = hipSuccess;
@@ -871,12 +968,118 @@ int kfx_stage_raycast(kfx_ctx *c, const kfx_pose *cam2vol, const float Rinv[9]) 
   std::memcpy(xp, cam2vol->R, sizeof(float) * 9);
   std::memcpy(xp + 9, cam2vol->t, sizeof(float) * 3);
   std::memcpy(xp + 12, Rinv, sizeof(float) * 9);
+  if (c->slab && c->world > 1) return set_err(KFX_ERR_STATE, "stage_raycast on one slab of several");
   HIPCHK(hipMemcpyAsync(c->xpose, xp, sizeof(xp), hipMemcpyHostToDevice, c->stream));
   launch_raycast(c->stream, c->vol, c->L, c->g, c->cur, c->prev, c->st, c->pose_log,
-                 to_dev(c->p.volu_pose), c->xpose);
+                 to_dev(c->p.volu_pose), c->xpose, c->slab ? c->key_local : nullptr);
+  if (c->slab) launch_resize(c->stream, c->L, c->g, c->cur, c->prev, c->st, c->xpose);
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(c->stream));
   return KFX_OK;
+}
+
+// ---- Z-slab sharding -------------------------------------------------------
+
+int kfx_slab_info(kfx_ctx *c, int *zb, int *zn, int *own0, int *own1) {
+  if (!c) return set_err(KFX_ERR_ARG, "null context");
+  if (zb) *zb = c->vol.zb;
+  if (zn) *zn = c->vol.zn;
+  if (own0) *own0 = c->vol.own0;
+  if (own1) *own1 = c->vol.own1;
+  return KFX_OK;
+}
+
+int kfx_comm_get_unique_id(uint8_t id[KFX_COMM_ID_BYTES]) {
+  if (!id) return set_err(KFX_ERR_ARG, "null id");
+  static_assert(sizeof(ncclUniqueId) == KFX_COMM_ID_BYTES, "RCCL unique id size");
+  ncclUniqueId u;
+  NCCLCHK(ncclGetUniqueId(&u));
+  std::memcpy(id, &u, sizeof(u));
+  return KFX_OK;
+}
+
+int kfx_comm_init(kfx_ctx *c, const uint8_t id[KFX_COMM_ID_BYTES]) {
+  int r = check_ctx(c);
+  if (r) return r;
+  if (!id) return set_err(KFX_ERR_ARG, "null id");
+  if (!c->slab) return set_err(KFX_ERR_STATE, "kfx_comm_init needs a slab context (kfx_create_slab)");
+  if (c->comm) return set_err(KFX_ERR_STATE, "communicator already initialised");
+  ncclUniqueId u;
+  std::memcpy(&u, id, sizeof(u));
+  NCCLCHK(ncclCommInitRank(&c->comm, c->world, u, c->rank));
+  destroy_graphs(c);
+  return KFX_OK;
+}
+
+int kfx_pipeline_group(kfx_ctx **cs, int n, const uint8_t *bgr, const float *depth_mm) {
+  if (!cs || n < 1 || n > kMaxGroup) return set_err(KFX_ERR_ARG, "group size must be 1..16");
+  if (!bgr || !depth_mm) return set_err(KFX_ERR_ARG, "null image");
+  for (int k = 0; k < n; ++k) {
+    kfx_ctx *c = cs[k];
+    if (!c || !c->slab || c->world != n || c->rank != k || c->comm)
+      return set_err(KFX_ERR_ARG, "group member k must be slab k of n without a communicator");
+    if (c->intr.width != cs[0]->intr.width || c->intr.height != cs[0]->intr.height)
+      return set_err(KFX_ERR_ARG, "group members differ in image size");
+  }
+  const size_t np = (size_t)cs[0]->intr.width * cs[0]->intr.height;
+  for (int k = 0; k < n; ++k) {  // members on other devices are read by peer access
+    for (int j = 0; j < n; ++j) {
+      if (cs[j]->device == cs[k]->device) continue;
+      (void)hipSetDevice(cs[k]->device);
+      (void)hipDeviceEnablePeerAccess(cs[j]->device, 0);
+      (void)hipGetLastError();
+    }
+  }
+  int r;
+  for (int k = 0; k < n; ++k) {  // local phase: preprocess, ICP, integrate, slab raycast
+    kfx_ctx *c = cs[k];
+    if ((r = check_ctx(c))) return r;
+    if ((r = ensure_pose_capacity(c, 1))) return r;
+    HIPCHK(hipMemcpyAsync(c->raw[0], depth_mm, np * 4, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->bgr, bgr, np * 3, hipMemcpyHostToDevice, c->stream));
+    c->last_bgr = c->bgr;
+    enqueue_local(c, {c->raw[0], nullptr, c->bgr}, false);
+    HIPCHK(hipGetLastError());
+  }
+  for (int k = 0; k < n; ++k) {
+    if ((r = check_ctx(cs[k]))) return r;
+    HIPCHK(hipStreamSynchronize(cs[k]->stream));
+  }
+  // combine, with the reductions of the collective path run by one kernel over
+  // every member's buffer
+  uint32_t *kin[kMaxGroup], *kout[kMaxGroup], *pay[kMaxGroup];
+  for (int k = 0; k < n; ++k) {
+    kin[k] = cs[k]->key_local;
+    kout[k] = cs[k]->key_min;
+    pay[k] = reinterpret_cast<uint32_t *>(cs[k]->prev.v[0]);
+  }
+  kfx_ctx *c0 = cs[0];
+  if ((r = check_ctx(c0))) return r;
+  launch_group_reduce(c0->stream, kin, n, kout, n, np, false);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(c0->stream));
+  for (int k = 0; k < n; ++k) {
+    if ((r = check_ctx(cs[k]))) return r;
+    launch_slab_mask(cs[k]->stream, cs[k]->key_local, cs[k]->key_min, cs[k]->prev.v[0],
+                     cs[k]->prev.n[0], (int)np);
+    HIPCHK(hipStreamSynchronize(cs[k]->stream));
+  }
+  if ((r = check_ctx(c0))) return r;
+  launch_group_reduce(c0->stream, pay, n, pay, n, 6 * np, true);
+  HIPCHK(hipStreamSynchronize(c0->stream));
+  int status = KFX_OK;
+  for (int k = 0; k < n; ++k) {
+    kfx_ctx *c = cs[k];
+    if ((r = check_ctx(c))) return r;
+    launch_resize(c->stream, c->L, c->g, c->cur, c->prev, c->st, nullptr);
+    HIPCHK(hipGetLastError());
+    c->pending += 1;
+    const int s = finish_frame(c);
+    if (s < 0) return s;
+    if (k == 0) status = s;
+    else if (s != status) return set_err(KFX_ERR_STATE, "slab members disagree on the tracking status");
+  }
+  return status;
 }
 
 }  // extern "C"

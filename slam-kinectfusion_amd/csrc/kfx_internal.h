@@ -67,18 +67,28 @@ struct IcpSync {
 };
 
 // SoA TSDF volume.  Each z slice is tiled in 8x8 (x,y) tiles; voxel (x,y,z)
-// lives at z*slice + ((y>>3)*tiles_x + (x>>3))*64 + (y&7)*8 + (x&7).
+// lives at (z-zb)*slice + ((y>>3)*tiles_x + (x>>3))*64 + (y&7)*8 + (x&7).
+//
+// Z-slab sharding: a context stores only the global slices
+// [zb, zb+zn) — its owned slices [own0, own1) plus a halo of kSlabHalo slices
+// on each side, which it integrates redundantly (bit-identical to the owner's
+// copy) so that raycast never needs a halo exchange.  A single-GPU volume is
+// the slab zb = own0 = 0, zn = own1 = Z.  X, Y, Z are always the global dims.
+constexpr int kSlabHalo = 4;
 struct VolView {
   int16_t *tsdf;
   int16_t *weight;
   uint32_t *rgb;  // u8 c0,c1,c2,pad
   int X, Y, Z;
+  int zb, zn;      // stored global slices [zb, zb+zn)
+  int own0, own1;  // owned global slices (raycast events, point extraction)
   int tiles_x, tiles_y;
   float vs[3];     // voxel size per axis
   float range[3];  // volume_range
   float trunc;
   float inv_trunc;  // RN(1/trunc), for the exact FMA division (kfx_kernels.hip div_rn)
   size_t slice;    // voxels per z slice (= X*Y)
+  size_t local_voxels() const { return slice * (size_t)zn; }
 };
 
 struct FrameView {
@@ -114,10 +124,22 @@ void launch_integrate(hipStream_t s, VolView v, LevelGeom g0, const float *dmap,
                       const uint8_t *bgr, const float *inv_lambda, DevState *st, DevPose *log,
                       DevPose vpose, const float *xpose,
                       unsigned long long *counters /* non-null: count-only, 32 words */);
-// raycast of level 0 + resizePointsNormals of levels >= 1 in one launch
+// raycast of level 0 + resizePointsNormals of levels >= 1 in one launch; with
+// keys != null the slab variant (owned events only, key per pixel, no resize)
 void launch_raycast(hipStream_t s, VolView v, int levels, const LevelGeom *g, FrameView cur,
                     FrameView prev, const DevState *st, const DevPose *log, DevPose vpose,
-                    const float *xpose);
+                    const float *xpose, uint32_t *keys);
+// resizePointsNormals of levels >= 1 from the level-0 model maps
+void launch_resize(hipStream_t s, int levels, const LevelGeom *g, FrameView cur, FrameView prev,
+                   const DevState *st, const float *xpose);
+// cross-slab combine: clear maps where the local key lost the MIN
+void launch_slab_mask(hipStream_t s, const uint32_t *key_local, const uint32_t *key_min,
+                      float *vmap, float *nmap, int n);
+constexpr int kMaxGroup = 16;
+// element-wise MIN/MAX of n_in u32 buffers (any device-accessible pointers),
+// result stored to each of the n_out buffers
+void launch_group_reduce(hipStream_t s, uint32_t *const *in, int n_in, uint32_t *const *out,
+                         int n_out, size_t count, bool is_max);
 void launch_inv_lambda(hipStream_t s, LevelGeom g0, float *inv_lambda);
 void launch_export_records(hipStream_t s, VolView v, int z0, int nz, uint64_t *dst);
 void launch_import_records(hipStream_t s, VolView v, int z0, int nz, const uint64_t *src);

@@ -146,9 +146,10 @@ __device__ __forceinline__ void frame_begin(DevState *st) {
   for (int i = 0; i < kDmaxShards; ++i) st->dmax_bits[i] = 0u;
 }
 
+// z is the global slice; the view stores slices [zb, zb+zn)
 __device__ __forceinline__ size_t vox_index(const VolView &v, int x, int y, int z) {
-  return (size_t)z * v.slice + ((size_t)(y >> 3) * v.tiles_x + (x >> 3)) * 64 + ((y & 7) << 3) +
-         (x & 7);
+  return (size_t)(z - v.zb) * v.slice + ((size_t)(y >> 3) * v.tiles_x + (x >> 3)) * 64 +
+         ((y & 7) << 3) + (x & 7);
 }
 
 // Level-indexed block decomposition for kernels that process all pyramid
@@ -856,9 +857,9 @@ __global__ __launch_bounds__(256) void k_integrate(VolView v, LevelGeom g,
   const size_t base = (size_t)tile * 64 + lane;
   if (s_kind == 2) {  // reset(): whole volume zeroed (A5 D)
     if (kCount) return;
-    const int z0 = (int)((long long)v.Z * chunk / nchunk);
-    const int z1 = (int)((long long)v.Z * (chunk + 1) / nchunk);
-    for (int z = z0; z < z1; ++z) {
+    const int z0 = (int)((long long)v.zn * chunk / nchunk);
+    const int z1 = (int)((long long)v.zn * (chunk + 1) / nchunk);
+    for (int z = z0; z < z1; ++z) {  // local slices
       const size_t i = base + (size_t)z * v.slice;
       v.tsdf[i] = 0;
       v.weight[i] = 0;
@@ -876,7 +877,9 @@ __global__ __launch_bounds__(256) void k_integrate(VolView v, LevelGeom g,
 #pragma unroll
   for (int i = 0; i < kDmaxShards; ++i) dm = max(dm, st->dmax_bits[i]);
   const float dmax = __uint_as_float(dm);
-  double lo = 1.0, hi = (double)(v.Z - 1);
+  // global z = 1..Z-1 (tsdf_volume.cu:53), restricted to the stored slab
+  double lo = (double)max(1, v.zb), hi = (double)min(v.Z - 1, v.zb + v.zn - 1);
+  const double lo0 = lo, hi0 = hi;
   {
     const double ax = vc.x, ay = vc.y, az = vc.z, sx = zs.x, sy = zs.y, sz = zs.z;
     const double M = 2.0;  // pixels
@@ -891,8 +894,8 @@ __global__ __launch_bounds__(256) void k_integrate(VolView v, LevelGeom g,
     clip_lin(zfar - az, -sz, lo, hi);
   }
   if (!(hi >= lo)) return;
-  const int zlo = max(1, (int)floor(lo) - 2);
-  const int zhi = min(v.Z - 1, (int)ceil(hi) + 2);
+  const int zlo = max((int)lo0, (int)floor(lo) - 2);
+  const int zhi = min((int)hi0, (int)ceil(hi) + 2);
   if (zhi < zlo) return;
   const int len = zhi - zlo + 1;
   const int za = zlo + (int)((long long)len * chunk / nchunk);
@@ -909,7 +912,7 @@ __global__ __launch_bounds__(256) void k_integrate(VolView v, LevelGeom g,
   // volume has < 2^30 voxels, so byte offsets of the u32 colour fit too)
   using Idx = typename std::conditional<kIdx32, unsigned, size_t>::type;
   const Idx slice = (Idx)v.slice;
-  Idx iz = (Idx)base + (Idx)za * slice;
+  Idx iz = (Idx)base + (Idx)(za - v.zb) * slice;
   // Batches of kB voxels: projections, then the kB depth gathers, then the
   // voxel loads of the batch are issued back to back (memory-level
   // parallelism); each voxel's arithmetic is exactly the reference's.
@@ -1017,12 +1020,16 @@ __device__ __forceinline__ float voxel2tsdf(const VolView &v, const RayConsts &r
   const int y = f2i_rn(p.y * rc.vs_inv.y);
   const int z = f2i_rn(p.z * rc.vs_inv.z);
   if (x >= v.X - 1 || y >= v.Y - 1 || z >= v.Z - 1 || x < 1 || y < 1 || z < 1) return NAN;
+  if ((unsigned)(z - v.zb) >= (unsigned)v.zn) return NAN;  // not stored on this slab
   return (float)v.tsdf[vox_index(v, x, y, z)] * kDivShortMax;
 }
 
 __device__ __forceinline__ float interp(const VolView &v, f3 cf) {
   const int gx = f2i_rd(cf.x), gy = f2i_rd(cf.y), gz = f2i_rd(cf.z);
   if (gx < 0 || gx >= v.X - 1 || gy < 0 || gy >= v.Y - 1 || gz < 0 || gz >= v.Z - 1) return NAN;
+  // slabs: an owned event's normal reads within the stored halo (DESIGN.md
+  // §7); the check only keeps any other read in bounds
+  if ((unsigned)(gz - v.zb) >= (unsigned)(v.zn - 1)) return NAN;
   const float a = cf.x - (float)gx, b = cf.y - (float)gy, c = cf.z - (float)gz;
   const float t000 = (float)v.tsdf[vox_index(v, gx, gy, gz)] * kDivShortMax;
   const float t001 = (float)v.tsdf[vox_index(v, gx, gy, gz + 1)] * kDivShortMax;
@@ -1071,7 +1078,7 @@ __device__ __forceinline__ int xcd_remap(int b, int nb) {
 template <bool kIdx32>
 __device__ __forceinline__ size_t ray_index(const VolView &v, int x, int y, int z) {
   if (kIdx32)
-    return (size_t)((unsigned)z * (unsigned)v.slice +
+    return (size_t)((unsigned)(z - v.zb) * (unsigned)v.slice +
                     (((unsigned)(y >> 3) * (unsigned)v.tiles_x + (unsigned)(x >> 3)) << 6) +
                     (unsigned)(((y & 7) << 3) | (x & 7)));
   return vox_index(v, x, y, z);
@@ -1082,12 +1089,24 @@ struct RayArgs {
   int levels;
 };
 
-template <bool kIdx32>
+__device__ void resize_tile(const RayArgs &ra, int kind, int tx0, int ty0, int lx, int ly, f3 vout,
+                            f3 nout, const FrameView &cur, const FrameView &prev);
+
+// kSlab (Z-slab sharding): the context stores slices
+// [zb, zb+zn) and owns [own0, own1).  Every sample position is still the
+// reference's accumulated one, but only samples whose nearest voxel lies in the
+// owned slices may end the ray here; the first such event's sample index is
+// written to keys[] (UINT_MAX: none) with its maps, and the ranks' results are
+// combined by an all-reduce MIN over keys (the earliest event along the ray is
+// the reference's result; each sample has exactly one owner).  The event at
+// sample i reads samples i-1 and i and the trilinear normal at most 4 slices
+// from sample i, all inside the stored halo.  Resize runs after the combine.
+template <bool kIdx32, bool kSlab>
 __global__ __launch_bounds__(256) void k_raycast(VolView v, RayArgs ra, RayConsts rc,
                                                     FrameView cur, FrameView prev,
                                                     const DevState *__restrict__ st,
                                                     const DevPose *__restrict__ log, DevPose vpose,
-                                                    const float *xpose) {
+                                                    const float *xpose, uint32_t *keys) {
   // cam2vol = volume_pose^-1 * pose, Rinv = R^T (tsdf_volume.cpp:59-61; D: transpose)
   __shared__ DevPose s_c2v;
   __shared__ float s_rinv[9];
@@ -1121,6 +1140,7 @@ __global__ __launch_bounds__(256) void k_raycast(VolView v, RayArgs ra, RayConst
   const size_t o = (size_t)y * g.w + x;
   const int kind = s_kind;
   f3 vout = {0.f, 0.f, 0.f}, nout = {0.f, 0.f, 0.f};
+  uint32_t key = kind == 0 ? 0u : UINT_MAX;  // kSlab: sample index of the decisive event
   if (kind == 0 && inimg) {  // frame 1: the measured maps become the model maps
     vout = ld3(cur.v[0], o);
     nout = ld3(cur.n[0], o);
@@ -1154,9 +1174,11 @@ __global__ __launch_bounds__(256) void k_raycast(VolView v, RayArgs ra, RayConst
     // and, if it is NaN, the scan resumes at the next event).
     constexpr int kR = 16;
     int sprev = isnan(tprev) ? 0 : (tprev > 0.f ? 1 : (tprev < 0.f ? -1 : 0));
+    uint32_t kbase = 1u;  // loop sample index of the batch's first sample
     while (__any(live)) {
       int16_t raw[kR];
       bool val[kR];
+      unsigned ownm = 0u;
       int je = kR;
       float rl = ray_len;
 #pragma unroll
@@ -1172,6 +1194,10 @@ __global__ __launch_bounds__(256) void k_raycast(VolView v, RayArgs ra, RayConst
         // 1 <= i <= dim-2 on each axis (tsdf_volume.cu:184-185), as unsigned compares
         val[j] = a & ((unsigned)(ix - 1) < (unsigned)(v.X - 2)) &
                  ((unsigned)(iy - 1) < (unsigned)(v.Y - 2)) & ((unsigned)(iz - 1) < (unsigned)(v.Z - 2));
+        if (kSlab) {
+          val[j] = val[j] & ((unsigned)(iz - v.zb) < (unsigned)v.zn);
+          ownm |= ((unsigned)(iz - v.own0) < (unsigned)(v.own1 - v.own0)) ? (1u << j) : 0u;
+        }
         raw[j] = v.tsdf[val[j] ? ray_index<kIdx32>(v, ix, iy, iz) : 0];
         rl = a ? rl + rc.step : rl;
       }
@@ -1188,6 +1214,7 @@ __global__ __launch_bounds__(256) void k_raycast(VolView v, RayArgs ra, RayConst
       }
       sprev = sp;
       tprev = val[kR - 1] ? (float)raw[kR - 1] * kDivShortMax : NAN;
+      if (kSlab) ev &= ownm;  // only owned samples may end the ray on this slab
       unsigned pend = live ? ev : 0u;
       while (__any(pend != 0u)) {
         if (pend != 0u) {
@@ -1195,6 +1222,7 @@ __global__ __launch_bounds__(256) void k_raycast(VolView v, RayArgs ra, RayConst
           if (!((hitm >> j0) & 1u)) {  // tsdf_cur < 0 && tsdf_next > 0: stop, no surface
             live = false;
             pend = 0u;
+            key = kbase + (uint32_t)j0;
           } else {
             // sample j0's ray_len: replay the batch's adds (event samples
             // always lie before je, where every step added rc.step)
@@ -1220,6 +1248,7 @@ __global__ __launch_bounds__(256) void k_raycast(VolView v, RayArgs ra, RayConst
               vout = rmul(ri, sub(vertex, org));
               live = false;
               pend = 0u;
+              key = kbase + (uint32_t)j0;
             } else {
               pend &= ~(1u << j0);
             }
@@ -1227,16 +1256,33 @@ __global__ __launch_bounds__(256) void k_raycast(VolView v, RayArgs ra, RayConst
         }
       }
       if (je < kR) live = false;  // left [.., tfar) inside this batch
+      if (kSlab && live) {
+        // z is monotonic along the ray: once the samples are more than 2
+        // slices past the owned range, no owned sample follows
+        const float zf = nextp.z * rc.vs_inv.z;
+        if ((dir.z >= 0.f && zf > (float)(v.own1 + 2)) || (dir.z <= 0.f && zf < (float)(v.own0 - 3)))
+          live = false;
+      }
       ray_len = rl;
+      kbase += kR;
     }
   }
   if (inimg) {
     st3(prev.v[0], o, vout);
     st3(prev.n[0], o, nout);
+    if (kSlab) keys[o] = key;
   }
-  // kernel_resizePointsNormals (image_process.cu:95-125) for levels >= 1: the
-  // block's 16x16 tile maps onto 8x8 / 4x4 / 2x2 tiles of levels 1 / 2 / 3,
-  // computed from the level below through LDS with the same float ops.
+  if (kSlab) return;  // resize runs after the cross-slab combine (k_resize)
+  resize_tile(ra, kind, tx0, ty0, lx, ly, vout, nout, cur, prev);
+}
+
+// kernel_resizePointsNormals (image_process.cu:95-125) for levels >= 1: the
+// block's 16x16 level-0 tile (this thread's values vout/nout at (lx, ly)) maps
+// onto 8x8 / 4x4 / 2x2 tiles of levels 1 / 2 / 3, computed from the level
+// below through LDS with the same float ops.  kind 0 (frame 1) copies the
+// measured maps, kind 2 (reset) writes zeros.
+__device__ void resize_tile(const RayArgs &ra, int kind, int tx0, int ty0, int lx, int ly, f3 vout,
+                            f3 nout, const FrameView &cur, const FrameView &prev) {
   if (ra.levels < 2) return;
   __shared__ f3 sv[2][256], sn[2][256];
   sv[0][ly * 16 + lx] = vout;
@@ -1279,6 +1325,55 @@ __global__ __launch_bounds__(256) void k_raycast(VolView v, RayArgs ra, RayConst
       }
     }
     __syncthreads();
+  }
+}
+
+// Resize of the combined level-0 model maps (slab mode): same tiles and ops as
+// the resize fused into k_raycast.
+__global__ __launch_bounds__(256) void k_resize(RayArgs ra, FrameView cur, FrameView prev,
+                                                const DevState *__restrict__ st,
+                                                const float *xpose) {
+  const int kind = xpose ? 1 : frame_kind(st);
+  const LevelGeom g = ra.g[0];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int nbx = (g.w + 15) / 16;
+  const int t = blockIdx.x;
+  const int tx0 = (t % nbx) * 16, ty0 = (t / nbx) * 16;
+  const int lx = (wv & 1) * 8 + (lane & 7), ly = (wv >> 1) * 8 + (lane >> 3);
+  const int x = tx0 + lx, y = ty0 + ly;
+  f3 vout = {0.f, 0.f, 0.f}, nout = {0.f, 0.f, 0.f};
+  if (x < g.w && y < g.h) {
+    const size_t o = (size_t)y * g.w + x;
+    vout = ld3(prev.v[0], o);
+    nout = ld3(prev.n[0], o);
+  }
+  resize_tile(ra, kind, tx0, ty0, lx, ly, vout, nout, cur, prev);
+}
+
+// Cross-slab combine, step 2 (after the all-reduce MIN of the keys): a rank
+// that does not hold the earliest event of a pixel clears its maps there, so
+// the all-reduce MAX of the map bits (step 3) leaves exactly the winner's bits
+// (0 is the smallest u32; -0.f and NaN payloads survive bit for bit).
+__global__ void k_slab_mask(const uint32_t *__restrict__ key_local,
+                            const uint32_t *__restrict__ key_min, float *vmap, float *nmap, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || key_local[i] == key_min[i]) return;
+  st3(vmap, i, {0.f, 0.f, 0.f});
+  st3(nmap, i, {0.f, 0.f, 0.f});
+}
+
+// In-process group combine (several slab contexts in one process): element-wise
+// MIN / MAX over the members' u32 buffers, result written back to every member.
+struct GroupBufs {
+  uint32_t *p[kMaxGroup];
+  int n;
+};
+__global__ void k_group_reduce(GroupBufs in, GroupBufs out, size_t count, int is_max) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < count;
+       i += (size_t)gridDim.x * blockDim.x) {
+    uint32_t r = in.p[0][i];
+    for (int k = 1; k < in.n; ++k) r = is_max ? max(r, in.p[k][i]) : min(r, in.p[k][i]);
+    for (int k = 0; k < out.n; ++k) out.p[k][i] = r;
   }
 }
 
@@ -1439,7 +1534,7 @@ void launch_integrate(hipStream_t s, VolView v, LevelGeom g0, const float *dmap,
   // z-chunks so that >= 16 waves per SIMD exist (16384 waves on 1024 SIMDs)
   const int nchunk = std::max(1, std::min(8, (16384 + tiles - 1) / tiles));
   dim3 grd((tiles + 3) / 4, nchunk);
-  const bool idx32 = v.slice * (size_t)v.Z < (1ull << 30);
+  const bool idx32 = v.local_voxels() < (1ull << 30);
   if (counters)
     hipLaunchKernelGGL((k_integrate<true, false>), grd, dim3(256), 0, s, v, g0, dmap, bgr,
                        inv_lambda, st, log, vpose, xpose, counters);
@@ -1453,7 +1548,7 @@ void launch_integrate(hipStream_t s, VolView v, LevelGeom g0, const float *dmap,
 
 void launch_raycast(hipStream_t s, VolView v, int levels, const LevelGeom *g, FrameView cur,
                     FrameView prev, const DevState *st, const DevPose *log, DevPose vpose,
-                    const float *xpose) {
+                    const float *xpose, uint32_t *keys) {
   RayConsts rc;
   rc.vs = {v.vs[0], v.vs[1], v.vs[2]};
   rc.vs_inv = {1.f / v.vs[0], 1.f / v.vs[1], 1.f / v.vs[2]};
@@ -1463,12 +1558,49 @@ void launch_raycast(hipStream_t s, VolView v, int levels, const LevelGeom *g, Fr
   ra.levels = levels;
   for (int l = 0; l < levels; ++l) ra.g[l] = g[l];
   dim3 grd(((g[0].w + 15) / 16) * ((g[0].h + 15) / 16));
-  if (v.slice * (size_t)v.Z < (1ull << 32))
-    hipLaunchKernelGGL(k_raycast<true>, grd, dim3(256), 0, s, v, ra, rc, cur, prev, st, log, vpose,
-                       xpose);
-  else
-    hipLaunchKernelGGL(k_raycast<false>, grd, dim3(256), 0, s, v, ra, rc, cur, prev, st, log, vpose,
-                       xpose);
+  const bool idx32 = v.local_voxels() < (1ull << 32);
+  if (keys) {
+    if (idx32)
+      hipLaunchKernelGGL((k_raycast<true, true>), grd, dim3(256), 0, s, v, ra, rc, cur, prev, st, log,
+                         vpose, xpose, keys);
+    else
+      hipLaunchKernelGGL((k_raycast<false, true>), grd, dim3(256), 0, s, v, ra, rc, cur, prev, st,
+                         log, vpose, xpose, keys);
+  } else if (idx32) {
+    hipLaunchKernelGGL((k_raycast<true, false>), grd, dim3(256), 0, s, v, ra, rc, cur, prev, st, log,
+                       vpose, xpose, keys);
+  } else {
+    hipLaunchKernelGGL((k_raycast<false, false>), grd, dim3(256), 0, s, v, ra, rc, cur, prev, st,
+                       log, vpose, xpose, keys);
+  }
+}
+
+void launch_resize(hipStream_t s, int levels, const LevelGeom *g, FrameView cur, FrameView prev,
+                   const DevState *st, const float *xpose) {
+  RayArgs ra{};
+  ra.levels = levels;
+  for (int l = 0; l < levels; ++l) ra.g[l] = g[l];
+  dim3 grd(((g[0].w + 15) / 16) * ((g[0].h + 15) / 16));
+  hipLaunchKernelGGL(k_resize, grd, dim3(256), 0, s, ra, cur, prev, st, xpose);
+}
+
+void launch_slab_mask(hipStream_t s, const uint32_t *key_local, const uint32_t *key_min,
+                      float *vmap, float *nmap, int n) {
+  hipLaunchKernelGGL(k_slab_mask, dim3((n + 255) / 256), dim3(256), 0, s, key_local, key_min, vmap,
+                     nmap, n);
+}
+
+void launch_group_reduce(hipStream_t s, uint32_t *const *in, int n_in, uint32_t *const *out,
+                         int n_out, size_t count, bool is_max) {
+  GroupBufs a{}, b{};
+  a.n = n_in;
+  b.n = n_out;
+  for (int k = 0; k < n_in; ++k) a.p[k] = in[k];
+  for (int k = 0; k < n_out; ++k) b.p[k] = out[k];
+  size_t blocks = (count + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(k_group_reduce, dim3((unsigned)blocks), dim3(256), 0, s, a, b, count,
+                     is_max ? 1 : 0);
 }
 
 void launch_inv_lambda(hipStream_t s, LevelGeom g0, float *inv_lambda) {

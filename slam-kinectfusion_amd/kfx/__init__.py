@@ -18,7 +18,7 @@ import numpy as np
 from .abi import (KFX_FRAME_CUR, KFX_FRAME_PREV, KFX_OK, KFX_TRACKING_LOST, Intrinsics, Params, Pose,
                   default_params, fptr, i16ptr, i64ptr, u8ptr, u16ptr)
 
-__all__ = ["KinectFusion", "KfxError", "lib", "build", "LIB_PATH", "Intrinsics", "Params", "Pose",
+__all__ = ["KinectFusion", "KfxError", "comm_unique_id", "pipeline_group", "lib", "build", "LIB_PATH", "Intrinsics", "Params", "Pose",
            "default_params", "KFX_FRAME_CUR", "KFX_FRAME_PREV", "KFX_OK", "KFX_TRACKING_LOST", "EXPORTS"]
 
 _PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -32,7 +32,8 @@ EXPORTS = [
     "kfx_write_poses_txt", "kfx_get_frame_maps", "kfx_set_frame_maps", "kfx_download_tsdf",
     "kfx_upload_tsdf", "kfx_download_volume_soa", "kfx_stage_preprocess", "kfx_stage_icp_accumulate",
     "kfx_stage_icp", "kfx_stage_integrate", "kfx_stage_raycast", "kfx_set_profiling", "kfx_get_stage_ms",
-    "kfx_integrate_counts",
+    "kfx_integrate_counts", "kfx_create_slab", "kfx_slab_info", "kfx_comm_get_unique_id", "kfx_comm_init",
+    "kfx_pipeline_group",
 ]
 
 
@@ -90,6 +91,11 @@ def lib():
         "kfx_set_profiling": ([vp, i], i),
         "kfx_get_stage_ms": ([vp, P(f)], i),
         "kfx_integrate_counts": ([vp, P(C.c_int64), P(C.c_int64)], i),
+        "kfx_create_slab": ([P(Intrinsics), P(Params), i, i, i, P(vp)], i),
+        "kfx_slab_info": ([vp, P(i), P(i), P(i), P(i)], i),
+        "kfx_comm_get_unique_id": ([P(C.c_uint8)], i),
+        "kfx_comm_init": ([vp, P(C.c_uint8)], i),
+        "kfx_pipeline_group": ([P(vp), i, P(C.c_uint8), P(f)], i),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -105,16 +111,43 @@ def _check(rc: int, what: str, ok=(KFX_OK,)) -> int:
     return rc
 
 
+def comm_unique_id() -> bytes:
+    """RCCL unique id (128 bytes) for kfx_comm_init; made on rank 0 and
+    broadcast to the other ranks by the launcher."""
+    buf = (C.c_uint8 * 128)()
+    _check(lib().kfx_comm_get_unique_id(buf), "kfx_comm_get_unique_id")
+    return bytes(buf)
+
+
+def pipeline_group(members, color: np.ndarray, depth: np.ndarray) -> int:
+    """One pipeline() frame over all Z-slabs held in this process
+    (members[k] = slab k of len(members))."""
+    color = np.ascontiguousarray(color, np.uint8)
+    d = np.ascontiguousarray(depth, np.float32)
+    hs = (C.c_void_p * len(members))(*[m._h for m in members])
+    rc = lib().kfx_pipeline_group(hs, len(members), u8ptr(color), fptr(d))
+    return _check(rc, "kfx_pipeline_group", ok=(KFX_OK, KFX_TRACKING_LOST))
+
+
 class KinectFusion:
     """kf::kinectfusion over the C-ABI.  Images: depth (H,W) float32/uint16 mm,
     colour (H,W,3) uint8 BGR."""
 
-    def __init__(self, intr, params: Params | None = None, device: int = 0):
+    def __init__(self, intr, params: Params | None = None, device: int = 0, slab=None):
+        """slab=(rank, world): this instance owns Z-slab `rank` of `world`
+        (kfx_create_slab); combine through comm_init (one process per GPU) or
+        pipeline_group (all slabs in this process)."""
         self.intr = Intrinsics.from_any(intr)
         self.params = params if params is not None else default_params()
         h = C.c_void_p()
-        _check(lib().kfx_create(C.byref(self.intr), C.byref(self.params), device, C.byref(h)), "kfx_create")
+        if slab is None:
+            _check(lib().kfx_create(C.byref(self.intr), C.byref(self.params), device, C.byref(h)), "kfx_create")
+        else:
+            rank, world = slab
+            _check(lib().kfx_create_slab(C.byref(self.intr), C.byref(self.params), device, int(rank), int(world),
+                                         C.byref(h)), "kfx_create_slab")
         self._h = h
+        self.slab = slab
         X, Y, Z = (int(d) for d in self.params.volu_dims)
         self.dims = (X, Y, Z)
         self.nvox = X * Y * Z
@@ -211,6 +244,17 @@ class KinectFusion:
         a, b = C.c_int64(), C.c_int64()
         _check(lib().kfx_integrate_counts(self._h, C.byref(a), C.byref(b)), "kfx_integrate_counts")
         return a.value, b.value
+
+    # ---- Z-slab sharding -------------------------------------------------
+    def slab_info(self):
+        """(zb, zn, own0, own1): stored slices [zb, zb+zn), owned [own0, own1)."""
+        a = [C.c_int() for _ in range(4)]
+        _check(lib().kfx_slab_info(self._h, *[C.byref(x) for x in a]), "kfx_slab_info")
+        return tuple(x.value for x in a)
+
+    def comm_init(self, uid: bytes):
+        buf = (C.c_uint8 * 128).from_buffer_copy(uid)
+        _check(lib().kfx_comm_init(self._h, buf), "kfx_comm_init")
 
     # ---- frames / volume -------------------------------------------------
     def frame_maps(self, which: int, level: int):
