@@ -6,19 +6,25 @@ Workload (BASELINE config C2): synthetic 640x480 depth + BGR frames of the
 analytic scene (kfx.synth), 512^3 TSDF @ 4 mm, 3-level ICP {10,5,4}.  A "step"
 is one kf::kinectfusion::pipeline() frame: preprocess, 19 ICP iterations,
 integrate, raycast, resize.  Frames are staged in HBM before the timed region
-(kfx_stage_frames); every timed frame then copies its input D2D and runs the
-captured per-frame hipGraph.
+(kfx_stage_frames); every timed frame then runs the captured per-frame hipGraph
+on its staged input.
 
-Multi-GPU (`torchrun --nproc-per-node N`): one process per GPU, each running an
-independent replica on its own synthetic camera stream (DESIGN.md §multi-GPU:
-Z-slab sharding of one stream is the next step); value = frames of all ranks /
-max wall time over ranks.
+Multi-GPU (`torchrun --nproc-per-node N`), one process per GPU:
+  --mode replicas (default for N > 1): every rank runs an independent
+      KinectFusion stream on its own camera trajectory (weak scaling, no
+      collective on the data path); value = frames of all ranks / max wall time.
+  --mode slab: ONE stream whose volume is Z-slab sharded over the N ranks
+      (kfx_create_slab + RCCL combine; strong scaling); value =
+      frames of the stream / max wall time.
+  With --mode replicas and N > 1 the JSON line also carries "zslab": the same
+  C2 stream Z-slab sharded over the N ranks, timed after the main measurement.
 
 The JSON line also carries:
   stage_ms      per-stage device ms (HIP events on the pipeline stream)
   roofline      integrate kernel: algorithmic bytes (8*N_upd + 8*N_col + 7*W*H,
                 SURVEY.md §8d; N counted on the device) / its event-timed
-                duration vs 8 TB/s HBM
+                duration vs 8 TB/s HBM; traffic = HBM bytes per launch from the
+                committed rocprofv3 PMC summary (profiles/integrate_pmc.json)
   cpu_baseline  the serial C++ oracle running the same pipeline on host cores
 """
 import argparse
@@ -26,6 +32,7 @@ import json
 import os
 import statistics
 import sys
+import threading
 import time
 
 import numpy as np
@@ -50,6 +57,9 @@ def parse():
     ap.add_argument("--profile-frames", type=int, default=20)
     ap.add_argument("--cpu-frames", type=int, default=3, help="oracle frames timed for cpu_baseline (0 = skip)")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--mode", choices=["auto", "replicas", "slab"], default="auto")
+    ap.add_argument("--zslab", type=int, default=1, help="with replicas at N>1: also time the Z-slab stream")
+    ap.add_argument("--zslab-timeout", type=float, default=240.0)
     return ap.parse_args()
 
 
@@ -93,19 +103,92 @@ def _cpu_model():
     return "unknown"
 
 
+class Dist:
+    """torch.distributed wrapper (None-safe for the single-process case)."""
+
+    def __init__(self, world, local):
+        self.world = world
+        self.dist = None
+        if world > 1:
+            import torch
+            import torch.distributed as dist
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+            if backend == "nccl":
+                torch.cuda.set_device(local)
+            dist.init_process_group(backend=backend)
+            self.dist = dist
+
+    def barrier(self):
+        if self.dist is not None:
+            self.dist.barrier()
+
+    def max(self, x: float) -> float:
+        if self.dist is None:
+            return x
+        import torch
+        dev = "cuda" if self.dist.get_backend() == "nccl" else "cpu"
+        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def bcast_bytes(self, b: bytes | None, src: int = 0) -> bytes:
+        if self.dist is None:
+            return b
+        obj = [b]
+        self.dist.broadcast_object_list(obj, src=src)
+        return obj[0]
+
+    def close(self):
+        if self.dist is not None:
+            self.dist.destroy_process_group()
+
+
+def timed_frames(kf, order, lo, hi, D):
+    """W/K contract: barrier + device sync on both sides, max over ranks."""
+    kf.synchronize()
+    D.barrier()
+    t0 = time.perf_counter()
+    for i in range(lo, hi):
+        kf.pipeline_staged(order[i])
+    kf.synchronize()
+    elapsed = time.perf_counter() - t0
+    elapsed = D.max(elapsed)
+    D.barrier()
+    return elapsed
+
+
+def zslab_stream(a, intr, params, D, rank, world, local):
+    """One C2 stream Z-slab sharded over the ranks (RCCL combine); frames/s."""
+    import kfx
+    from kfx import synth
+    from kfx.abi import Intrinsics
+    bgr, dep, _ = synth.sequence(a.unique, intr, L=a.range, noise=True, traj_seed=7, dropout=0.005)
+    order = synth.ping_pong(a.unique, a.warmup + a.steps)
+    kf = kfx.KinectFusion(Intrinsics.from_any(intr), params, device=local, slab=(rank, world))
+    uid = D.bcast_bytes(kfx.comm_unique_id() if rank == 0 else None)
+    kf.comm_init(uid)
+    kf.set_graph_mode(not a.no_graph)
+    kf.stage_frames(bgr, dep.astype(np.float32))
+    for i in range(a.warmup):
+        kf.pipeline_staged(order[i])
+    elapsed = timed_frames(kf, order, a.warmup, a.warmup + a.steps, D)
+    poses = kf.pose_record.shape[0]
+    zb, zn, o0, o1 = kf.slab_info()
+    kf.close()
+    return {"value": round(a.steps / elapsed, 3), "unit": "frames/s", "scaling": "strong",
+            "ms_per_step": round(1000.0 * elapsed / a.steps, 4), "n_gpus": world,
+            "slab_slices": o1 - o0, "stored_slices": zn, "poses": int(poses),
+            "note": "one C2 stream, volume Z-slab sharded over the ranks, raycast combined by "
+                    "RCCL all-reduce MIN(key)+MAX(bits) per frame, ICP replicated"}
+
+
 def main():
     a = parse()
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch
-        import torch.distributed as dist
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
-        if backend == "nccl":
-            torch.cuda.set_device(local)
-        dist.init_process_group(backend=backend)
+    D = Dist(world, local)
+    mode = a.mode if a.mode != "auto" else ("replicas" if world > 1 else "single")
 
     import kfx
     from kfx import synth
@@ -113,43 +196,31 @@ def main():
 
     intr = intrinsics(a.width, a.height)
     params = default_params(dims=a.dims, range_m=a.range)
-    bgr, dep, gt = synth.sequence(a.unique, intr, L=a.range, noise=True, traj_seed=7 + rank, dropout=0.005)
+    W, H = intr.width, intr.height
+    slab_main = mode == "slab"
+    seed = 7 if (slab_main or world == 1) else 7 + rank
+    bgr, dep, gt = synth.sequence(a.unique, intr, L=a.range, noise=True, traj_seed=seed, dropout=0.005)
     order = synth.ping_pong(a.unique, a.warmup + a.steps + a.profile_frames)
 
-    kf = kfx.KinectFusion(Intrinsics.from_any(intr), params, device=local)
+    if slab_main:
+        kf = kfx.KinectFusion(Intrinsics.from_any(intr), params, device=local, slab=(rank, world))
+        kf.comm_init(D.bcast_bytes(kfx.comm_unique_id() if rank == 0 else None))
+    else:
+        kf = kfx.KinectFusion(Intrinsics.from_any(intr), params, device=local)
     kf.set_graph_mode(not a.no_graph)
     kf.stage_frames(bgr, dep.astype(np.float32))
 
-    def sync_all():
-        kf.synchronize()
-        if dist is not None:
-            dist.barrier()
-
     for i in range(a.warmup):
         kf.pipeline_staged(order[i])
-    sync_all()
-    n_before = kf.pose_record.shape[0]
-    t0 = time.perf_counter()
-    for i in range(a.warmup, a.warmup + a.steps):
-        kf.pipeline_staged(order[i])
     kf.synchronize()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
-    if dist is not None:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64,
-                         device="cuda" if dist.get_backend() == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        dist.barrier()
-    n_after = kf.pose_record.shape[0]
-    tracked = n_after - n_before  # frames that appended a pose (failures reset the record)
+    n_before = kf.pose_record.shape[0]
+    elapsed = timed_frames(kf, order, a.warmup, a.warmup + a.steps, D)
+    tracked = kf.pose_record.shape[0] - n_before  # frames that appended a pose
 
     # per-stage device ms + integrate roofline on further frames (profiled, eager)
     kf.set_profiling(True)
     stages = {k: [] for k in ("preprocess", "icp", "integrate", "raycast", "total")}
     int_bytes, int_ms = [], []
-    W, H = intr.width, intr.height
     for i in range(a.warmup + a.steps, a.warmup + a.steps + a.profile_frames):
         kf.pipeline_staged(order[i])
         ms = kf.stage_ms()
@@ -159,13 +230,15 @@ def main():
         int_bytes.append(8 * nu + 8 * nc + 7 * W * H)
         int_ms.append(ms["integrate"])
     kf.set_profiling(False)
-    stage_med = {k: round(statistics.median(v), 4) for k, v in stages.items()}
-    avg_bytes = float(np.mean(int_bytes))
-    avg_ms = float(np.mean(int_ms))
-    achieved = avg_bytes / (avg_ms * 1e-3) / 1e9
+    kf.synchronize()
+    kf.close()
+    stage_med = {k: round(statistics.median(v), 4) for k, v in stages.items()} if a.profile_frames else {}
+    avg_bytes = float(np.mean(int_bytes)) if int_bytes else 0.0
+    avg_ms = float(np.mean(int_ms)) if int_ms else float("nan")
+    achieved = avg_bytes / (avg_ms * 1e-3) / 1e9 if int_ms else 0.0
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", "integrate_pmc.json")
-    if os.path.exists(pmc_path):
+    if os.path.exists(pmc_path) and not slab_main and (a.dims, W, H) == (512, 640, 480):
         try:
             traffic = json.load(open(pmc_path)).get("hbm_bytes_per_launch")
         except (OSError, ValueError):
@@ -175,48 +248,77 @@ def main():
     if rank == 0 and world == 1 and a.cpu_frames > 0:
         cpu = cpu_baseline(intr, params, bgr, dep, min(a.cpu_frames, a.unique - 1))
 
-    total_frames = a.steps * world
-    value = total_frames / elapsed
-    if rank == 0:
-        out = {
-            "metric": "frames/sec at 640×480, 512³ TSDF; per-stage ms (ICP/integrate/raycast)",
-            "value": round(value, 3),
-            "unit": "frames/s",
-            "n_gpus": world,
-            "steps": a.steps,
-            "warmup": a.warmup,
-            "ms_per_step": round(1000.0 * elapsed / a.steps, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": round((value / world) / (1000.0 / REF_MS_PER_FRAME), 3),
-            "dtype": "f32",
-            "data": "synthetic",
-            "config": {
-                "workload": f"C2: synthetic {W}x{H} depth+BGR, {a.dims}^3 TSDF @ "
-                            f"{1000 * a.range / a.dims:.1f} mm, 3-level ICP {{10,5,4}}, full pipeline per frame",
-                "width": W, "height": H, "volume_dims": a.dims, "volume_range_m": a.range,
-                "frames_unique": a.unique, "graph": not a.no_graph,
-                "parallelism": f"replicas x{world}" if world > 1 else "single",
-                "tracked_frames": int(tracked),
-            },
-            "stage_ms": stage_med,
-            "roofline": {
-                "kernel": "k_integrate",
-                "bound": "hbm",
-                "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
-                "algorithmic_bytes_per_launch": int(avg_bytes),
-                "avg_launch_ms": round(avg_ms, 4),
-            },
-            "cpu_baseline": cpu,
-        }
-        print(json.dumps(out))
-    kf.close()
-    if dist is not None:
-        dist.destroy_process_group()
+    frames = a.steps if slab_main else a.steps * world
+    value = frames / elapsed
+    out = {
+        "metric": "frames/sec at 640×480, 512³ TSDF; per-stage ms (ICP/integrate/raycast)",
+        "value": round(value, 3),
+        "unit": "frames/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(1000.0 * elapsed / a.steps, 4),
+        "higher_is_better": True,
+        "scaling": "strong" if slab_main else "weak",
+        "vs_baseline": round(value / (1000.0 / REF_MS_PER_FRAME), 3),
+        "dtype": "f32",
+        "data": "synthetic",
+        "config": {
+            "workload": f"C2: synthetic {W}x{H} depth+BGR, {a.dims}^3 TSDF @ "
+                        f"{1000 * a.range / a.dims:.1f} mm, 3-level ICP {{10,5,4}}, full pipeline per frame",
+            "width": W, "height": H, "volume_dims": a.dims, "volume_range_m": a.range,
+            "frames_unique": a.unique, "graph": not a.no_graph,
+            "parallelism": (f"zslab x{world}" if slab_main else
+                            (f"replicas x{world} (independent streams)" if world > 1 else "single")),
+            "tracked_frames": int(tracked),
+            "reference_ms_per_frame": REF_MS_PER_FRAME,
+        },
+        "stage_ms": stage_med,
+        "roofline": {
+            "kernel": "k_integrate",
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "algorithmic_bytes_per_launch": int(avg_bytes),
+            "avg_launch_ms": round(avg_ms, 4),
+        },
+        "cpu_baseline": cpu,
+    }
+
+    if mode == "replicas" and a.zslab:
+        # the main measurement is complete: a failure or hang in the Z-slab
+        # side measurement must not lose it
+        lock = threading.Lock()
+        printed = []
+
+        def emit(extra):
+            with lock:
+                if printed:
+                    return
+                printed.append(1)
+                if rank == 0:
+                    out["zslab"] = extra
+                    print(json.dumps(out), flush=True)
+
+        def on_timeout():
+            emit({"error": f"timed out after {a.zslab_timeout:.0f} s"})
+            os._exit(0)
+
+        timer = threading.Timer(a.zslab_timeout, on_timeout)
+        timer.daemon = True
+        timer.start()
+        try:
+            extra = zslab_stream(a, intr, params, D, rank, world, local)
+        except Exception as e:  # noqa: BLE001 — reported in the JSON line
+            extra = {"error": f"{type(e).__name__}: {e}"[:300]}
+        timer.cancel()
+        emit(extra)
+    elif rank == 0:
+        print(json.dumps(out), flush=True)
+    D.close()
 
 
 if __name__ == "__main__":

@@ -503,6 +503,7 @@ struct RayCtx {
   int X, Y, Z;
   int64_t slice;
   V3 vs, vs_inv, gd;
+  int zb, zn;  // slices that may be read: [zb, zb+zn) (the whole volume unless slab)
 };
 // raycasthelper::voxel2tsdf (tsdf_volume.cu:178-191): nearest voxel, valid 1..dim-2
 inline float voxel2tsdf(const RayCtx &c, V3 p) {
@@ -510,12 +511,14 @@ inline float voxel2tsdf(const RayCtx &c, V3 p) {
   const int y = f2i_rn(p.y * c.vs_inv.y);
   const int z = f2i_rn(p.z * c.vs_inv.z);
   if (x >= c.X - 1 || y >= c.Y - 1 || z >= c.Z - 1 || x < 1 || y < 1 || z < 1) return NAN;
+  if (z < c.zb || z >= c.zb + c.zn) return NAN;  // slab: not stored
   return (float)c.tsdf[(int64_t)x + (int64_t)y * c.X + (int64_t)z * c.slice] * kDivShortMax;
 }
 // interpolate (tsdf_volume.cu:137-161), terms accumulated in listed order
 inline float interp(const RayCtx &c, V3 cf) {
   const int gx = f2i_rd(cf.x), gy = f2i_rd(cf.y), gz = f2i_rd(cf.z);
   if (gx < 0 || gx >= c.X - 1 || gy < 0 || gy >= c.Y - 1 || gz < 0 || gz >= c.Z - 1) return NAN;
+  if (gz < c.zb || gz + 1 >= c.zb + c.zn) return NAN;  // slab: not stored
   const float a = cf.x - (float)gx, b = cf.y - (float)gy, cc = cf.z - (float)gz;
   auto T = [&](int dx, int dy, int dz) {
     return (float)c.tsdf[(int64_t)(gx + dx) + (int64_t)(gy + dy) * c.X +
@@ -550,15 +553,21 @@ inline V3 compute_normal(const RayCtx &c, V3 p) {
 }  // namespace
 
 // raycasthelper::operator() (tsdf_volume.cu:210-260) + intersect (:120-136).
-void kfo_raycast(const int16_t *tsdf, const int dims[3], const float vs[3],
-                 const float range[3], const kfx_intrinsics *in, const kfx_pose *pose,
-                 const float Rinv[9], float *vmap, float *nmap, const int32_t *pix,
-                 int64_t npix) {
+// Slab restatement (keys != null): only slices [zb, zb+zn) may be read, only
+// samples whose nearest voxel z is in [own0, own1) may end the ray, and the
+// loop index (from 1) of the sample that ended it is written to keys
+// (UINT32_MAX: none) — the per-slab half of the Z-slab raycast.
+static void raycast_impl(const int16_t *tsdf, const int dims[3], const float vs[3],
+                         const float range[3], const kfx_intrinsics *in, const kfx_pose *pose,
+                         const float Rinv[9], float *vmap, float *nmap, const int32_t *pix,
+                         int64_t npix, int zb, int zn, int own0, int own1, uint32_t *keys) {
   RayCtx c;
   c.tsdf = tsdf;
   c.X = dims[0];
   c.Y = dims[1];
   c.Z = dims[2];
+  c.zb = zb;
+  c.zn = zn;
   c.slice = (int64_t)c.X * c.Y;
   c.vs = {vs[0], vs[1], vs[2]};
   c.vs_inv = {1.f / vs[0], 1.f / vs[1], 1.f / vs[2]};  // raycasthelper ctor (host)
@@ -578,6 +587,7 @@ void kfo_raycast(const int16_t *tsdf, const int dims[3], const float vs[3],
     const int64_t o = (int64_t)y * in->width + x;
     st3(vmap, o, {0.f, 0.f, 0.f});
     st3(nmap, o, {0.f, 0.f, 0.f});
+    if (keys) keys[o] = UINT32_MAX;
     const V3 pp = {(1.f * ((float)x - in->cx)) / in->fx, (1.f * ((float)y - in->cy)) / in->fy,
                    1.f};
     const V3 dir = normalized(rmul(pose->R, pp));
@@ -597,12 +607,21 @@ void kfo_raycast(const int16_t *tsdf, const int dims[3], const float vs[3],
     ray_len += step;
     V3 nextp = add(org, scl(dir, ray_len));
     float tn = voxel2tsdf(c, nextp);
+    uint32_t k = 0;
     for (; ray_len < tfar; ray_len += step) {
       nextp = add(nextp, vstep);
+      ++k;
       const float tcur = tn;
       tn = voxel2tsdf(c, nextp);
       if (std::isnan(tn)) continue;
-      if (tcur < 0.f && tn > 0.f) break;
+      if (keys) {  // slab: an event counts only at an owned sample
+        const int iz = f2i_rn(nextp.z * c.vs_inv.z);
+        if (iz < own0 || iz >= own1) continue;
+      }
+      if (tcur < 0.f && tn > 0.f) {
+        if (keys) keys[o] = k;
+        break;
+      }
       if (tcur > 0.f && tn < 0.f) {
         const float Ts = ray_len - (vs[0] * tcur) / (tcur - tn);  // A3 (R)
         const V3 vertex = add(org, scl(dir, Ts));
@@ -610,11 +629,28 @@ void kfo_raycast(const int16_t *tsdf, const int dims[3], const float vs[3],
         if (!std::isnan(n.x * n.y * n.z)) {
           st3(nmap, o, rmul(Rinv, n));
           st3(vmap, o, rmul(Rinv, sub(vertex, org)));
+          if (keys) keys[o] = k;
           break;
         }
       }
     }
   }
+}
+
+void kfo_raycast(const int16_t *tsdf, const int dims[3], const float vs[3],
+                 const float range[3], const kfx_intrinsics *in, const kfx_pose *pose,
+                 const float Rinv[9], float *vmap, float *nmap, const int32_t *pix,
+                 int64_t npix) {
+  raycast_impl(tsdf, dims, vs, range, in, pose, Rinv, vmap, nmap, pix, npix, 0, dims[2], 0,
+               dims[2], nullptr);
+}
+
+void kfo_raycast_slab(const int16_t *tsdf, const int dims[3], const float vs[3],
+                      const float range[3], const kfx_intrinsics *in, const kfx_pose *pose,
+                      const float Rinv[9], int zb, int zn, int own0, int own1, float *vmap,
+                      float *nmap, uint32_t *keys) {
+  raycast_impl(tsdf, dims, vs, range, in, pose, Rinv, vmap, nmap, nullptr, 0, zb, zn, own0, own1,
+               keys);
 }
 
 int kfo_format_pose(const kfx_pose *p, char *buf, int cap) {

@@ -92,6 +92,14 @@ void kfo_raycast(const int16_t *tsdf, const int dims[3], const float voxel_size[
                  float *nmap, const int32_t *pix, int64_t npix);
 
 /* Whole-pipeline restatement of kf::kinectfusion (kinectfusion.cpp:9-195). */
+/* Z-slab restatement of the raycast: tsdf readable only in
+ * slices [zb, zb+zn); events only at samples whose nearest voxel z is in
+ * [own0, own1); keys[] = loop index of the deciding sample (UINT32_MAX none). */
+void kfo_raycast_slab(const int16_t *tsdf, const int dims[3], const float vs[3],
+                      const float range[3], const kfx_intrinsics *in, const kfx_pose *pose,
+                      const float Rinv[9], int zb, int zn, int own0, int own1, float *vmap,
+                      float *nmap, uint32_t *keys);
+
 typedef struct kfo_pipe kfo_pipe;
 kfo_pipe *kfo_pipe_create(const kfx_intrinsics *intr, const kfx_params *p);
 void kfo_pipe_destroy(kfo_pipe *pp);

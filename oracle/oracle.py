@@ -56,6 +56,8 @@ def lib():
                                     P(C.c_int64), P(C.c_int64)]
         L.kfo_raycast.argtypes = [P(C.c_int16), P(i), P(f), P(f), P(Intrinsics), P(Pose), P(f), P(f), P(f),
                                   P(C.c_int32), C.c_int64]
+        L.kfo_raycast_slab.argtypes = [P(C.c_int16), P(i), P(f), P(f), P(Intrinsics), P(Pose), P(f), i, i, i, i,
+                                       P(f), P(f), P(C.c_uint32)]
         L.kfo_pipe_create.argtypes = [P(Intrinsics), P(Params)]
         L.kfo_pipe_create.restype = C.c_void_p
         L.kfo_pipe_destroy.argtypes = [C.c_void_p]
@@ -221,6 +223,30 @@ def raycast(vol: Volume, intr: Intrinsics, cam2vol: Pose, Rinv: np.ndarray, pix:
                       fptr(vol.range), C.byref(intr), C.byref(cam2vol), fptr(Rinv), fptr(vmap), fptr(nmap),
                       pp, npix)
     return vmap, nmap
+
+
+def raycast_slab(tsdf: np.ndarray, vol: Volume, intr: Intrinsics, cam2vol: Pose, Rinv: np.ndarray,
+                 zb: int, zn: int, own0: int, own1: int):
+    """Per-slab raycast of the Z-slab decomposition: only slices
+    [zb, zb+zn) of `tsdf` (full-size array) are read.  Returns (keys u32, vmap, nmap)."""
+    vmap = np.zeros((intr.height, intr.width, 3), np.float32)
+    nmap = np.zeros_like(vmap)
+    keys = np.zeros((intr.height, intr.width), np.uint32)
+    Rinv = _f32(Rinv).reshape(9)
+    tsdf = np.ascontiguousarray(tsdf, np.int16)
+    lib().kfo_raycast_slab(i16ptr(tsdf), vol.dims.ctypes.data_as(C.POINTER(C.c_int)), fptr(vol.voxel_size),
+                           fptr(vol.range), C.byref(intr), C.byref(cam2vol), fptr(Rinv), zb, zn, own0, own1,
+                           fptr(vmap), fptr(nmap), keys.ctypes.data_as(C.POINTER(C.c_uint32)))
+    return keys, vmap, nmap
+
+
+def slab_bounds(Z: int, rank: int, world: int, halo: int = 4):
+    """(zb, zn, own0, own1) of slab `rank` (kfx_create_slab's partition)."""
+    own0, own1 = Z * rank // world, Z * (rank + 1) // world
+    if world == 1:
+        return 0, Z, 0, Z
+    zb = max(0, own0 - halo)
+    return zb, min(Z, own1 + halo) - zb, own0, own1
 
 
 def format_pose(p: Pose) -> str:

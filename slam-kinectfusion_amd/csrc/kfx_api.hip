@@ -87,6 +87,7 @@ struct kfx_ctx {
   uint8_t *bgr = nullptr;
   FrameView cur{}, prev{};
   float *inv_lambda = nullptr;
+  float2 *dl0 = nullptr;  // level-0 {depth m, 1/lambda}, the integrate gather table
   VolView vol{};
   DevState *st = nullptr;
   DevPose *pose_log = nullptr;
@@ -216,7 +217,7 @@ void enqueue_local(kfx_ctx *c, FrameInput in, bool events) {
   }
   launch_preprocess_maps(s, c->L, raw, in.d16, c->g, c->cur, c->p.bfilter_kernel_size,
                          c->p.bfilter_color_sigma, c->p.bfilter_spatial_sigma, c->p.dfilter_dist,
-                         c->st);
+                         c->inv_lambda, c->dl0, c->st);
   if (events) (void)hipEventRecord(c->ev[1], s);
   // ICPRegistration::rigidTransform (icp_registration.cpp:16-46)
   if (c->icp_persistent && c->icp_persistent_enabled) {
@@ -230,7 +231,7 @@ void enqueue_local(kfx_ctx *c, FrameInput in, bool events) {
     }
   }
   if (events) (void)hipEventRecord(c->ev[2], s);
-  launch_integrate(s, c->vol, c->g[0], c->cur.d[0], in.bgr, c->inv_lambda, c->st, c->pose_log,
+  launch_integrate(s, c->vol, c->g[0], c->dl0, in.bgr, c->st, c->pose_log,
                    to_dev(c->p.volu_pose), nullptr, nullptr);
   if (events) (void)hipEventRecord(c->ev[3], s);
   launch_raycast(s, c->vol, c->L, c->g, c->cur, c->prev, c->st, c->pose_log,
@@ -293,6 +294,21 @@ int ensure_pose_capacity(kfx_ctx *c, int more) {
   return KFX_OK;
 }
 
+// Capture the per-frame graph for `in` if graph mode is on and it does not
+// exist yet.  RCCL calls that refuse stream capture switch the context to
+// eager launches (returns KFX_OK with graph mode off).
+int ensure_graph(kfx_ctx *c, FrameInput in, hipGraphExec_t *graph) {
+  if (!c->graph_mode || !graph || *graph) return KFX_OK;
+  int r = build_graph(c, in, graph);
+  if (r && c->comm) {
+    (void)hipGetLastError();
+    c->graph_mode = false;
+    destroy_graphs(c);
+    return KFX_OK;
+  }
+  return r;
+}
+
 // graph: the cached executable for this input (built on first use), or null
 int run_frame(kfx_ctx *c, FrameInput in, hipGraphExec_t *graph) {
   int r = ensure_pose_capacity(c, 1);
@@ -306,25 +322,14 @@ int run_frame(kfx_ctx *c, FrameInput in, hipGraphExec_t *graph) {
     HIPCHK(hipEventElapsedTime(&c->stage_ms[4], c->ev[0], c->ev[4]));
     // stage order in the events: preprocess, icp(+commit), integrate,
     // raycast(+slab combine, +resize)
-  } else if (c->graph_mode && graph) {
-    if (!*graph) {
-      r = build_graph(c, in, graph);
-      if (r && c->comm) {
-        // RCCL calls that refuse stream capture: run this context eagerly
-        (void)hipGetLastError();
-        c->graph_mode = false;
-        destroy_graphs(c);
-        if ((r = enqueue_frame(c, in, false))) return r;
-        HIPCHK(hipGetLastError());
-        c->pending += 1;
-        return KFX_OK;
-      }
-      if (r) return r;
-    }
-    HIPCHK(hipGraphLaunch(*graph, c->stream));
   } else {
-    if ((r = enqueue_frame(c, in, false))) return r;
-    HIPCHK(hipGetLastError());
+    if ((r = ensure_graph(c, in, graph))) return r;
+    if (c->graph_mode && graph && *graph) {
+      HIPCHK(hipGraphLaunch(*graph, c->stream));
+    } else {
+      if ((r = enqueue_frame(c, in, false))) return r;
+      HIPCHK(hipGetLastError());
+    }
   }
   c->pending += 1;
   return KFX_OK;
@@ -367,6 +372,21 @@ VolView make_vol(const kfx_params &p, int rank, int world) {
   }
   v.trunc = p.volu_trun_dist;
   v.inv_trunc = 1.f / v.trunc;
+  // tsdf fixed point T* of the saturated free-space update (w = 64, ts = 1),
+  // iterated with the kernel's exact operations (tsdfhelper, tsdf_volume.cu:76-81)
+  v.tsat = 1 << 20;  // none
+  int t = 32767;
+  for (int it = 0; it < 64; ++it) {
+    const float pre_t = (float)t * 0.0000305185f;
+    const float new_t = std::fma(pre_t, 64.f, 1.f) / 65.f;
+    int q = (int)(new_t * 32767.f);
+    q = std::max(-32767, std::min(32767, q));
+    if (q == t) {
+      v.tsat = t;
+      break;
+    }
+    t = q;
+  }
   return v;
 }
 
@@ -525,6 +545,7 @@ static int create_impl(const kfx_intrinsics *intr, const kfx_params *params, int
   if ((r = dalloc(c, (void **)&c->raw0_u16, np0 * 2))) return fail(r);
   if ((r = dalloc(c, (void **)&c->bgr, np0 * 3))) return fail(r);
   if ((r = dalloc(c, (void **)&c->inv_lambda, np0 * 4))) return fail(r);
+  if ((r = dalloc(c, (void **)&c->dl0, np0 * 8))) return fail(r);
   c->vol = make_vol(p, rank, world);
   const size_t n = nvox(c);
   if ((r = dalloc(c, (void **)&c->vol.tsdf, n * 2))) return fail(r);
@@ -614,6 +635,11 @@ int kfx_stage_frames(kfx_ctx *c, int n, const uint8_t *bgr, const float *depth_m
   HIPCHK(hipMemcpyAsync(c->staged_bgr, bgr, np * 3 * (size_t)n, hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   c->n_staged = n;
+  // capture every staged frame's graph now, outside any timed frame loop
+  for (int i = 0; i < n; ++i)
+    if ((r = ensure_graph(c, {c->staged_depth + np * i, nullptr, c->staged_bgr + np * 3 * i},
+                          &c->staged_graph[i])))
+      return r;
   return KFX_OK;
 }
 
@@ -863,7 +889,8 @@ int kfx_stage_preprocess(kfx_ctx *c, const uint8_t *bgr, const float *depth_mm) 
                     nullptr);
   launch_preprocess_maps(c->stream, c->L, c->raw, nullptr, c->g, c->cur,
                          c->p.bfilter_kernel_size, c->p.bfilter_color_sigma,
-                         c->p.bfilter_spatial_sigma, c->p.dfilter_dist, c->st);
+                         c->p.bfilter_spatial_sigma, c->p.dfilter_dist, c->inv_lambda, c->dl0,
+                         c->st);
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(c->stream));
   return KFX_OK;
@@ -921,8 +948,8 @@ int kfx_stage_icp(kfx_ctx *c, kfx_pose *out) {
 
 static int integrate_counts_impl(kfx_ctx *c, int64_t *nu, int64_t *nc, const float *xpose) {
   HIPCHK(hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * 32, c->stream));
-  launch_integrate(c->stream, c->vol, c->g[0], c->cur.d[0], c->last_bgr ? c->last_bgr : c->bgr,
-                   c->inv_lambda, c->st, c->pose_log, to_dev(c->p.volu_pose), xpose, c->counters);
+  launch_integrate(c->stream, c->vol, c->g[0], c->dl0, c->last_bgr ? c->last_bgr : c->bgr, c->st,
+                   c->pose_log, to_dev(c->p.volu_pose), xpose, c->counters);
   HIPCHK(hipGetLastError());
   unsigned long long h[32];
   HIPCHK(hipMemcpyAsync(h, c->counters, sizeof(h), hipMemcpyDeviceToHost, c->stream));
@@ -947,8 +974,8 @@ int kfx_stage_integrate(kfx_ctx *c, const kfx_pose *vol2cam, int64_t *nu, int64_
   HIPCHK(hipMemcpyAsync(c->xpose, xp, sizeof(xp), hipMemcpyHostToDevice, c->stream));
   if (nu || nc)
     if ((r = integrate_counts_impl(c, nu, nc, c->xpose))) return r;
-  launch_integrate(c->stream, c->vol, c->g[0], c->cur.d[0], c->bgr, c->inv_lambda, c->st,
-                   c->pose_log, to_dev(c->p.volu_pose), c->xpose, nullptr);
+  launch_integrate(c->stream, c->vol, c->g[0], c->dl0, c->bgr, c->st, c->pose_log,
+                   to_dev(c->p.volu_pose), c->xpose, nullptr);
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(c->stream));
   return KFX_OK;

@@ -87,8 +87,9 @@ struct VolView {
   float range[3];  // volume_range
   float trunc;
   float inv_trunc;  // RN(1/trunc), for the exact FMA division (kfx_kernels.hip div_rn)
+  int tsat;         // tsdf fixed point of a weight-64, ts = 1 update (integrate skip), or 1<<20
   size_t slice;    // voxels per z slice (= X*Y)
-  size_t local_voxels() const { return slice * (size_t)zn; }
+  __host__ __device__ size_t local_voxels() const { return slice * (size_t)zn; }
 };
 
 struct FrameView {
@@ -104,7 +105,8 @@ void launch_pyr_down(hipStream_t s, const float *src, const uint16_t *src16, int
 // bilateral + truncation + vertex + normal maps, all levels (raw[l] = raw mm)
 void launch_preprocess_maps(hipStream_t s, int levels, const float *const raw[kMaxLevels],
                             const uint16_t *raw0_u16, const LevelGeom *g, FrameView cur, int ksz,
-                            float sigma_color, float sigma_spatial, float max_dist, DevState *st);
+                            float sigma_color, float sigma_spatial, float max_dist,
+                            const float *inv_lambda, float2 *dl0, DevState *st);
 int icp_blocks(const LevelGeom &g);
 // one ICP iteration (rigid_icp.cu:135-169 + icp_registration.cpp:33-42) in a
 // single launch; shards = 8 x 27 int64 zeroed, ticket zeroed (both self-reset)
@@ -120,9 +122,10 @@ void launch_icp(hipStream_t s, const LevelGeom &g, const float *cv, const float 
 // DevState + pose log (no separate commit launch).  `xpose` (device, 12 or 21
 // floats: pose [, Rinv]) overrides them for the stage seams; bookkeeping is
 // then skipped.
-void launch_integrate(hipStream_t s, VolView v, LevelGeom g0, const float *dmap,
-                      const uint8_t *bgr, const float *inv_lambda, DevState *st, DevPose *log,
-                      DevPose vpose, const float *xpose,
+// dl0: level-0 {depth m, 1/lambda} (written by launch_preprocess_maps)
+void launch_integrate(hipStream_t s, VolView v, LevelGeom g0, const float2 *dl0,
+                      const uint8_t *bgr, DevState *st, DevPose *log, DevPose vpose,
+                      const float *xpose,
                       unsigned long long *counters /* non-null: count-only, 32 words */);
 // raycast of level 0 + resizePointsNormals of levels >= 1 in one launch; with
 // keys != null the slab variant (owned events only, key per pixel, no resize)

@@ -230,6 +230,8 @@ struct BilatArgs {
   int ksz;
   float s_half, c_half;
   float max_dist;
+  const float *invl;  // 1/lambda per level-0 pixel
+  float2 *dl0;        // level 0: {filtered depth (m), 1/lambda} — the integrate gather
 };
 
 // cv::cuda::bilateralFilter (kinectfusion.cpp:57-65, A1 D: out of place) +
@@ -305,6 +307,7 @@ __global__ __launch_bounds__(256) void k_preprocess_maps(BilatArgs a, DevState *
   if (in) {
     const size_t o = (size_t)y * g.w + x;
     a.d[l][o] = dval;
+    if (l == 0) a.dl0[o] = make_float2(dval, a.invl[o]);
     st3(a.v[l], o, sv[c]);
     f3 n = {0.f, 0.f, 0.f};
     if (x >= 1 && x < g.w - 1 && y >= 1 && y < g.h - 1) {
@@ -812,6 +815,88 @@ __device__ __forceinline__ void clip_lin(double alpha, double beta, double &lo, 
   }
 }
 
+// Correctly rounded reciprocal for |d| in [2^-125, 2^125]: one Newton step on
+// v_rcp_f32 (checked against IEEE 1/d for every float in that range on gfx950,
+// tools/rn_check.hip).
+__device__ __forceinline__ float rcp_rn(float d) {
+  const float r = __builtin_amdgcn_rcpf(d);
+  return fmaf(fmaf(-d, r, 1.0f), r, r);
+}
+// Correctly rounded sqrt for x in [2^-96, 2^126]: v_rsq_f32 + one Newton step
+// (exhaustively checked against IEEE sqrtf, tools/rn_check.hip).
+__device__ __forceinline__ float sqrt_rn(float x) {
+  const float y = __builtin_amdgcn_rsqf(x);
+  const float s0 = x * y;
+  return fmaf(fmaf(-s0, s0, x), 0.5f * y, s0);
+}
+// A column's vc values are vc0 + zs accumulated by float adds: each component
+// is a multiple of 2^(min(exp(vc0), exp(zs)) - 23) (exact sums of multiples of
+// a power of two round to multiples of it), so it is 0 or at least that large,
+// and it stays below |vc0| + Z|zs| (x2 for rounding).  When every component
+// lies in {0} u [2^-40, 2^40], rcp_rn (|vc.z| in range), the shared-reciprocal
+// quotient (tools/markstein_general.c) and sqrt_rn (|vc|^2 in [2^-80, 2^82],
+// or vc.z <= 0 and the voxel is rejected anyway) are all exact; otherwise the
+// column takes the IEEE sequences.
+__device__ __forceinline__ int exp_of(float a) { return (int)((__float_as_uint(a) >> 23) & 0xffu) - 127; }
+__device__ __forceinline__ bool column_fast(f3 vc0, f3 zs, int Z) {
+  const float c0[3] = {vc0.x, vc0.y, vc0.z}, s[3] = {zs.x, zs.y, zs.z};
+  bool ok = true;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const double bound = 2.0 * ((double)fabsf(c0[k]) + (double)(Z + 1) * (double)fabsf(s[k]));
+    ok = ok && bound <= 0x1p40;  // false for NaN / inf poses
+    int e = 1000;
+    if (c0[k] != 0.f) e = min(e, exp_of(c0[k]));
+    if (s[k] != 0.f) e = min(e, exp_of(s[k]));
+    ok = ok && (e == 1000 || e - 23 >= -40);
+  }
+  return ok;
+}
+
+// 32-bit-offset buffer access (raw buffer resource; loads past num_records
+// return 0 and stores are dropped, so a rejected lane passes offset ~0u).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *p, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, (int)bytes, 0x00020000);
+}
+constexpr unsigned kOob = 0xFFFFFFFFu;
+
+// Voxel storage access of k_integrate: kIdx32 (local volume < 2^30 voxels)
+// uses buffer loads/stores with 32-bit byte offsets, else 64-bit pointers.
+template <bool kIdx32>
+struct VoxMem;
+template <>
+struct VoxMem<true> {
+  using Idx = unsigned;
+  __amdgpu_buffer_rsrc_t t, w, c;
+  __device__ VoxMem(const VolView &v) {
+    const size_t n = v.local_voxels();
+    t = make_rsrc(v.tsdf, (unsigned)(2 * n));
+    w = make_rsrc(v.weight, (unsigned)(2 * n));
+    c = make_rsrc(v.rgb, (unsigned)(4 * n));
+  }
+  __device__ int16_t ld_t(Idx i) const { return __builtin_amdgcn_raw_buffer_load_b16(t, i << 1, 0, 0); }
+  __device__ int16_t ld_w(Idx i) const { return __builtin_amdgcn_raw_buffer_load_b16(w, i << 1, 0, 0); }
+  __device__ uint32_t ld_c(Idx i) const { return __builtin_amdgcn_raw_buffer_load_b32(c, i << 2, 0, 0); }
+  __device__ void st_t(Idx i, int16_t x) const { __builtin_amdgcn_raw_buffer_store_b16(x, t, i << 1, 0, 0); }
+  __device__ void st_w(Idx i, int16_t x) const { __builtin_amdgcn_raw_buffer_store_b16(x, w, i << 1, 0, 0); }
+  __device__ void st_c(Idx i, uint32_t x) const { __builtin_amdgcn_raw_buffer_store_b32(x, c, i << 2, 0, 0); }
+  static constexpr Idx kNone = 0x7FFFFFFFu;  // byte offsets past every buffer
+};
+template <>
+struct VoxMem<false> {
+  using Idx = size_t;
+  int16_t *t, *w;
+  uint32_t *c;
+  __device__ VoxMem(const VolView &v) : t(v.tsdf), w(v.weight), c(v.rgb) {}
+  __device__ int16_t ld_t(Idx i) const { return t[i]; }
+  __device__ int16_t ld_w(Idx i) const { return w[i]; }
+  __device__ uint32_t ld_c(Idx i) const { return c[i]; }
+  __device__ void st_t(Idx i, int16_t x) const { t[i] = x; }
+  __device__ void st_w(Idx i, int16_t x) const { w[i] = x; }
+  __device__ void st_c(Idx i, uint32_t x) const { c[i] = x; }
+  static constexpr Idx kNone = 0;  // rejected lanes read voxel 0 (never written by them)
+};
+
 // Work split: a wave owns an 8x8 tile of columns and one of gridDim.y z-chunks
 // of every column's in-range interval (more waves per SIMD to hide latency);
 // each lane replays the vc adds up to its chunk start, so every voxel's vc is
@@ -820,9 +905,8 @@ __device__ __forceinline__ void clip_lin(double alpha, double beta, double &lo, 
 // algorithmic-byte inputs of the roofline.
 template <bool kCount, bool kIdx32>
 __global__ __launch_bounds__(256) void k_integrate(VolView v, LevelGeom g,
-                                                   const float *__restrict__ dmap,
+                                                   const float2 *__restrict__ dl,
                                                    const uint8_t *__restrict__ bgr,
-                                                   const float *__restrict__ invl,
                                                    DevState *__restrict__ st, DevPose *log,
                                                    DevPose vpose, const float *xpose,
                                                    unsigned long long *counters) {
@@ -908,45 +992,60 @@ __global__ __launch_bounds__(256) void k_integrate(VolView v, LevelGeom g,
   int z = 1;
 #pragma unroll 8
   for (; z < za; ++z) vc = add(vc, zs);
-  // voxel index of (x, y, z), advanced by one slice per z (32-bit when the
-  // volume has < 2^30 voxels, so byte offsets of the u32 colour fit too)
-  using Idx = typename std::conditional<kIdx32, unsigned, size_t>::type;
+  using Mem = VoxMem<kIdx32>;
+  using Idx = typename Mem::Idx;
+  const Mem mem(v);
+  const __amdgpu_buffer_rsrc_t rdl = make_rsrc(dl, (unsigned)(8 * g.w * g.h));
   const Idx slice = (Idx)v.slice;
-  Idx iz = (Idx)base + (Idx)(za - v.zb) * slice;
-  // Batches of kB voxels: projections, then the kB depth gathers, then the
-  // voxel loads of the batch are issued back to back (memory-level
-  // parallelism); each voxel's arithmetic is exactly the reference's.
+  Idx iz = (Idx)base + (Idx)(za - v.zb) * slice;  // voxel index of (x, y, z)
+  const bool fast = __all(column_fast(vc, zs, v.Z));  // wave-uniform
+  const float fw = (float)g.w, fh = (float)g.h;
+  // Batches of kB voxels: positions, projections, the kB {depth, 1/lambda}
+  // gathers, then the kB tsdf/weight loads are issued back to back
+  // (memory-level parallelism); each voxel's arithmetic is exactly the
+  // reference's (tsdf_volume.cu:56-98).
   constexpr int kB = 4;
   for (; z <= zb; z += kB) {
-    float sdf[kB], n2[kB];
-    int pix[kB];
-    bool ok[kB];
-    // Branch-free: both projections, the depth gathers and sdf are computed
-    // for every voxel of the batch (results of voxels the reference skips are
-    // discarded by ok[]), so the kB division chains interleave.
+    f3 p[kB];
+    float n2[kB];
 #pragma unroll
     for (int j = 0; j < kB; ++j) {
       vc = add(vc, zs);
+      p[j] = vc;
       n2[j] = dot(vc, vc);
-      const float y = 1.f / vc.z;
-      const float uf = proj_rn(vc.x, vc.z, y, g.fx, g.cx);
-      const float vf = proj_rn(vc.y, vc.z, y, g.fy, g.cy);
-      ok[j] = (z + j <= zb) & (vc.z > 0) & (int)in_range(uf, g.w) & (int)in_range(vf, g.h);
-      pix[j] = ok[j] ? (int)vf * g.w + (int)uf : 0;
     }
-    // Loads are issued unconditionally (inactive lanes read a dummy element
-    // that every such lane shares, so they add no traffic): a predicated load
-    // makes the compiler wait for it inside its branch.
-    float dep[kB], il[kB];
+    float sdf[kB];
+    unsigned pix[kB];
+    bool ok[kB];
+    if (fast) {  // the cheap exact sequences
 #pragma unroll
-    for (int j = 0; j < kB; ++j) {
-      dep[j] = dmap[pix[j]];
-      il[j] = invl[pix[j]];
-    }
+      for (int j = 0; j < kB; ++j) {
+        const float yv = rcp_rn(p[j].z);
+        const float uf = rintf(div_rn(p[j].x, p[j].z, yv) * g.fx + g.cx);
+        const float vf = rintf(div_rn(p[j].y, p[j].z, yv) * g.fy + g.cy);
+        ok[j] = (z + j <= zb) & (p[j].z > 0) & (uf >= 0.f) & (uf < fw) & (vf >= 0.f) & (vf < fh);
+        pix[j] = ok[j] ? ((unsigned)(int)vf * (unsigned)g.w + (unsigned)(int)uf) * 8u : kOob;
+      }
+      float2 d[kB];
 #pragma unroll
-    for (int j = 0; j < kB; ++j) {
-      sdf[j] = -(il[j] * sqrtf(n2[j]) - dep[j]);
-      ok[j] = ok[j] & (dep[j] > 0) & (sdf[j] >= -trunc);
+      for (int j = 0; j < kB; ++j)
+        d[j] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rdl, pix[j], 0, 0));
+#pragma unroll
+      for (int j = 0; j < kB; ++j) {
+        sdf[j] = -(d[j].y * sqrt_rn(n2[j]) - d[j].x);
+        ok[j] = ok[j] & (d[j].x > 0) & (sdf[j] >= -trunc);
+      }
+    } else {  // IEEE division / sqrt (tiny or huge operands)
+#pragma unroll
+      for (int j = 0; j < kB; ++j) {
+        const float uf = rintf((p[j].x / p[j].z) * g.fx + g.cx);
+        const float vf = rintf((p[j].y / p[j].z) * g.fy + g.cy);
+        ok[j] = (z + j <= zb) & (p[j].z > 0) & (uf >= 0.f) & (uf < fw) & (vf >= 0.f) & (vf < fh);
+        pix[j] = ok[j] ? ((unsigned)(int)vf * (unsigned)g.w + (unsigned)(int)uf) * 8u : kOob;
+        const float2 d = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rdl, pix[j], 0, 0));
+        sdf[j] = -(d.y * sqrtf(n2[j]) - d.x);
+        ok[j] = ok[j] & (d.x > 0) & (sdf[j] >= -trunc);
+      }
     }
     if (kCount) {
       iz += (Idx)kB * slice;
@@ -963,14 +1062,17 @@ __global__ __launch_bounds__(256) void k_integrate(VolView v, LevelGeom g,
 #pragma unroll
     for (int j = 0; j < kB; ++j) {
       vi[j] = iz + (Idx)j * slice;
-      const Idx i = ok[j] ? vi[j] : 0;
-      t0[j] = v.tsdf[i];
-      w0[j] = v.weight[i];
+      const Idx i = ok[j] ? vi[j] : Mem::kNone;
+      t0[j] = mem.ld_t(i);
+      w0[j] = mem.ld_w(i);
     }
     iz += (Idx)kB * slice;
 #pragma unroll
     for (int j = 0; j < kB; ++j) {
-      if (!ok[j]) continue;
+      // saturated free space (w = 64 at the tsdf fixed point T* of a ts = 1
+      // update, sdf >= trunc so ts = 1 and no colour band): the update is
+      // the identity — skip it (same stores skipped as below)
+      if (!ok[j] || (w0[j] == kMaxWeight && t0[j] == v.tsat && sdf[j] >= trunc)) continue;
       const Idx i = vi[j];
       const float ts = fminf(1.f, div_rn(sdf[j], trunc, v.inv_trunc));
       const int pre_w = w0[j];
@@ -982,11 +1084,11 @@ __global__ __launch_bounds__(256) void k_integrate(VolView v, LevelGeom g,
       q = max(-kShortMax, min(kShortMax, q));
       // saturated voxels (w = 64 at a tsdf fixed point) keep their values:
       // skipping those stores changes nothing and saves write bandwidth
-      if (q != t0[j]) v.tsdf[i] = (int16_t)q;
-      if (new_w != pre_w) v.weight[i] = (int16_t)new_w;
+      if (q != t0[j]) mem.st_t(i, (int16_t)q);
+      if (new_w != pre_w) mem.st_w(i, (int16_t)new_w);
       if (sdf[j] <= thres_color && sdf[j] >= -thres_color) {  // colour band (rare)
-        const uint32_t c0 = v.rgb[i];
-        const uint8_t *px = bgr + 3 * (size_t)pix[j];
+        const uint32_t c0 = mem.ld_c(i);
+        const uint8_t *px = bgr + 3 * (size_t)(pix[j] >> 3);
         const float c = (float)(new_w + 1);
         const float rc = rtab[new_w + 1];
         uint32_t out = 0u;
@@ -996,7 +1098,7 @@ __global__ __launch_bounds__(256) void k_integrate(VolView v, LevelGeom g,
           const float m = (float)(new_w * m0 + (int)px[ch]);
           out |= (uint32_t)(uint8_t)div_rn(m, c, rc) << (8 * ch);
         }
-        if (out != c0) v.rgb[i] = out;
+        if (out != c0) mem.st_c(i, out);
       }
     }
   }
@@ -1453,8 +1555,10 @@ void launch_pyr_down(hipStream_t s, const float *src, const uint16_t *src16, int
 void launch_preprocess_maps(hipStream_t s, int levels, const float *const raw[kMaxLevels],
                             const uint16_t *raw0_u16, const LevelGeom *g, FrameView cur, int ksz,
                             float sigma_color, float sigma_spatial, float max_dist,
-                            DevState *st) {
+                            const float *inv_lambda, float2 *dl0, DevState *st) {
   BilatArgs a{};
+  a.invl = inv_lambda;
+  a.dl0 = dl0;
   a.t = make_tiles(levels, g);
   for (int l = 0; l < levels; ++l) {
     a.raw[l] = raw[l];
@@ -1527,23 +1631,23 @@ void launch_icp(hipStream_t s, const LevelGeom &g, const float *cv, const float 
                      dist_thr, angle_thr, st, shards, ticket, force, update);
 }
 
-void launch_integrate(hipStream_t s, VolView v, LevelGeom g0, const float *dmap,
-                      const uint8_t *bgr, const float *inv_lambda, DevState *st, DevPose *log,
-                      DevPose vpose, const float *xpose, unsigned long long *counters) {
+void launch_integrate(hipStream_t s, VolView v, LevelGeom g0, const float2 *dl0,
+                      const uint8_t *bgr, DevState *st, DevPose *log, DevPose vpose,
+                      const float *xpose, unsigned long long *counters) {
   const int tiles = v.tiles_x * v.tiles_y;
   // z-chunks so that >= 16 waves per SIMD exist (16384 waves on 1024 SIMDs)
   const int nchunk = std::max(1, std::min(8, (16384 + tiles - 1) / tiles));
   dim3 grd((tiles + 3) / 4, nchunk);
   const bool idx32 = v.local_voxels() < (1ull << 30);
   if (counters)
-    hipLaunchKernelGGL((k_integrate<true, false>), grd, dim3(256), 0, s, v, g0, dmap, bgr,
-                       inv_lambda, st, log, vpose, xpose, counters);
+    hipLaunchKernelGGL((k_integrate<true, false>), grd, dim3(256), 0, s, v, g0, dl0, bgr, st, log,
+                       vpose, xpose, counters);
   else if (idx32)
-    hipLaunchKernelGGL((k_integrate<false, true>), grd, dim3(256), 0, s, v, g0, dmap, bgr,
-                       inv_lambda, st, log, vpose, xpose, counters);
+    hipLaunchKernelGGL((k_integrate<false, true>), grd, dim3(256), 0, s, v, g0, dl0, bgr, st, log,
+                       vpose, xpose, counters);
   else
-    hipLaunchKernelGGL((k_integrate<false, false>), grd, dim3(256), 0, s, v, g0, dmap, bgr,
-                       inv_lambda, st, log, vpose, xpose, counters);
+    hipLaunchKernelGGL((k_integrate<false, false>), grd, dim3(256), 0, s, v, g0, dl0, bgr, st, log,
+                       vpose, xpose, counters);
 }
 
 void launch_raycast(hipStream_t s, VolView v, int levels, const LevelGeom *g, FrameView cur,

@@ -20,14 +20,14 @@ int main(int argc, char **argv) {
 #pragma omp for
     for (long it = 0; it < millions; ++it) {
       for (int k = 0; k < 1000000; ++k) {
-        // d: exponent in [2^-12, 2^12], any significand; a quarter with extreme significands
+        // d, x: exponents in [2^-40, 2^40], any significand; a quarter with extreme significands
         uint32_t dm = RND() & 0x7fffffu;
         const uint32_t sel = RND() & 7u;
         if (sel == 0) dm = 0x7fffffu - (RND() & 0xffu);
         if (sel == 1) dm = RND() & 0xffu;
-        const uint32_t de = 127 - 12 + (RND() % 25);
+        const uint32_t de = 127 - 40 + (RND() % 81);
         const float d = bits((de << 23) | dm) * ((RND() & 1) ? -1.f : 1.f);
-        const uint32_t xe = 127 - 30 + (RND() % 61);
+        const uint32_t xe = 127 - 40 + (RND() % 81);
         const float x = bits((xe << 23) | (RND() & 0x7fffffu)) * ((RND() & 1) ? -1.f : 1.f);
         const float y = 1.0f / d;
         const float q0 = x * y;
