@@ -48,6 +48,7 @@ struct IcpPlan {
   int levels, nblocks, slots;
   LevelGeom g[kMaxLevels];
   int xe[kMaxLevels], npix[kMaxLevels], groups[kMaxLevels], iters[kMaxLevels];
+  int ppl[kMaxLevels];  // pixels per lane at each level
   const float *cv[kMaxLevels], *cn[kMaxLevels], *pv[kMaxLevels], *pn[kMaxLevels];
   float dist_thr, angle_thr;
 };

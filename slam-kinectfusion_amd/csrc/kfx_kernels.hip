@@ -12,6 +12,16 @@
 
 #include "kfx_internal.h"
 
+#ifndef KFX_INT_KB
+#define KFX_INT_KB 4  // integrate: voxels per batch (loads in flight per lane)
+#endif
+#ifndef KFX_SINCOS
+#define KFX_SINCOS 1
+#endif
+#ifndef KFX_INT_WAVES
+#define KFX_INT_WAVES 16384  // integrate: target wave count (z-chunks per column tile)
+#endif
+
 namespace kfx {
 namespace {
 
@@ -357,7 +367,8 @@ __device__ int icp_update(const long long *sums, DevPose &pose, double *xo);
 // oracle's int64 sums; the block total converts to int64 exactly.
 __device__ __forceinline__ void icp_lane(const LevelGeom &g, const DevPose &P,
                                          const f3 (&n0)[kIcpPix], const f3 (&v0)[kIcpPix],
-                                         const bool (&ok0)[kIcpPix], const float *__restrict__ pv,
+                                         const bool (&ok0)[kIcpPix], int ppl,
+                                         const float *__restrict__ pv,
                                          const float *__restrict__ pn, float dist_thr,
                                          float angle_thr, double (&acc)[27]) {
   const f3 t = {P.t[0], P.t[1], P.t[2]};
@@ -368,6 +379,9 @@ __device__ __forceinline__ void icp_lane(const LevelGeom &g, const DevPose &P,
   bool ok[kIcpPix];
 #pragma unroll
   for (int q = 0; q < kIcpPix; ++q) {
+    ok[q] = false;
+    j[q] = 0;
+    if (q >= ppl) continue;  // block-uniform: pixels per lane at this level
     vcur[q] = add(rmul(P.R, v0[q]), t);
     const int px = f2i_rn((vcur[q].x / vcur[q].z) * g.fx + g.cx);
     const int py = f2i_rn((vcur[q].y / vcur[q].z) * g.fy + g.cy);
@@ -380,6 +394,7 @@ __device__ __forceinline__ void icp_lane(const LevelGeom &g, const DevPose &P,
   f3 vpre[kIcpPix], npre[kIcpPix];
 #pragma unroll
   for (int q = 0; q < kIcpPix; ++q) {
+    if (q >= ppl) continue;
     vpre[q] = ld3(pv, j[q]);
     npre[q] = ld3(pn, j[q]);
   }
@@ -409,48 +424,97 @@ __device__ __forceinline__ void icp_lane(const LevelGeom &g, const DevPose &P,
 
 // Current-frame vertex/normal of the lane's pixels of pixel group grp.
 __device__ __forceinline__ void icp_load_cur(const LevelGeom &g, int xe, int npix, int grp,
-                                             const float *__restrict__ cv,
+                                             int ppl, const float *__restrict__ cv,
                                              const float *__restrict__ cn, f3 (&n0)[kIcpPix],
                                              f3 (&v0)[kIcpPix], bool (&ok)[kIcpPix]) {
 #pragma unroll
   for (int q = 0; q < kIcpPix; ++q) {
-    const int i = grp * kIcpBlockPix + q * 256 + threadIdx.x;
-    ok[q] = i < npix;
+    const int i = grp * 256 * ppl + q * 256 + threadIdx.x;
+    ok[q] = q < ppl && i < npix;
     const size_t idx = ok[q] ? (size_t)(i / xe) * g.w + (i % xe) : 0;
     n0[q] = ld3(cn, idx);
     v0[q] = ld3(cv, idx);
   }
 }
 
-// LDS transpose reduction of the block's 256 x 27 lane sums: row (wave, k)
-// holds 64 lane values (stride 65 to spread banks); 108 threads sum one row
-// each.  Returns, in threads 0..26, the block's sum of product k as int64.
+// Block reduction of the 256 lanes' 27 sums.  Within a wave, a reduce-scatter
+// butterfly in registers: at each step a lane keeps the half of its values
+// selected by one lane bit and adds its partner's copy of that half, so after
+// 5 steps lane L holds value (L >> 1) summed over 32 lanes, and a last
+// exchange completes the wave sum — 32 exchanges instead of 27 full
+// reductions, all cross-lane VALU ops (gfx950 v_permlane32/16_swap for lane
+// bits 5 and 4, DPP row_ror:8 / row_half_mirror / quad_perm for bits 3..0), no
+// LDS round trips.  The 4 waves then meet in LDS.  Values are integers below
+// 2^53: every order of fp64 adds is exact.  Returns, in threads 0..26, the
+// block's sum k as int64.
 struct IcpRed {
-  double red[4 * 27 * 65];
   double red2[kIcpShards * 27];  // >= 4 * 27; also stages the shard reads
 };
+__device__ __forceinline__ unsigned lo32(double v) { return (unsigned)__double_as_longlong(v); }
+__device__ __forceinline__ unsigned hi32(double v) {
+  return (unsigned)((unsigned long long)__double_as_longlong(v) >> 32);
+}
+__device__ __forceinline__ double mk64(unsigned lo, unsigned hi) {
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+// Lane bits 5 / 4: v_permlane{32,16}_swap exchanges x of the upper lanes with y
+// of the lower lanes, after which x + y is, in every lane, its kept value plus
+// the partner's copy of it (lower lanes keep x = in[v], upper lanes y = in[N+v]).
+template <int N, bool k32>
+__device__ __forceinline__ void butterfly_swap(const double (&in)[2 * N], double (&out)[N]) {
+#pragma unroll
+  for (int v = 0; v < N; ++v) {
+    const double x = in[v], y = in[N + v];
+    unsigned xl, xh, yl, yh;
+    if (k32) {
+      const auto rl = __builtin_amdgcn_permlane32_swap(lo32(x), lo32(y), false, false);
+      const auto rh = __builtin_amdgcn_permlane32_swap(hi32(x), hi32(y), false, false);
+      xl = rl[0], yl = rl[1], xh = rh[0], yh = rh[1];
+    } else {
+      const auto rl = __builtin_amdgcn_permlane16_swap(lo32(x), lo32(y), false, false);
+      const auto rh = __builtin_amdgcn_permlane16_swap(hi32(x), hi32(y), false, false);
+      xl = rl[0], yl = rl[1], xh = rh[0], yh = rh[1];
+    }
+    out[v] = mk64(xl, xh) + mk64(yl, yh);
+  }
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp64(double v) {
+  return mk64((unsigned)__builtin_amdgcn_mov_dpp((int)lo32(v), CTRL, 0xf, 0xf, false),
+              (unsigned)__builtin_amdgcn_mov_dpp((int)hi32(v), CTRL, 0xf, 0xf, false));
+}
+// Lane bits 3..1 through DPP: the partner (row_ror:8, row_half_mirror,
+// quad_perm [2,3,0,1]) differs in `bit`; lanes with the bit clear keep in[v].
+template <int N, int CTRL>
+__device__ __forceinline__ void butterfly_dpp(const double (&in)[2 * N], double (&out)[N], int bit) {
+  const bool hi = (threadIdx.x >> bit) & 1;
+#pragma unroll
+  for (int v = 0; v < N; ++v) {
+    const double keep = hi ? in[N + v] : in[v];
+    const double give = hi ? in[v] : in[N + v];
+    out[v] = keep + dpp64<CTRL>(give);
+  }
+}
 __device__ __forceinline__ long long icp_block_reduce(IcpRed &r, const double (&acc)[27]) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  double a32[32];
 #pragma unroll
-  for (int k = 0; k < 27; ++k) r.red[(wv * 27 + k) * 65 + lane] = acc[k];
-  __syncthreads();
-  if (threadIdx.x < 108) {
-    const double *row = r.red + threadIdx.x * 65;
-    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
-    for (int q = 0; q < 64; q += 4) {
-      s0 += row[q];
-      s1 += row[q + 1];
-      s2 += row[q + 2];
-      s3 += row[q + 3];
-    }
-    r.red2[threadIdx.x] = (s0 + s1) + (s2 + s3);
-  }
+  for (int k = 0; k < 32; ++k) a32[k] = k < 27 ? acc[k] : 0.0;
+  double a16[16], a8[8], a4[4], a2[2], a1[1];
+  butterfly_swap<16, true>(a32, a16);    // lane bit 5
+  butterfly_swap<8, false>(a16, a8);     // lane bit 4
+  butterfly_dpp<4, 0x128>(a8, a4, 3);    // row_ror:8       (lane bit 3)
+  butterfly_dpp<2, 0x141>(a4, a2, 2);    // row_half_mirror (lane bit 2)
+  butterfly_dpp<1, 0x4E>(a2, a1, 1);     // quad_perm [2,3,0,1] (lane bit 1)
+  const double w = a1[0] + dpp64<0xB1>(a1[0]);  // quad_perm [1,0,3,2]: value (lane >> 1)
+  if ((lane & 1) == 0 && (lane >> 1) < 27) r.red2[wv * 27 + (lane >> 1)] = w;
   __syncthreads();
   long long v = 0;
   if (threadIdx.x < 27) {
     const int k = threadIdx.x;
     v = (long long)(r.red2[k] + r.red2[27 + k] + r.red2[54 + k] + r.red2[81 + k]);
   }
+  __syncthreads();  // red2 is reused by the caller
   return v;
 }
 
@@ -469,9 +533,9 @@ __global__ __launch_bounds__(256) void k_icp_acc(LevelGeom g, int xe, int npix,
   const DevPose P = st->icp_pose;
   f3 n0[kIcpPix], v0[kIcpPix];
   bool ok[kIcpPix];
-  icp_load_cur(g, xe, npix, blockIdx.x, cv, cn, n0, v0, ok);
+  icp_load_cur(g, xe, npix, blockIdx.x, kIcpPix, cv, cn, n0, v0, ok);
   double acc[27];
-  icp_lane(g, P, n0, v0, ok, pv, pn, dist_thr, angle_thr, acc);
+  icp_lane(g, P, n0, v0, ok, kIcpPix, pv, pn, dist_thr, angle_thr, acc);
   __shared__ IcpRed red;
   const long long bsum = icp_block_reduce(red, acc);
   // Cross-block sum + solve in the same launch: wave 0 adds the block's 27
@@ -550,7 +614,8 @@ __global__ __launch_bounds__(256, 2) void k_icp_track(IcpPlan pl, DevState *__re
     const bool mine = (int)blockIdx.x < pl.groups[l];
     f3 n0[kIcpPix], v0[kIcpPix];
     bool ok[kIcpPix];
-    if (mine) icp_load_cur(g, pl.xe[l], pl.npix[l], blockIdx.x, pl.cv[l], pl.cn[l], n0, v0, ok);
+    if (mine)
+      icp_load_cur(g, pl.xe[l], pl.npix[l], blockIdx.x, pl.ppl[l], pl.cv[l], pl.cn[l], n0, v0, ok);
     for (int it = 0; it < pl.iters[l] && !fail; ++it, ++slot) {
       unsigned long long *sh = sy->sums + (size_t)slot * kIcpShards * 27;
       target += pl.groups[l];
@@ -558,7 +623,7 @@ __global__ __launch_bounds__(256, 2) void k_icp_track(IcpPlan pl, DevState *__re
       if (tr && blockIdx.x == 0) sy->trace[slot][0] = wall_clock64();
       if (mine) {
         double acc[27];
-        icp_lane(g, P, n0, v0, ok, pl.pv[l], pl.pn[l], pl.dist_thr, pl.angle_thr, acc);
+        icp_lane(g, P, n0, v0, ok, pl.ppl[l], pl.pv[l], pl.pn[l], pl.dist_thr, pl.angle_thr, acc);
         if (tr && blockIdx.x == 0) sy->trace[slot][8] = wall_clock64() + (acc[3] == -1.5 ? 1 : 0);
         const long long bsum = icp_block_reduce(red, acc);
         if (tr && blockIdx.x == 0) sy->trace[slot][9] = wall_clock64() + (bsum == -7 ? 1 : 0);
@@ -676,62 +741,75 @@ __device__ __forceinline__ double bcast(double v, int src) {
   return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
-// icp_registration.cpp:33-42 on the device, run by one whole wave: A/b unpack
-// (rigid_icp.cu:156-165), partial-pivot LU with det check, LU solve (D:
-// instead of SVD), Rodrigues, pose = pose * Tinc.  Lane 7*i+j holds A[i][j]
-// (j == 6: b[i]); each elimination step updates all (i > k, j > k) elements
-// at once with exactly the oracle's per-element operation
-// A[i][j] - (A[i][k] / A[k][k]) * A[k][j] (kfo_icp_update), so the result is
-// bit-identical to the sequential loop.  Everything after the LU is computed
-// redundantly by every lane (uniform results).  sums: 27 int64 (any memory).
+// icp_registration.cpp:33-42 on the device: A/b unpack (rigid_icp.cu:156-165),
+// partial-pivot LU with det check, LU solve (D: instead of SVD), Rodrigues,
+// pose = pose * Tinc.  Every lane runs the whole solve on its own registers
+// (identical, wave-uniform values: no cross-lane traffic on the critical
+// path); the pivot row is made uniform so the row swap is a scalar branch.
+// Each double operation is the oracle's (kfo_icp_update) in the same order,
+// so the result is bit-identical.  Columns left of the pivot are dead after
+// their step and are not swapped.  sums: 27 int64 (any memory, read by all
+// lanes).
 __device__ int icp_update(const long long *sums, DevPose &pose, double *xo) {
-  const int lane = threadIdx.x & 63;
-  const int i = lane / 7, j = lane - 7 * (lane / 7);
-  const bool live = lane < 42;
-  double a = 0.0;
-  if (live) {
-    const int r = (j == 6 || i <= j) ? i : j, c = (j == 6 || i <= j) ? j : i;
-    a = (double)sums[7 * r - r * (r - 1) / 2 + (c - r)] * (1.0 / 4294967296.0);
+  double A[6][7];  // column 6 = b
+  {
+    int q = 0;
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+      for (int j = i; j < 7; ++j) {
+        const double v = (double)sums[q++] * (1.0 / 4294967296.0);
+        A[i][j] = v;
+        if (j < 6) A[j][i] = v;
+      }
   }
   int sign = 1;
 #pragma unroll
   for (int k = 0; k < 6; ++k) {
     int p = k;
-    double best = fabs(bcast(a, 7 * k + k));
+    double best = fabs(A[k][k]);
 #pragma unroll
-    for (int r = k + 1; r < 6; ++r) {
-      const double t = fabs(bcast(a, 7 * r + k));
+    for (int i = k + 1; i < 6; ++i) {
+      const double t = fabs(A[i][k]);
       if (t > best) {
         best = t;
-        p = r;
+        p = i;
       }
     }
-    if (p != k) {  // wave-uniform
-      const int src = (i == k) ? 7 * p + j : ((i == p) ? 7 * k + j : lane);
-      a = __shfl(a, src);
+    p = __builtin_amdgcn_readfirstlane(p);  // identical in every lane
+    if (p != k) {
+#pragma unroll
+      for (int i = k + 1; i < 6; ++i)
+        if (p == i) {
+#pragma unroll
+          for (int j = k; j < 7; ++j) {
+            const double tmp = A[k][j];
+            A[k][j] = A[i][j];
+            A[i][j] = tmp;
+          }
+        }
       sign = -sign;
     }
-    const double akk = bcast(a, 7 * k + k);
-    if (akk != 0.0) {
-      const double aik = __shfl(a, live ? 7 * i + k : lane);
-      const double akj = __shfl(a, live ? 7 * k + j : lane);
-      if (live && i > k && j > k) {
-        const double f = aik / akk;
-        a = a - f * akj;
+    if (A[k][k] != 0.0) {
+#pragma unroll
+      for (int i = k + 1; i < 6; ++i) {
+        const double f = A[i][k] / A[k][k];
+#pragma unroll
+        for (int j = k + 1; j < 7; ++j) A[i][j] = A[i][j] - f * A[k][j];
       }
     }
   }
   double det = (double)sign;
 #pragma unroll
-  for (int k = 0; k < 6; ++k) det = det * bcast(a, 7 * k + k);
+  for (int k = 0; k < 6; ++k) det = det * A[k][k];
   if (fabs(det) < 1e-15 || isnan(det)) return 1;
   double x[6];
 #pragma unroll
   for (int r = 5; r >= 0; --r) {
-    double acc = bcast(a, 7 * r + 6);
+    double acc = A[r][6];
 #pragma unroll
-    for (int c = r + 1; c < 6; ++c) acc = acc - bcast(a, 7 * r + c) * x[c];
-    x[r] = acc / bcast(a, 7 * r + r);
+    for (int c = r + 1; c < 6; ++c) acc = acc - A[r][c] * x[c];
+    x[r] = acc / A[r][r];
   }
 #pragma unroll
   for (int r = 0; r < 6; ++r) xo[r] = x[r];
@@ -747,7 +825,17 @@ __device__ int icp_update(const long long *sums, DevPose &pose, double *xo) {
 #pragma unroll
     for (int q = 0; q < 9; ++q) inc.R[q] = (q % 4 == 0) ? 1.f : 0.f;
   } else {
-    const double c = cos(theta), sn = sin(theta), c1 = 1.0 - c;
+    double sn, c;
+#if KFX_SINCOS == 2  // timing experiment only (wrong values)
+    c = 1.0 - 0.5 * theta * theta;
+    sn = theta;
+#elif KFX_SINCOS
+    sincos(theta, &sn, &c);  // one shared range reduction
+#else
+    c = cos(theta);
+    sn = sin(theta);
+#endif
+    const double c1 = 1.0 - c;
     const double it = 1.0 / theta;
     const float r[3] = {(float)(rv[0] * it), (float)(rv[1] * it), (float)(rv[2] * it)};
     const float rrt[9] = {r[0] * r[0], r[0] * r[1], r[0] * r[2], r[0] * r[1], r[1] * r[1],
@@ -1004,7 +1092,7 @@ __global__ __launch_bounds__(256) void k_integrate(VolView v, LevelGeom g,
   // gathers, then the kB tsdf/weight loads are issued back to back
   // (memory-level parallelism); each voxel's arithmetic is exactly the
   // reference's (tsdf_volume.cu:56-98).
-  constexpr int kB = 4;
+  constexpr int kB = KFX_INT_KB;
   for (; z <= zb; z += kB) {
     f3 p[kB];
     float n2[kB];
@@ -1595,7 +1683,10 @@ IcpPlan make_icp_plan(int levels, const LevelGeom *g, const int *iters, FrameVie
   for (int l = 0; l < levels; ++l) {
     pl.g[l] = g[l];
     pl.npix[l] = icp_npix(g[l], &pl.xe[l]);
-    pl.groups[l] = (pl.npix[l] + kIcpBlockPix - 1) / kIcpBlockPix;
+    // pixels per lane: the fewest that keep the level within one block per
+    // CU (256), so coarse levels spread over more waves (shorter lane phase)
+    pl.ppl[l] = std::max(1, std::min(kIcpPix, (pl.npix[l] + 256 * 256 - 1) / (256 * 256)));
+    pl.groups[l] = std::max(1, (pl.npix[l] + 256 * pl.ppl[l] - 1) / (256 * pl.ppl[l]));
     pl.iters[l] = iters[l];
     pl.cv[l] = cur.v[l];
     pl.cn[l] = cur.n[l];
@@ -1635,8 +1726,8 @@ void launch_integrate(hipStream_t s, VolView v, LevelGeom g0, const float2 *dl0,
                       const uint8_t *bgr, DevState *st, DevPose *log, DevPose vpose,
                       const float *xpose, unsigned long long *counters) {
   const int tiles = v.tiles_x * v.tiles_y;
-  // z-chunks so that >= 16 waves per SIMD exist (16384 waves on 1024 SIMDs)
-  const int nchunk = std::max(1, std::min(8, (16384 + tiles - 1) / tiles));
+  // z-chunks so that >= KFX_INT_WAVES waves exist (16 per SIMD on 1024 SIMDs)
+  const int nchunk = std::max(1, std::min(8, (KFX_INT_WAVES + tiles - 1) / tiles));
   dim3 grd((tiles + 3) / 4, nchunk);
   const bool idx32 = v.local_voxels() < (1ull << 30);
   if (counters)

@@ -22,7 +22,7 @@ __all__ = ["KinectFusion", "KfxError", "comm_unique_id", "pipeline_group", "lib"
            "default_params", "KFX_FRAME_CUR", "KFX_FRAME_PREV", "KFX_OK", "KFX_TRACKING_LOST", "EXPORTS"]
 
 _PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(_PKG, "lib", "libkfx.so")
+LIB_PATH = os.environ.get("KFX_LIB_PATH") or os.path.join(_PKG, "lib", "libkfx.so")  # override: tuning runs
 
 # every symbol include/kfx.h declares
 EXPORTS = [
