@@ -985,6 +985,35 @@ struct VoxMem<false> {
   static constexpr Idx kNone = 0;  // rejected lanes read voxel 0 (never written by them)
 };
 
+// tsdf reads of k_raycast: kIdx32 (local volume < 2^31 voxels) uses a buffer
+// load with a 32-bit byte offset (24-bit multiplies; rejected samples read 0
+// past the buffer end without a memory access), else 64-bit pointers.
+template <bool kIdx32>
+struct RayMem;
+template <>
+struct RayMem<true> {
+  __amdgpu_buffer_rsrc_t t;
+  unsigned slice, tiles_x;
+  int zb;
+  __device__ RayMem(const VolView &v)
+      : t(make_rsrc(v.tsdf, (unsigned)(2 * v.local_voxels()))), slice((unsigned)v.slice),
+        tiles_x((unsigned)v.tiles_x), zb(v.zb) {}
+  __device__ int16_t ld(bool valid, int x, int y, int z) const {
+    const unsigned ux = (unsigned)x, uy = (unsigned)y;
+    const unsigned in_slice = (__umul24(uy >> 3, tiles_x) + (ux >> 3)) * 64u + ((uy & 7u) << 3 | (ux & 7u));
+    const unsigned idx = __umul24((unsigned)(z - zb), slice) + in_slice;
+    return __builtin_amdgcn_raw_buffer_load_b16(t, valid ? idx * 2u : kOob, 0, 0);
+  }
+};
+template <>
+struct RayMem<false> {
+  const VolView *v;
+  __device__ RayMem(const VolView &vv) : v(&vv) {}
+  __device__ int16_t ld(bool valid, int x, int y, int z) const {
+    return valid ? v->tsdf[vox_index(*v, x, y, z)] : (int16_t)0;
+  }
+};
+
 // Work split: a wave owns an 8x8 tile of columns and one of gridDim.y z-chunks
 // of every column's in-range interval (more waves per SIMD to hide latency);
 // each lane replays the vc adds up to its chunk start, so every voxel's vc is
@@ -1365,45 +1394,48 @@ __global__ __launch_bounds__(256) void k_raycast(VolView v, RayArgs ra, RayConst
     constexpr int kR = 16;
     int sprev = isnan(tprev) ? 0 : (tprev > 0.f ? 1 : (tprev < 0.f ? -1 : 0));
     uint32_t kbase = 1u;  // loop sample index of the batch's first sample
+    const RayMem<kIdx32> mem(v);
+    // voxel validity 1 <= i <= dim-2 (tsdf_volume.cu:184-185) tested on the
+    // rounded floats (exact integers; NaN fails like __float2int_rn's INT_MIN)
+    const float hx = (float)(v.X - 2), hy = (float)(v.Y - 2), hz = (float)(v.Z - 2);
+    const float szb = (float)v.zb, sze = (float)(v.zb + v.zn);
+    const float so0 = (float)v.own0, so1 = (float)v.own1;
     while (__any(live)) {
       int16_t raw[kR];
-      bool val[kR];
-      unsigned ownm = 0u;
-      int je = kR;
+      unsigned pm = 0u, nm = 0u, am = 0u, ownm = 0u;
       float rl = ray_len;
 #pragma unroll
       for (int j = 0; j < kR; ++j) {
+        // a is monotone in j (rl only grows), so lanes past tfar or dead
+        // just keep stepping: their samples are masked off
         const bool a = live && rl < tfar;
-        je = (!a && je == kR) ? j : je;
-        nextp.x = a ? nextp.x + vstep.x : nextp.x;
-        nextp.y = a ? nextp.y + vstep.y : nextp.y;
-        nextp.z = a ? nextp.z + vstep.z : nextp.z;
-        const int ix = f2i_rn(nextp.x * rc.vs_inv.x);
-        const int iy = f2i_rn(nextp.y * rc.vs_inv.y);
-        const int iz = f2i_rn(nextp.z * rc.vs_inv.z);
-        // 1 <= i <= dim-2 on each axis (tsdf_volume.cu:184-185), as unsigned compares
-        val[j] = a & ((unsigned)(ix - 1) < (unsigned)(v.X - 2)) &
-                 ((unsigned)(iy - 1) < (unsigned)(v.Y - 2)) & ((unsigned)(iz - 1) < (unsigned)(v.Z - 2));
+        am |= a ? (1u << j) : 0u;
+        nextp = add(nextp, vstep);
+        const float fx = rintf(nextp.x * rc.vs_inv.x);
+        const float fy = rintf(nextp.y * rc.vs_inv.y);
+        const float fz = rintf(nextp.z * rc.vs_inv.z);
+        bool val = a & (fx >= 1.f) & (fx <= hx) & (fy >= 1.f) & (fy <= hy) & (fz >= 1.f) & (fz <= hz);
         if (kSlab) {
-          val[j] = val[j] & ((unsigned)(iz - v.zb) < (unsigned)v.zn);
-          ownm |= ((unsigned)(iz - v.own0) < (unsigned)(v.own1 - v.own0)) ? (1u << j) : 0u;
+          val = val & (fz >= szb) & (fz < sze);
+          ownm |= ((fz >= so0) & (fz < so1)) ? (1u << j) : 0u;
         }
-        raw[j] = v.tsdf[val[j] ? ray_index<kIdx32>(v, ix, iy, iz) : 0];
-        rl = a ? rl + rc.step : rl;
+        raw[j] = mem.ld(val, (int)fx, (int)fy, (int)fz);
+        pm |= (val && raw[j] > 0) ? (1u << j) : 0u;
+        nm |= (val && raw[j] < 0) ? (1u << j) : 0u;
+        rl = rl + rc.step;
       }
-      unsigned ev = 0u, hitm = 0u;
+      const int je = __builtin_ctz(~am);  // first sample outside [.., tfar) (kR if none)
+      // an event at j needs opposite signs at samples j-1, j (tsdf_cur is the
+      // previous sample; NaN = sign 0): +/- is a hit candidate, -/+ a stop
+      const unsigned pprev = (pm << 1) | (sprev > 0 ? 1u : 0u);
+      const unsigned nprev = (nm << 1) | (sprev < 0 ? 1u : 0u);
+      const unsigned hitm = pprev & nm;
+      unsigned ev = hitm | (nprev & pm);
       const float tfirst = tprev;
-      int sp = sprev;
-#pragma unroll
-      for (int j = 0; j < kR; ++j) {
-        const int sj = val[j] ? (raw[j] > 0) - (raw[j] < 0) : 0;
-        const bool e = sp * sj == -1;
-        ev |= e ? (1u << j) : 0u;
-        hitm |= (e && sj < 0) ? (1u << j) : 0u;
-        sp = sj;
-      }
-      sprev = sp;
-      tprev = val[kR - 1] ? (float)raw[kR - 1] * kDivShortMax : NAN;
+      sprev = ((pm >> (kR - 1)) & 1u) ? 1 : (((nm >> (kR - 1)) & 1u) ? -1 : 0);
+      // tsdf_cur of the next batch's first sample; read only when it is a
+      // valid positive sample (a +/- event at j = 0 needs sprev > 0)
+      tprev = (float)raw[kR - 1] * kDivShortMax;
       if (kSlab) ev &= ownm;  // only owned samples may end the ray on this slab
       unsigned pend = live ? ev : 0u;
       while (__any(pend != 0u)) {
@@ -1753,7 +1785,7 @@ void launch_raycast(hipStream_t s, VolView v, int levels, const LevelGeom *g, Fr
   ra.levels = levels;
   for (int l = 0; l < levels; ++l) ra.g[l] = g[l];
   dim3 grd(((g[0].w + 15) / 16) * ((g[0].h + 15) / 16));
-  const bool idx32 = v.local_voxels() < (1ull << 32);
+  const bool idx32 = v.local_voxels() < (1ull << 31) && v.slice < (1ull << 24);
   if (keys) {
     if (idx32)
       hipLaunchKernelGGL((k_raycast<true, true>), grd, dim3(256), 0, s, v, ra, rc, cur, prev, st, log,
