@@ -179,9 +179,29 @@ int kfx_get_stage_ms(kfx_ctx *ctx, float out_ms[5]);
  * volume is not touched. */
 int kfx_integrate_counts(kfx_ctx *ctx, int64_t *n_updated, int64_t *n_colored);
 
+/* ---- point cloud ------------------------------------------ */
+/* TSDFVolume::fetchPointCloud buffer size (tsdf_volume.cpp:67) */
+#define KFX_DEFAULT_CLOUD_POINTS 10000000
+/* kinectfusion::extracePointcloud (kinectfusion.cpp:142-147) ->
+ * TSDFVolume::fetchPointCloud (tsdf_volume.cpp:63-84) -> device::extract_points
+ * (FullScan6, tsdf_volume.cu:307-499): zero crossings of the volume along +x,
+ * +y, +z, in volume-pose (world) coordinates.  Writes min(cap, total) points
+ * (float3) to xyz (NULL with cap 0: count only) and the total to *n_points.
+ * The reference's order is nondeterministic (atomics); here it is canonical
+ * (slice chunk, 8x8 tile, z, lane, edge), so the first `cap` points
+ * are deterministic.  A slab context extracts its owned slices; concatenating
+ * slabs in rank order gives the single-volume cloud. */
+int kfx_extract_points(kfx_ctx *ctx, float *xyz, int64_t cap, int64_t *n_points);
+/* kinectfusion::savePointcloud (kinectfusion.cpp:148-166): ASCII PLY, x y z per
+ * line with ostream's default 6 significant digits. */
+int kfx_write_ply(const char *path, const float *xyz, int64_t n);
+/* extract (cap <= 0: KFX_DEFAULT_CLOUD_POINTS) + kfx_write_ply */
+int kfx_save_pointcloud(kfx_ctx *ctx, const char *path, int64_t cap);
+
 /* ---- Z-slab sharding (new; the reference is single-GPU) -------------------
  * One kf::kinectfusion stream split over `world` GPUs: slab
- * `rank` owns global z slices [Z*rank/world, Z*(rank+1)/world) of the volume
+ * `rank` owns global z slices [cut(rank), cut(rank+1)) of the volume, cut(r) =
+ * floor(Z*r/world) rounded down to a multiple of 8 (cut(world) = Z),
  * and stores 4 halo slices on each side, which it integrates itself.
  * Preprocess and ICP run on every slab (identical results, no collective);
  * raycast events are combined across slabs each frame (all-reduce MIN of the

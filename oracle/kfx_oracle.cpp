@@ -653,6 +653,55 @@ void kfo_raycast_slab(const int16_t *tsdf, const int dims[3], const float vs[3],
                keys);
 }
 
+// FullScan6 (tsdf_volume.cu:307-481) in the canonical order of the GPU
+// extraction (D: the reference's order comes from warp atomics): chunks of 8
+// slices aligned to global multiples of 8, then 8x8 (x,y) tiles row-major,
+// then z, then (y&7, x&7), then the +x/+y/+z edge.  z covers [zlo, zhi)
+// (zhi <= Z-1).  Writes min(cap, total) points, returns the total.
+int64_t kfo_extract_points(const int16_t *tsdf, const int16_t *weight, const int dims[3],
+                           const float vs[3], const kfx_pose *aff, int zlo, int zhi, float *out,
+                           int64_t cap) {
+  const int X = dims[0], Y = dims[1];
+  const int64_t slice = (int64_t)X * Y;
+  auto idx = [&](int x, int y, int z) { return (int64_t)x + (int64_t)y * X + (int64_t)z * slice; };
+  const V3 t = {aff->t[0], aff->t[1], aff->t[2]};
+  int64_t n = 0;
+  const int a0 = (zlo / 8) * 8;
+  for (int c0 = a0; c0 < zhi; c0 += 8)
+    for (int ty = 0; ty < Y / 8; ++ty)
+      for (int tx = 0; tx < X / 8; ++tx)
+        for (int z = std::max(zlo, c0); z < std::min(zhi, c0 + 8); ++z)
+          for (int yy = 0; yy < 8; ++yy)
+            for (int xx = 0; xx < 8; ++xx) {
+              const int x = tx * 8 + xx, y = ty * 8 + yy;
+              const int W = weight[idx(x, y, z)];
+              const float F = (float)tsdf[idx(x, y, z)] * kDivShortMax;
+              if (W == 0 || F == 1.f) continue;
+              const V3 V = {((float)x + 0.5f) * vs[0], ((float)y + 0.5f) * vs[1],
+                            ((float)z + 0.5f) * vs[2]};
+              for (int axis = 0; axis < 3; ++axis) {
+                if (axis == 0 && x + 1 >= X) continue;
+                if (axis == 1 && y + 1 >= Y) continue;
+                const int64_t j = idx(x + (axis == 0), y + (axis == 1), z + (axis == 2));
+                const int Wn = weight[j];
+                const float Fn = (float)tsdf[j] * kDivShortMax;
+                if (Wn != 0 && Fn != 1.f && ((F > 0 && Fn < 0) || (F < 0 && Fn > 0))) {
+                  V3 p = V;
+                  const float Va = axis == 0 ? V.x : (axis == 1 ? V.y : V.z);
+                  const float Vn = Va + vs[axis];
+                  const float d_inv = 1.f / (std::fabs(F) + std::fabs(Fn));
+                  const float cc = (Va * std::fabs(Fn) + Vn * std::fabs(F)) * d_inv;
+                  if (axis == 0) p.x = cc;
+                  else if (axis == 1) p.y = cc;
+                  else p.z = cc;
+                  if (n < cap) st3(out, n, add(rmul(aff->R, p), t));
+                  ++n;
+                }
+              }
+            }
+  return n;
+}
+
 int kfo_format_pose(const kfx_pose *p, char *buf, int cap) {
   return std::snprintf(buf, cap,
                        "[%.8g, %.8g, %.8g, %.8g;\n %.8g, %.8g, %.8g, %.8g;\n %.8g, %.8g, "

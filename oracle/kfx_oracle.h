@@ -100,6 +100,12 @@ void kfo_raycast_slab(const int16_t *tsdf, const int dims[3], const float vs[3],
                       const float Rinv[9], int zb, int zn, int own0, int own1, float *vmap,
                       float *nmap, uint32_t *keys);
 
+/* FullScan6 point extraction (tsdf_volume.cu:307-481), canonical order; x-fastest
+ * volume; z in [zlo, zhi); writes min(cap, total) points, returns total. */
+int64_t kfo_extract_points(const int16_t *tsdf, const int16_t *weight, const int dims[3],
+                           const float vs[3], const kfx_pose *aff, int zlo, int zhi, float *out,
+                           int64_t cap);
+
 typedef struct kfo_pipe kfo_pipe;
 kfo_pipe *kfo_pipe_create(const kfx_intrinsics *intr, const kfx_params *p);
 void kfo_pipe_destroy(kfo_pipe *pp);

@@ -58,6 +58,9 @@ def lib():
                                   P(C.c_int32), C.c_int64]
         L.kfo_raycast_slab.argtypes = [P(C.c_int16), P(i), P(f), P(f), P(Intrinsics), P(Pose), P(f), i, i, i, i,
                                        P(f), P(f), P(C.c_uint32)]
+        L.kfo_extract_points.argtypes = [P(C.c_int16), P(C.c_int16), P(i), P(f), P(Pose), i, i, P(f),
+                                         C.c_int64]
+        L.kfo_extract_points.restype = C.c_int64
         L.kfo_pipe_create.argtypes = [P(Intrinsics), P(Params)]
         L.kfo_pipe_create.restype = C.c_void_p
         L.kfo_pipe_destroy.argtypes = [C.c_void_p]
@@ -242,11 +245,38 @@ def raycast_slab(tsdf: np.ndarray, vol: Volume, intr: Intrinsics, cam2vol: Pose,
 
 def slab_bounds(Z: int, rank: int, world: int, halo: int = 4):
     """(zb, zn, own0, own1) of slab `rank` (kfx_create_slab's partition)."""
-    own0, own1 = Z * rank // world, Z * (rank + 1) // world
+    def cut(r):
+        return Z if r >= world else (Z * r // world) // 8 * 8
+    own0, own1 = cut(rank), cut(rank + 1)
     if world == 1:
         return 0, Z, 0, Z
     zb = max(0, own0 - halo)
     return zb, min(Z, own1 + halo) - zb, own0, own1
+
+
+def extract_points(vol: Volume, vpose: Pose, zlo: int = 0, zhi: int | None = None, cap: int = 10_000_000,
+                   tsdf: np.ndarray | None = None, weight: np.ndarray | None = None):
+    """FullScan6 zero-crossing points (canonical order), (N, 3) float32, and the total."""
+    Z = int(vol.dims[2])
+    zhi = Z - 1 if zhi is None else zhi
+    t = np.ascontiguousarray(vol.tsdf if tsdf is None else tsdf, np.int16)
+    w = np.ascontiguousarray(vol.weight if weight is None else weight, np.int16)
+    n = lib().kfo_extract_points(i16ptr(t), i16ptr(w), vol.dims.ctypes.data_as(C.POINTER(C.c_int)),
+                                 fptr(vol.voxel_size), C.byref(vpose), zlo, zhi, None, 0)
+    m = min(n, cap)
+    out = np.zeros((m, 3), np.float32)
+    if m:
+        lib().kfo_extract_points(i16ptr(t), i16ptr(w), vol.dims.ctypes.data_as(C.POINTER(C.c_int)),
+                                 fptr(vol.voxel_size), C.byref(vpose), zlo, zhi, fptr(out), m)
+    return out, n
+
+
+def ply_text(xyz: np.ndarray) -> str:
+    """kinectfusion::savePointcloud (kinectfusion.cpp:148-166) text: ostream's
+    default float format is printf %g (6 significant digits)."""
+    head = ("ply\nformat ascii 1.0\nelement vertex %d\nproperty float x\nproperty float y\n"
+            "property float z\nend_header\n" % len(xyz))
+    return head + "".join("%g %g %g\n" % (float(a), float(b), float(c)) for a, b, c in xyz)
 
 
 def format_pose(p: Pose) -> str:

@@ -354,8 +354,11 @@ VolView make_vol(const kfx_params &p, int rank, int world) {
   v.X = p.volu_dims[0];
   v.Y = p.volu_dims[1];
   v.Z = p.volu_dims[2];
-  v.own0 = (int)((long long)v.Z * rank / world);
-  v.own1 = (int)((long long)v.Z * (rank + 1) / world);
+  // slab boundaries on multiples of 8 slices (the point-extraction chunk), so
+  // slab clouds concatenate to the single-volume cloud
+  auto cut = [&](int r) { return r >= world ? v.Z : (int)((long long)v.Z * r / world) / 8 * 8; };
+  v.own0 = cut(rank);
+  v.own1 = cut(rank + 1);
   if (world > 1) {
     v.zb = std::max(0, v.own0 - kSlabHalo);
     v.zn = std::min(v.Z, v.own1 + kSlabHalo) - v.zb;
@@ -470,8 +473,8 @@ int kfx_create(const kfx_intrinsics *intr, const kfx_params *params, int device,
 int kfx_create_slab(const kfx_intrinsics *intr, const kfx_params *params, int device, int rank,
                     int world, kfx_ctx **out) {
   if (world < 1 || rank < 0 || rank >= world) return set_err(KFX_ERR_ARG, "bad rank/world");
-  if (params && params->volu_dims[2] < 2 * world)
-    return set_err(KFX_ERR_ARG, "fewer than 2 slices per slab");
+  if (params && params->volu_dims[2] < 16 * world)
+    return set_err(KFX_ERR_ARG, "fewer than 16 slices per slab");
   return create_impl(intr, params, device, rank, world, true, out);
 }
 
@@ -1003,6 +1006,77 @@ int kfx_stage_raycast(kfx_ctx *c, const kfx_pose *cam2vol, const float Rinv[9]) 
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(c->stream));
   return KFX_OK;
+}
+
+// ---- point cloud / PLY -----------------------------------------------------
+
+int kfx_extract_points(kfx_ctx *c, float *xyz, int64_t cap, int64_t *n_points) {
+  int r = check_ctx(c);
+  if (r) return r;
+  if (cap < 0 || (cap > 0 && !xyz)) return set_err(KFX_ERR_ARG, "bad point buffer");
+  HIPCHK(hipStreamSynchronize(c->stream));
+  // FullScan6 visits z = 0 .. Z-2 (it reads z + 1); a slab its owned part
+  const int zlo = std::max(0, c->vol.own0), zhi = std::min(c->vol.own1, c->vol.Z - 1);
+  const size_t waves = extract_waves(c->vol, zlo, zhi);
+  int64_t total = 0;
+  if (waves > 0) {
+    const size_t nb = scan_blocks(waves);
+    char *ws = nullptr;
+    const size_t bytes = waves * 4 + waves * 8 + nb * 8 + 64;
+    HIPCHK(hipMalloc(&ws, bytes));
+    unsigned *counts = (unsigned *)ws;
+    unsigned long long *offsets = (unsigned long long *)(ws + ((waves * 4 + 7) & ~(size_t)7));
+    unsigned long long *bsum = offsets + waves;
+    unsigned long long *dtot = bsum + nb;
+    const DevPose vp = to_dev(c->p.volu_pose);
+    launch_extract(c->stream, c->vol, vp, zlo, zhi, counts, nullptr, nullptr, 0);
+    launch_scan(c->stream, counts, offsets, bsum, waves, dtot);
+    unsigned long long ht = 0;
+    hipError_t e = hipMemcpyAsync(&ht, dtot, 8, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    total = (int64_t)ht;
+    const int64_t n = std::min<int64_t>(total, cap);
+    float *dout = nullptr;
+    if (e == hipSuccess && n > 0) {
+      e = hipMalloc(&dout, (size_t)n * 12);
+      if (e == hipSuccess) {
+        launch_extract(c->stream, c->vol, vp, zlo, zhi, counts, offsets, dout,
+                       (unsigned long long)n);
+        e = hipMemcpyAsync(xyz, dout, (size_t)n * 12, hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        (void)hipFree(dout);
+      }
+    }
+    (void)hipFree(ws);
+    if (e != hipSuccess) return set_err(KFX_ERR_HIP, std::string("extract_points: ") + hipGetErrorString(e));
+  }
+  if (n_points) *n_points = total;
+  return KFX_OK;
+}
+
+int kfx_write_ply(const char *path, const float *xyz, int64_t n) {
+  if (!path || n < 0 || (n > 0 && !xyz)) return set_err(KFX_ERR_ARG, "bad argument");
+  FILE *f = std::fopen(path, "w");
+  if (!f) return set_err(KFX_ERR_ARG, std::string("cannot open ") + path);
+  // kinectfusion.cpp:154-165: ostream << float uses the default "%g" (6 digits)
+  std::fprintf(f, "ply\nformat ascii 1.0\nelement vertex %lld\nproperty float x\nproperty float y\n"
+               "property float z\nend_header\n", (long long)n);
+  for (int64_t i = 0; i < n; ++i)
+    std::fprintf(f, "%g %g %g\n", xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2]);
+  std::fclose(f);
+  return KFX_OK;
+}
+
+int kfx_save_pointcloud(kfx_ctx *c, const char *path, int64_t cap) {
+  if (!path) return set_err(KFX_ERR_ARG, "null path");
+  if (cap <= 0) cap = KFX_DEFAULT_CLOUD_POINTS;
+  int64_t total = 0;
+  int r = kfx_extract_points(c, nullptr, 0, &total);
+  if (r) return r;
+  const int64_t n = std::min(total, cap);
+  std::vector<float> pts((size_t)n * 3);
+  if (n > 0 && (r = kfx_extract_points(c, pts.data(), n, &total))) return r;
+  return kfx_write_ply(path, pts.data(), n);
 }
 
 // ---- Z-slab sharding -------------------------------------------------------

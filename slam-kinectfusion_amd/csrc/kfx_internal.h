@@ -145,6 +145,15 @@ constexpr int kMaxGroup = 16;
 void launch_group_reduce(hipStream_t s, uint32_t *const *in, int n_in, uint32_t *const *out,
                          int n_out, size_t count, bool is_max);
 void launch_inv_lambda(hipStream_t s, LevelGeom g0, float *inv_lambda);
+// point extraction (FullScan6) over global slices [zlo, zhi): offsets == null
+// counts points per wave, else writes them (float3) at offsets (< cap)
+size_t extract_waves(const VolView &v, int zlo, int zhi);
+void launch_extract(hipStream_t s, const VolView &v, DevPose vpose, int zlo, int zhi,
+                    unsigned *counts, const unsigned long long *offsets, float *out,
+                    unsigned long long cap);
+size_t scan_blocks(size_t n);  // bsum entries launch_scan needs (<= 65536)
+void launch_scan(hipStream_t s, const unsigned *counts, unsigned long long *offsets,
+                 unsigned long long *bsum, size_t n, unsigned long long *total);
 void launch_export_records(hipStream_t s, VolView v, int z0, int nz, uint64_t *dst);
 void launch_import_records(hipStream_t s, VolView v, int z0, int nz, const uint64_t *src);
 void launch_export_soa(hipStream_t s, VolView v, int z0, int nz, int16_t *t, int16_t *w,

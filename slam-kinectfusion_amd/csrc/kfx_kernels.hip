@@ -1599,6 +1599,147 @@ __global__ void k_group_reduce(GroupBufs in, GroupBufs out, size_t count, int is
   }
 }
 
+// ---------------------------------------------------------------------------
+// Point-cloud extraction — FullScan6 (tsdf_volume.cu:307-481): for every voxel
+// with W != 0 and F != 1 (A11: never 1), a zero crossing towards the +x, +y
+// and +z neighbour (W != 0, F != 1, opposite signs) gives the point
+// p = (V * |Fn| + Vn * |F|) / (|F| + |Fn|) along that edge, V the voxel
+// centre ((i + 0.5) * vs), transformed by the volume pose (R * p + t).
+//
+// The reference appends points with warp atomics (nondeterministic order, a
+// nondeterministic subset when the 10 M buffer fills).  Here the order is
+// canonical (D): wave = one 8x8 column tile x kExtractZ slices; points are
+// ordered by (slice chunk, tile, z, lane = (y&7)*8 + (x&7), edge x/y/z), so
+// the output and its first `cap` points are deterministic.  Pass 1 counts
+// per wave, a scan turns counts into offsets, pass 2 writes.
+constexpr int kExtractZ = 8;
+
+__device__ __forceinline__ int extract_voxel(const VolView &v, const DevPose &aff, int x, int y,
+                                             int z, f3 (&pts)[3]) {
+  const size_t i = vox_index(v, x, y, z);
+  const int W = v.weight[i];
+  const float F = (float)v.tsdf[i] * kDivShortMax;
+  if (W == 0 || F == 1.f) return 0;
+  const f3 V = {((float)x + 0.5f) * v.vs[0], ((float)y + 0.5f) * v.vs[1], ((float)z + 0.5f) * v.vs[2]};
+  const f3 t = {aff.t[0], aff.t[1], aff.t[2]};
+  int n = 0;
+  auto edge = [&](int axis, size_t j) {
+    const int Wn = v.weight[j];
+    const float Fn = (float)v.tsdf[j] * kDivShortMax;
+    if (Wn != 0 && Fn != 1.f && ((F > 0 && Fn < 0) || (F < 0 && Fn > 0))) {
+      f3 p = V;
+      const float Va = axis == 0 ? V.x : (axis == 1 ? V.y : V.z);
+      const float Vn = Va + v.vs[axis];
+      const float d_inv = 1.f / (fabsf(F) + fabsf(Fn));
+      const float c = (Va * fabsf(Fn) + Vn * fabsf(F)) * d_inv;
+      if (axis == 0) p.x = c;
+      else if (axis == 1) p.y = c;
+      else p.z = c;
+      pts[n++] = add(rmul(aff.R, p), t);
+    }
+  };
+  if (x + 1 < v.X) edge(0, vox_index(v, x + 1, y, z));
+  if (y + 1 < v.Y) edge(1, vox_index(v, x, y + 1, z));
+  edge(2, vox_index(v, x, y, z + 1));  // z + 1 < Z: guaranteed by the z range
+  return n;
+}
+
+// kEmit = false: counts[wave] = points of the wave; true: write them at
+// offsets[wave] + rank (rank < cap only).  z in [zlo, zhi) (global slices,
+// zhi <= Z - 1; a slab passes its owned range).
+template <bool kEmit>
+__global__ __launch_bounds__(256) void k_extract(VolView v, DevPose aff, int zlo, int zhi,
+                                                 unsigned *counts, const unsigned long long *offsets,
+                                                 float *out, unsigned long long cap) {
+  const int lane = threadIdx.x & 63;
+  const int ntiles = v.tiles_x * v.tiles_y;
+  const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (tile >= ntiles) return;
+  const size_t wave = (size_t)blockIdx.y * ntiles + tile;
+  const int x = (tile % v.tiles_x) * 8 + (lane & 7);
+  const int y = (tile / v.tiles_x) * 8 + (lane >> 3);
+  // chunks are aligned to global multiples of kExtractZ (slab boundaries are
+  // too), so concatenating slabs in rank order reproduces the single volume
+  const int c0 = (zlo / kExtractZ) * kExtractZ + (int)blockIdx.y * kExtractZ;
+  const int z0 = max(zlo, c0), z1 = min(zhi, c0 + kExtractZ);
+  unsigned long long base = kEmit ? offsets[wave] : 0ull;
+  unsigned total = 0;
+  const unsigned long long below = (1ull << lane) - 1ull;
+  for (int z = z0; z < z1; ++z) {
+    f3 pts[3];
+    const int n = extract_voxel(v, aff, x, y, z, pts);
+    const unsigned long long b1 = __ballot(n >= 1), b2 = __ballot(n >= 2), b3 = __ballot(n >= 3);
+    if (kEmit) {
+      const unsigned long long r = base + (unsigned long long)(__popcll(b1 & below) +
+                                                               __popcll(b2 & below) +
+                                                               __popcll(b3 & below));
+      for (int l = 0; l < n; ++l)
+        if (r + l < cap) st3(out, (size_t)(r + l), pts[l]);
+    }
+    const unsigned wt = (unsigned)(__popcll(b1) + __popcll(b2) + __popcll(b3));
+    base += wt;
+    total += wt;
+  }
+  if (!kEmit && lane == 0) counts[wave] = total;
+}
+
+// Exclusive scan of n u32 counts into u64 offsets (one 1024-thread block per
+// 4096 counts, then the block totals, then the fix-up); *total = the sum.
+__global__ __launch_bounds__(1024) void k_scan_local(const unsigned *in, unsigned long long *out,
+                                                     unsigned long long *bsum, size_t n) {
+  __shared__ unsigned long long s[1024];
+  const size_t b0 = (size_t)blockIdx.x * 4096 + threadIdx.x * 4;
+  unsigned long long v[4], acc = 0;
+  for (int k = 0; k < 4; ++k) {
+    v[k] = (b0 + k < n) ? in[b0 + k] : 0ull;
+    acc += v[k];
+  }
+  s[threadIdx.x] = acc;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {  // Hillis-Steele inclusive scan
+    const unsigned long long t = threadIdx.x >= off ? s[threadIdx.x - off] : 0ull;
+    __syncthreads();
+    s[threadIdx.x] += t;
+    __syncthreads();
+  }
+  unsigned long long run = s[threadIdx.x] - acc;
+  for (int k = 0; k < 4; ++k) {
+    if (b0 + k < n) out[b0 + k] = run;
+    run += v[k];
+  }
+  if (threadIdx.x == 1023) bsum[blockIdx.x] = s[1023];
+}
+__global__ __launch_bounds__(1024) void k_scan_blocks(unsigned long long *bsum, int nb,
+                                                      unsigned long long *total) {
+  // nb <= 1024 * 64: each thread scans a contiguous run, then one block scan
+  __shared__ unsigned long long s[1024];
+  const int per = (nb + 1023) / 1024;
+  const int b0 = threadIdx.x * per;
+  unsigned long long acc = 0;
+  for (int k = 0; k < per; ++k)
+    if (b0 + k < nb) acc += bsum[b0 + k];
+  s[threadIdx.x] = acc;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {
+    const unsigned long long t = threadIdx.x >= off ? s[threadIdx.x - off] : 0ull;
+    __syncthreads();
+    s[threadIdx.x] += t;
+    __syncthreads();
+  }
+  unsigned long long run = s[threadIdx.x] - acc;
+  for (int k = 0; k < per; ++k)
+    if (b0 + k < nb) {
+      const unsigned long long c = bsum[b0 + k];
+      bsum[b0 + k] = run;
+      run += c;
+    }
+  if (threadIdx.x == 1023) *total = s[1023];
+}
+__global__ void k_scan_add(unsigned long long *out, const unsigned long long *bsum, size_t n) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] += bsum[i / 4096];
+}
+
 __global__ void k_inv_lambda(LevelGeom g, float *out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= g.w * g.h) return;
@@ -1828,6 +1969,37 @@ void launch_group_reduce(hipStream_t s, uint32_t *const *in, int n_in, uint32_t 
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(k_group_reduce, dim3((unsigned)blocks), dim3(256), 0, s, a, b, count,
                      is_max ? 1 : 0);
+}
+
+static int extract_chunks(int zlo, int zhi) {
+  if (zhi <= zlo) return 0;
+  const int a = (zlo / kExtractZ) * kExtractZ;
+  return (zhi - a + kExtractZ - 1) / kExtractZ;
+}
+size_t extract_waves(const VolView &v, int zlo, int zhi) {
+  return (size_t)v.tiles_x * v.tiles_y * (size_t)extract_chunks(zlo, zhi);
+}
+void launch_extract(hipStream_t s, const VolView &v, DevPose vpose, int zlo, int zhi,
+                    unsigned *counts, const unsigned long long *offsets, float *out,
+                    unsigned long long cap) {
+  const int nc = extract_chunks(zlo, zhi);
+  if (nc == 0) return;
+  const int tiles = v.tiles_x * v.tiles_y;
+  dim3 grd((tiles + 3) / 4, nc);
+  if (offsets)
+    hipLaunchKernelGGL(k_extract<true>, grd, dim3(256), 0, s, v, vpose, zlo, zhi, counts, offsets,
+                       out, cap);
+  else
+    hipLaunchKernelGGL(k_extract<false>, grd, dim3(256), 0, s, v, vpose, zlo, zhi, counts, offsets,
+                       out, cap);
+}
+size_t scan_blocks(size_t n) { return (n + 4095) / 4096; }
+void launch_scan(hipStream_t s, const unsigned *counts, unsigned long long *offsets,
+                 unsigned long long *bsum, size_t n, unsigned long long *total) {
+  const size_t nb = scan_blocks(n);
+  hipLaunchKernelGGL(k_scan_local, dim3((unsigned)nb), dim3(1024), 0, s, counts, offsets, bsum, n);
+  hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, s, bsum, (int)nb, total);
+  hipLaunchKernelGGL(k_scan_add, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, offsets, bsum, n);
 }
 
 void launch_inv_lambda(hipStream_t s, LevelGeom g0, float *inv_lambda) {

@@ -18,7 +18,7 @@ import numpy as np
 from .abi import (KFX_FRAME_CUR, KFX_FRAME_PREV, KFX_OK, KFX_TRACKING_LOST, Intrinsics, Params, Pose,
                   default_params, fptr, i16ptr, i64ptr, u8ptr, u16ptr)
 
-__all__ = ["KinectFusion", "KfxError", "comm_unique_id", "pipeline_group", "lib", "build", "LIB_PATH", "Intrinsics", "Params", "Pose",
+__all__ = ["KinectFusion", "KfxError", "comm_unique_id", "pipeline_group", "write_ply", "lib", "build", "LIB_PATH", "Intrinsics", "Params", "Pose",
            "default_params", "KFX_FRAME_CUR", "KFX_FRAME_PREV", "KFX_OK", "KFX_TRACKING_LOST", "EXPORTS"]
 
 _PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -33,7 +33,7 @@ EXPORTS = [
     "kfx_upload_tsdf", "kfx_download_volume_soa", "kfx_stage_preprocess", "kfx_stage_icp_accumulate",
     "kfx_stage_icp", "kfx_stage_integrate", "kfx_stage_raycast", "kfx_set_profiling", "kfx_get_stage_ms",
     "kfx_integrate_counts", "kfx_create_slab", "kfx_slab_info", "kfx_comm_get_unique_id", "kfx_comm_init",
-    "kfx_pipeline_group",
+    "kfx_pipeline_group", "kfx_extract_points", "kfx_write_ply", "kfx_save_pointcloud",
 ]
 
 
@@ -96,6 +96,9 @@ def lib():
         "kfx_comm_get_unique_id": ([P(C.c_uint8)], i),
         "kfx_comm_init": ([vp, P(C.c_uint8)], i),
         "kfx_pipeline_group": ([P(vp), i, P(C.c_uint8), P(f)], i),
+        "kfx_extract_points": ([vp, P(f), C.c_int64, P(C.c_int64)], i),
+        "kfx_write_ply": ([C.c_char_p, P(f), C.c_int64], i),
+        "kfx_save_pointcloud": ([vp, C.c_char_p, C.c_int64], i),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -109,6 +112,12 @@ def _check(rc: int, what: str, ok=(KFX_OK,)) -> int:
     if rc not in ok:
         raise KfxError(f"{what} failed ({rc}): {lib().kfx_last_error().decode(errors='replace')}")
     return rc
+
+
+def write_ply(path: str, xyz: np.ndarray):
+    """kinectfusion::savePointcloud's ASCII PLY for an (N, 3) float32 array."""
+    xyz = np.ascontiguousarray(xyz, np.float32)
+    _check(lib().kfx_write_ply(path.encode(), fptr(xyz), xyz.shape[0]), "kfx_write_ply")
 
 
 def comm_unique_id() -> bytes:
@@ -244,6 +253,20 @@ class KinectFusion:
         a, b = C.c_int64(), C.c_int64()
         _check(lib().kfx_integrate_counts(self._h, C.byref(a), C.byref(b)), "kfx_integrate_counts")
         return a.value, b.value
+
+    # ---- point cloud (kinectfusion::extracePointcloud / savePointcloud) ---
+    def extract_points(self, cap: int = 10_000_000) -> np.ndarray:
+        """(N, 3) float32 zero-crossing points in world coordinates (canonical order)."""
+        n = C.c_int64()
+        _check(lib().kfx_extract_points(self._h, None, 0, C.byref(n)), "kfx_extract_points")
+        m = min(n.value, cap)
+        out = np.zeros((m, 3), np.float32)
+        if m:
+            _check(lib().kfx_extract_points(self._h, fptr(out), m, C.byref(n)), "kfx_extract_points")
+        return out
+
+    def save_pointcloud(self, path: str, cap: int = 0):
+        _check(lib().kfx_save_pointcloud(self._h, path.encode(), cap), "kfx_save_pointcloud")
 
     # ---- Z-slab sharding -------------------------------------------------
     def slab_info(self):

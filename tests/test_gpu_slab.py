@@ -13,6 +13,7 @@ import pytest
 
 from kfx import KFX_FRAME_PREV, KFX_OK, KFX_TRACKING_LOST, KinectFusion, comm_unique_id, pipeline_group, synth
 from kfx.abi import Intrinsics, default_params
+import oracle as O
 
 pytestmark = pytest.mark.gpu
 
@@ -71,7 +72,7 @@ def test_slab_group_matches_single_volume(world, seq_qvga):
     members = [KinectFusion(Intrinsics.from_any(intr), p, slab=(r, world)) for r in range(world)]
     for r, m in enumerate(members):
         zb, zn, o0, o1 = m.slab_info()
-        assert o0 == 64 * r // world and o1 == 64 * (r + 1) // world
+        assert (zb, zn, o0, o1) == O.slab_bounds(64, r, world)
         assert zb == max(0, o0 - 4) and zb + zn == min(64, o1 + 4)
     gst = [pipeline_group(members, bgr[k], dep[k].astype(np.float32)) for k in range(len(dep))]
     assert gst == st == [KFX_OK] * len(dep)

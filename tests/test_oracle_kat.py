@@ -307,3 +307,53 @@ def test_pose_text_format_matches_reference_artifact(oracle_lib, tmp_path):
         m = np.array(nums, dtype=np.float32).reshape(4, 4)
         out.append(oracle_lib.format_pose(Pose.from_matrix(m)))
     assert "".join(out) == ref
+
+
+def test_extract_points_plane(oracle_lib):
+    """FullScan6 (tsdf_volume.cu:307-481) on the integrated plane z = D: the +z
+    zero crossings of every observed column lie on the plane (world z = D,
+    since the volume pose is translate(-L/2, -L/2, 0.5) and the camera is at
+    the origin), within the tsdf quantisation."""
+    intr = Intrinsics(160, 120, 131.25, 131.25, 79.5, 59.5)
+    L, dims = 2.0, 64
+    p = plane_params(dims, L)
+    vol = oracle_lib.Volume((dims,) * 3, (L,) * 3)
+    D = 1.5
+    dmap = np.full((120, 160), D, np.float32)
+    bgr = np.zeros((120, 160, 3), np.uint8)
+    for _ in range(3):
+        oracle_lib.integrate(vol, p.volu_trun_dist, intr, p.volu_pose, dmap, bgr)
+    pts, n = oracle_lib.extract_points(vol, p.volu_pose)
+    assert n == len(pts) > 500
+    # integrate samples voxel z at z*vs, FullScan6 places it at (z + 0.5)*vs
+    # (SURVEY.md §8f): the crossings sit half a voxel beyond the plane
+    assert np.median(np.abs(pts[:, 2] - (D + 0.5 * L / dims))) < 0.25 * L / dims
+    # a capped call returns the prefix of the canonical order
+    pts2, n2 = oracle_lib.extract_points(vol, p.volu_pose, cap=100)
+    assert n2 == n and np.array_equal(pts2, pts[:100])
+    # slabs [0, 32) + [32, 63) concatenate to the full extraction
+    a, _ = oracle_lib.extract_points(vol, p.volu_pose, 0, 32)
+    b, _ = oracle_lib.extract_points(vol, p.volu_pose, 32, dims - 1)
+    assert np.array_equal(np.concatenate([a, b]), pts)
+
+
+def test_extract_points_needs_weight_and_sign_change(oracle_lib):
+    dims, L = 16, 1.0
+    vol = oracle_lib.Volume((dims,) * 3, (L,) * 3)
+    t = vol.tsdf.reshape(dims, dims, dims)
+    w = vol.weight.reshape(dims, dims, dims)
+    t[5, 5, 5], t[5, 5, 6] = 16383, -16383   # +x crossing at the midpoint
+    w[5, 5, 5] = w[5, 5, 6] = 1
+    pose = Pose.identity()
+    pts, n = oracle_lib.extract_points(vol, pose)
+    assert n == 1
+    vs = L / dims
+    np.testing.assert_allclose(pts[0], [6 * vs, 5.5 * vs, 5.5 * vs], rtol=0, atol=1e-6)
+    w[5, 5, 6] = 0  # unobserved neighbour: no point
+    assert oracle_lib.extract_points(vol, pose)[1] == 0
+
+
+def test_ply_text_format(oracle_lib):
+    txt = oracle_lib.ply_text(np.array([[0.1, -2.5, 1234567.0], [1e-7, 0.0, 3.0]], np.float32))
+    assert txt == ("ply\nformat ascii 1.0\nelement vertex 2\nproperty float x\nproperty float y\n"
+                   "property float z\nend_header\n0.1 -2.5 1.23457e+06\n1e-07 0 3\n")
