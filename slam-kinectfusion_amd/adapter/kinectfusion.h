@@ -14,8 +14,10 @@
 #include <opencv2/core.hpp>
 #include <opencv2/core/affine.hpp>
 
+#include <algorithm>
 #include <cmath>
 #include <fstream>
+#include <iostream>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -161,8 +163,22 @@ class kinectfusion {
       }
     return out;
   }
-  cv::Mat extracePointcloud();          // next: zero-crossing extraction (DESIGN.md §1 row f)
-  void savePointcloud(std::string path);  // next: ASCII PLY writer (kinectfusion.cpp:148-166)
+  // kinectfusion.cpp:142-147: 1 x N CV_32FC3 zero-crossing cloud (world frame),
+  // at most the reference's 10 M buffer (tsdf_volume.cpp:67)
+  cv::Mat extracePointcloud() {
+    int64_t n = 0;
+    if (kfx_extract_points(ctx_, nullptr, 0, &n) != KFX_OK) throw std::runtime_error(kfx_last_error());
+    n = std::min<int64_t>(n, KFX_DEFAULT_CLOUD_POINTS);
+    points_array_ = cv::Mat(1, (int)n, CV_32FC3);
+    if (n > 0 && kfx_extract_points(ctx_, points_array_.ptr<float>(), n, &n) != KFX_OK)
+      throw std::runtime_error(kfx_last_error());
+    return points_array_;
+  }
+  // kinectfusion.cpp:148-166: ASCII PLY of the last extracted cloud
+  void savePointcloud(std::string path) {
+    kfx_write_ply(path.c_str(), points_array_.empty() ? nullptr : points_array_.ptr<float>(),
+                  points_array_.cols);
+  }
   cv::Affine3f getCurCameraPose() { return pose_record.back(); }
   void release() {
     if (ctx_) kfx_destroy(ctx_);
@@ -186,6 +202,7 @@ class kinectfusion {
   }
 
   kfx_ctx *ctx_ = nullptr;
+  cv::Mat points_array_;
   Intrinsics intr_;
   kinectfuison_params params_;
 };
