@@ -55,7 +55,7 @@ def parse():
     ap.add_argument("--height", type=int, default=480)
     ap.add_argument("--unique", type=int, default=48, help="distinct frames rendered (played ping-pong)")
     ap.add_argument("--profile-frames", type=int, default=20)
-    ap.add_argument("--cpu-frames", type=int, default=3, help="oracle frames timed for cpu_baseline (0 = skip)")
+    ap.add_argument("--cpu-frames", type=int, default=8, help="oracle frames timed for cpu_baseline (0 = skip)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--mode", choices=["auto", "replicas", "slab"], default="auto")
     ap.add_argument("--zslab", type=int, default=1, help="with replicas at N>1: also time the Z-slab stream")
