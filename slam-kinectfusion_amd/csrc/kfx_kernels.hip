@@ -15,6 +15,9 @@
 #ifndef KFX_INT_KB
 #define KFX_INT_KB 4  // integrate: voxels per batch (loads in flight per lane)
 #endif
+#ifndef KFX_RAY_KR
+#define KFX_RAY_KR 16  // raycast: samples per batch (loads in flight per lane)
+#endif
 #ifndef KFX_SINCOS
 #define KFX_SINCOS 1
 #endif
@@ -1391,7 +1394,7 @@ __global__ __launch_bounds__(256) void k_raycast(VolView v, RayArgs ra, RayConst
     // 16-bit event mask with plain VALU math and only lanes with an event do
     // more work (a -/+ event ends the ray; a +/- event computes the normal
     // and, if it is NaN, the scan resumes at the next event).
-    constexpr int kR = 16;
+    constexpr int kR = KFX_RAY_KR;
     int sprev = isnan(tprev) ? 0 : (tprev > 0.f ? 1 : (tprev < 0.f ? -1 : 0));
     uint32_t kbase = 1u;  // loop sample index of the batch's first sample
     const RayMem<kIdx32> mem(v);
@@ -1400,10 +1403,22 @@ __global__ __launch_bounds__(256) void k_raycast(VolView v, RayArgs ra, RayConst
     const float hx = (float)(v.X - 2), hy = (float)(v.Y - 2), hz = (float)(v.Z - 2);
     const float szb = (float)v.zb, sze = (float)(v.zb + v.zn);
     const float so0 = (float)v.own0, so1 = (float)v.own1;
+    // Hit candidates (+/- events) are not resolved inside the march: a lane
+    // stops there, and once no lane of the wave is marching, all candidates
+    // compute their normals in ONE pass (6 trilinear interpolations, 48
+    // gathers).  A NaN normal (the reference keeps marching) resumes the march
+    // after the candidate sample from the saved state — same samples, same
+    // order, same result.
+    bool cand = false;
+    f3 cvert = {0.f, 0.f, 0.f}, r_nextp = nextp;
+    float r_rl = 0.f, r_tprev = 0.f;
+    uint32_t ckey = 0u, r_kbase = 0u;
+    while (__any(live || cand)) {
     while (__any(live)) {
       int16_t raw[kR];
       unsigned pm = 0u, nm = 0u, am = 0u, ownm = 0u;
       float rl = ray_len;
+      const f3 p0 = nextp;  // position before the batch's first sample
 #pragma unroll
       for (int j = 0; j < kR; ++j) {
         // a is monotone in j (rl only grows), so lanes past tfar or dead
@@ -1457,23 +1472,20 @@ __global__ __launch_bounds__(256) void k_raycast(VolView v, RayArgs ra, RayConst
               if (j < j0) rj += rc.step;
             }
             const float Ts = rj - (v.vs[0] * tc) / (tc - tn);  // A3 (R)
-            const f3 vertex = add(org, scl(dir, Ts));
-            const f3 n = compute_normal(v, rc, vertex);
-            if (!isnan(n.x * n.y * n.z)) {
-              // Rinv re-read from LDS here (volatile: not held in registers
-              // through the march)
-              float ri[9];
-              const volatile float *vr = s_rinv;
+            cvert = add(org, scl(dir, Ts));
+            cand = true;
+            ckey = kbase + (uint32_t)j0;
+            // resume state: sample j0 was processed, the next is j0 + 1
+            f3 pj = p0;
 #pragma unroll
-              for (int q = 0; q < 9; ++q) ri[q] = vr[q];
-              nout = rmul(ri, n);
-              vout = rmul(ri, sub(vertex, org));
-              live = false;
-              pend = 0u;
-              key = kbase + (uint32_t)j0;
-            } else {
-              pend &= ~(1u << j0);
-            }
+            for (int j = 0; j < kR; ++j)
+              if (j <= j0) pj = add(pj, vstep);
+            r_nextp = pj;
+            r_rl = rj + rc.step;
+            r_kbase = kbase + (uint32_t)j0 + 1u;
+            r_tprev = tn;
+            live = false;
+            pend = 0u;
           }
         }
       }
@@ -1487,6 +1499,29 @@ __global__ __launch_bounds__(256) void k_raycast(VolView v, RayArgs ra, RayConst
       }
       ray_len = rl;
       kbase += kR;
+    }
+    if (cand) {  // the wave's normal pass
+      cand = false;
+      const f3 n = compute_normal(v, rc, cvert);
+      if (!isnan(n.x * n.y * n.z)) {
+        // Rinv re-read from LDS here (volatile: not held in registers
+        // through the march)
+        float ri[9];
+        const volatile float *vr = s_rinv;
+#pragma unroll
+        for (int q = 0; q < 9; ++q) ri[q] = vr[q];
+        nout = rmul(ri, n);
+        vout = rmul(ri, sub(cvert, org));
+        key = ckey;
+      } else {  // NaN normal: keep marching after the candidate (tsdf_volume.cu:251)
+        live = true;
+        nextp = r_nextp;
+        ray_len = r_rl;
+        kbase = r_kbase;
+        sprev = -1;  // the candidate sample is negative (tsdf_next < 0)
+        tprev = r_tprev;
+      }
+    }
     }
   }
   if (inimg) {
