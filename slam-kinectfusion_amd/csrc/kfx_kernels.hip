@@ -1403,6 +1403,8 @@ __global__ __launch_bounds__(256) void k_raycast(VolView v, RayArgs ra, RayConst
     const float hx = (float)(v.X - 2), hy = (float)(v.Y - 2), hz = (float)(v.Z - 2);
     const float szb = (float)v.zb, sze = (float)(v.zb + v.zn);
     const float so0 = (float)v.own0, so1 = (float)v.own1;
+    const float fzlo = (float)max(1, kSlab ? v.zb : 1);
+    const float fzhi = (float)min(v.Z - 2, kSlab ? v.zb + v.zn - 1 : v.Z - 2);
     // Hit candidates (+/- events) are not resolved inside the march: a lane
     // stops there, and once no lane of the wave is marching, all candidates
     // compute their normals in ONE pass (6 trilinear interpolations, 48
@@ -1419,6 +1421,33 @@ __global__ __launch_bounds__(256) void k_raycast(VolView v, RayArgs ra, RayConst
       unsigned pm = 0u, nm = 0u, am = 0u, ownm = 0u;
       float rl = ray_len;
       const f3 p0 = nextp;  // position before the batch's first sample
+      // Interior batch: if the first and (estimated) last sample round into the
+      // valid (and stored) voxel box with a half-voxel margin and the batch ends
+      // before tfar, every sample of the batch is valid (positions are
+      // monotone per axis along the ray), so the per-sample checks drop out.
+      bool interior = !live;
+      if (live) {
+        const f3 ua = mulc(add(p0, vstep), rc.vs_inv);
+        const f3 ub = mulc(add(p0, scl(vstep, (float)kR)), rc.vs_inv);
+        interior = rl + (float)kR * rc.step < tfar && fminf(ua.x, ub.x) >= 1.f &&
+                   fmaxf(ua.x, ub.x) <= hx && fminf(ua.y, ub.y) >= 1.f && fmaxf(ua.y, ub.y) <= hy &&
+                   fminf(ua.z, ub.z) >= fzlo && fmaxf(ua.z, ub.z) <= fzhi;
+      }
+      if (kIdx32 && __all(interior)) {
+#pragma unroll
+        for (int j = 0; j < kR; ++j) {
+          nextp = add(nextp, vstep);
+          const float fx = rintf(nextp.x * rc.vs_inv.x);
+          const float fy = rintf(nextp.y * rc.vs_inv.y);
+          const float fz = rintf(nextp.z * rc.vs_inv.z);
+          if (kSlab) ownm |= ((fz >= so0) & (fz < so1)) ? (1u << j) : 0u;
+          raw[j] = mem.ld(live, (int)fx, (int)fy, (int)fz);  // dead lanes: no access, 0
+          pm |= raw[j] > 0 ? (1u << j) : 0u;
+          nm |= raw[j] < 0 ? (1u << j) : 0u;
+          rl = rl + rc.step;
+        }
+        am = (1u << kR) - 1u;
+      } else {
 #pragma unroll
       for (int j = 0; j < kR; ++j) {
         // a is monotone in j (rl only grows), so lanes past tfar or dead
@@ -1438,6 +1467,7 @@ __global__ __launch_bounds__(256) void k_raycast(VolView v, RayArgs ra, RayConst
         pm |= (val && raw[j] > 0) ? (1u << j) : 0u;
         nm |= (val && raw[j] < 0) ? (1u << j) : 0u;
         rl = rl + rc.step;
+      }
       }
       const int je = __builtin_ctz(~am);  // first sample outside [.., tfar) (kR if none)
       // an event at j needs opposite signs at samples j-1, j (tsdf_cur is the
