@@ -334,7 +334,8 @@ void kfo_pose_identity(kfx_pose *out) {
 }
 
 // icp_registration.cpp:33-42: A/b unpack (rigid_icp.cu:156-165), det check
-// (cv::determinant, LU), solve (D: LU with partial pivoting instead of SVD),
+// (cv::determinant, LU), solve (D: LU with partial pivoting and pivot
+// reciprocals instead of SVD),
 // Tinc = Affine3f(rvec, t) (OpenCV Rodrigues, float/double mix), pose*Tinc (A6).
 int kfo_icp_update(const int64_t sums[27], kfx_pose *pose, double x_out[6]) {
   double A[6][6], b[6];
@@ -348,6 +349,7 @@ int kfo_icp_update(const int64_t sums[27], kfx_pose *pose, double x_out[6]) {
         A[i][j] = A[j][i] = v;
     }
   int sign = 1;
+  double rdiag[6];
   for (int k = 0; k < 6; ++k) {
     int p = k;
     double best = std::fabs(A[k][k]);
@@ -367,9 +369,10 @@ int kfo_icp_update(const int64_t sums[27], kfx_pose *pose, double x_out[6]) {
       b[p] = tb;
       sign = -sign;
     }
+    rdiag[k] = 1.0 / A[k][k];  // pivot reciprocal (D: multiplied, one division per step)
     if (A[k][k] != 0.0) {
       for (int i = k + 1; i < 6; ++i) {
-        const double f = A[i][k] / A[k][k];
+        const double f = A[i][k] * rdiag[k];
         for (int j = k + 1; j < 6; ++j) A[i][j] = A[i][j] - f * A[k][j];
         b[i] = b[i] - f * b[k];
       }
@@ -382,7 +385,7 @@ int kfo_icp_update(const int64_t sums[27], kfx_pose *pose, double x_out[6]) {
   for (int i = 5; i >= 0; --i) {
     double acc = b[i];
     for (int j = i + 1; j < 6; ++j) acc = acc - A[i][j] * x[j];
-    x[i] = acc / A[i][i];
+    x[i] = acc * rdiag[i];
   }
   if (x_out)
     for (int i = 0; i < 6; ++i) x_out[i] = x[i];

@@ -746,7 +746,8 @@ __device__ __forceinline__ double bcast(double v, int src) {
 
 // icp_registration.cpp:33-42 on the device: A/b unpack (rigid_icp.cu:156-165),
 // partial-pivot LU with det check, LU solve (D: instead of SVD), Rodrigues,
-// pose = pose * Tinc.  Every lane runs the whole solve on its own registers
+// pose = pose * Tinc (the LU multiplies by pivot reciprocals, as the oracle
+// does).  Every lane runs the whole solve on its own registers
 // (identical, wave-uniform values: no cross-lane traffic on the critical
 // path); the pivot row is made uniform so the row swap is a scalar branch.
 // Each double operation is the oracle's (kfo_icp_update) in the same order,
@@ -767,6 +768,7 @@ __device__ int icp_update(const long long *sums, DevPose &pose, double *xo) {
       }
   }
   int sign = 1;
+  double rdiag[6];
 #pragma unroll
   for (int k = 0; k < 6; ++k) {
     int p = k;
@@ -793,10 +795,11 @@ __device__ int icp_update(const long long *sums, DevPose &pose, double *xo) {
         }
       sign = -sign;
     }
+    rdiag[k] = 1.0 / A[k][k];  // pivot reciprocal (D: one division per step)
     if (A[k][k] != 0.0) {
 #pragma unroll
       for (int i = k + 1; i < 6; ++i) {
-        const double f = A[i][k] / A[k][k];
+        const double f = A[i][k] * rdiag[k];
 #pragma unroll
         for (int j = k + 1; j < 7; ++j) A[i][j] = A[i][j] - f * A[k][j];
       }
@@ -812,7 +815,7 @@ __device__ int icp_update(const long long *sums, DevPose &pose, double *xo) {
     double acc = A[r][6];
 #pragma unroll
     for (int c = r + 1; c < 6; ++c) acc = acc - A[r][c] * x[c];
-    x[r] = acc / A[r][r];
+    x[r] = acc * rdiag[r];
   }
 #pragma unroll
   for (int r = 0; r < 6; ++r) xo[r] = x[r];
