@@ -57,6 +57,8 @@ def parse():
     ap.add_argument("--profile-frames", type=int, default=20)
     ap.add_argument("--cpu-frames", type=int, default=8, help="oracle frames timed for cpu_baseline (0 = skip)")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="single-stream frames (no preprocess/ICP overlap across frames)")
     ap.add_argument("--mode", choices=["auto", "replicas", "slab"], default="auto")
     ap.add_argument("--zslab", type=int, default=1, help="with replicas at N>1: also time the Z-slab stream")
     ap.add_argument("--zslab-timeout", type=float, default=240.0)
@@ -168,6 +170,7 @@ def zslab_stream(a, intr, params, D, rank, world, local):
     uid = D.bcast_bytes(kfx.comm_unique_id() if rank == 0 else None)
     kf.comm_init(uid)
     kf.set_graph_mode(not a.no_graph)
+    kf.set_frame_overlap(not a.no_overlap)
     kf.stage_frames(bgr, dep.astype(np.float32))
     for i in range(a.warmup):
         kf.pipeline_staged(order[i])
@@ -208,6 +211,7 @@ def main():
     else:
         kf = kfx.KinectFusion(Intrinsics.from_any(intr), params, device=local)
     kf.set_graph_mode(not a.no_graph)
+    kf.set_frame_overlap(not a.no_overlap)
     kf.stage_frames(bgr, dep.astype(np.float32))
 
     for i in range(a.warmup):
@@ -267,7 +271,7 @@ def main():
             "workload": f"C2: synthetic {W}x{H} depth+BGR, {a.dims}^3 TSDF @ "
                         f"{1000 * a.range / a.dims:.1f} mm, 3-level ICP {{10,5,4}}, full pipeline per frame",
             "width": W, "height": H, "volume_dims": a.dims, "volume_range_m": a.range,
-            "frames_unique": a.unique, "graph": not a.no_graph,
+            "frames_unique": a.unique, "graph": not a.no_graph, "overlap": not a.no_overlap,
             "parallelism": (f"zslab x{world}" if slab_main else
                             (f"replicas x{world} (independent streams)" if world > 1 else "single")),
             "tracked_frames": int(tracked),

@@ -109,6 +109,10 @@ int kfx_pipeline_staged(kfx_ctx *ctx, int frame_index);
 int kfx_synchronize(kfx_ctx *ctx);
 /* Use a captured hipGraph for the per-frame launch sequence (default on). */
 int kfx_set_graph_mode(kfx_ctx *ctx, int enabled);
+/* Overlap each staged frame's preprocess with the previous frame's tracking on
+ * a second stream, over double-buffered frame maps (default on; staged frames
+ * then launch eagerly instead of through graphs).  Results are identical. */
+int kfx_set_frame_overlap(kfx_ctx *ctx, int enabled);
 /* Run all ICP iterations of a frame as one persistent launch (default on; used
  * only when its grid fits co-resident on the device, else one launch per
  * iteration).  Returns 1 if the persistent kernel is usable on this context, 0

@@ -87,7 +87,18 @@ struct kfx_ctx {
   uint8_t *bgr = nullptr;
   FrameView cur{}, prev{};
   float *inv_lambda = nullptr;
-  float2 *dl0 = nullptr;  // level-0 {depth m, 1/lambda}, the integrate gather table
+  float2 *dl0 = nullptr;  // level-0 {depth m, 1/lambda}, the integrate gather table (+ dmax shards)
+  // cur maps, dl0 and the ICP plan over them are double-buffered: with frame
+  // overlap, frame k+1's preprocess (on pstream) fills one set while frame k's
+  // ICP / integrate / raycast (on stream) read the other.  cur/dl0/icp_plan
+  // above alias set `par`, the one the last frame used.
+  FrameView curb[2]{};
+  float2 *dl0b[2]{};
+  IcpPlan planb[2]{};
+  int par = 0;
+  bool overlap = true;
+  hipStream_t pstream = nullptr;
+  hipEvent_t ev_prep = nullptr, ev_free[2]{};
   VolView vol{};
   DevState *st = nullptr;
   DevPose *pose_log = nullptr;
@@ -143,6 +154,13 @@ int dalloc(kfx_ctx *c, void **p, size_t bytes) {
 
 size_t nvox(const kfx_ctx *c) { return c->vol.local_voxels(); }
 
+void set_par(kfx_ctx *c, int p) {
+  c->par = p;
+  c->cur = c->curb[p];
+  c->dl0 = c->dl0b[p];
+  c->icp_plan = c->planb[p];
+}
+
 void destroy_graphs(kfx_ctx *c) {
   for (auto &gx : c->graph)
     if (gx) {
@@ -168,6 +186,7 @@ struct FrameInput {
 // Slab contexts stop after their local raycast (enqueue_local) and then
 // combine the slabs' raycast results (enqueue_combine).
 void enqueue_local(kfx_ctx *c, FrameInput in, bool events);
+void enqueue_track(kfx_ctx *c, FrameInput in, bool events, bool begin);
 int enqueue_combine(kfx_ctx *c);
 
 int enqueue_frame(kfx_ctx *c, FrameInput in, bool events) {
@@ -209,20 +228,29 @@ void enqueue_local(kfx_ctx *c, FrameInput in, bool events) {
   for (int l = 0; l < kMaxLevels; ++l) raw[l] = c->raw[l];
   raw[0] = in.d32;
   if (c->L > 1) {
-    launch_pyr_down(s, in.d32, in.d16, c->g[0].w, c->g[0].h, c->raw[1], c->st);
+    launch_pyr_down(s, in.d32, in.d16, c->g[0].w, c->g[0].h, c->raw[1], c->st, c->dl0);
     for (int l = 2; l < c->L; ++l)
-      launch_pyr_down(s, c->raw[l - 1], nullptr, c->g[l - 1].w, c->g[l - 1].h, c->raw[l], nullptr);
+      launch_pyr_down(s, c->raw[l - 1], nullptr, c->g[l - 1].w, c->g[l - 1].h, c->raw[l], nullptr,
+                      nullptr);
   } else {
-    launch_frame_begin(s, c->st);
+    launch_frame_begin(s, c->st, c->dl0, c->g[0]);
   }
   launch_preprocess_maps(s, c->L, raw, in.d16, c->g, c->cur, c->p.bfilter_kernel_size,
                          c->p.bfilter_color_sigma, c->p.bfilter_spatial_sigma, c->p.dfilter_dist,
-                         c->inv_lambda, c->dl0, c->st);
+                         c->inv_lambda, c->dl0);
   if (events) (void)hipEventRecord(c->ev[1], s);
+  enqueue_track(c, in, events, false);
+}
+
+// ICP, integrate and raycast of the frame whose maps are in the current set;
+// begin: the frame's frame_begin has not run yet (overlapped frames)
+void enqueue_track(kfx_ctx *c, FrameInput in, bool events, bool begin) {
+  hipStream_t s = c->stream;
   // ICPRegistration::rigidTransform (icp_registration.cpp:16-46)
   if (c->icp_persistent && c->icp_persistent_enabled) {
-    launch_icp_track(s, c->icp_plan, c->st, c->icp_sync);
+    launch_icp_track(s, c->icp_plan, c->st, c->icp_sync, begin ? 1 : 0);  // folds frame_begin in
   } else {
+    if (begin) launch_frame_begin(s, c->st, nullptr, c->g[0]);
     for (int level = c->L - 1; level >= 0; --level) {
       for (int it = 0; it < c->p.icp_iter_count[level]; ++it)
         launch_icp(s, c->g[level], c->cur.v[level], c->cur.n[level], c->prev.v[level],
@@ -236,6 +264,41 @@ void enqueue_local(kfx_ctx *c, FrameInput in, bool events) {
   if (events) (void)hipEventRecord(c->ev[3], s);
   launch_raycast(s, c->vol, c->L, c->g, c->cur, c->prev, c->st, c->pose_log,
                  to_dev(c->p.volu_pose), nullptr, c->slab ? c->key_local : nullptr);
+}
+
+// Frame overlap: the preprocess of this frame runs on pstream into the set the
+// previous frame is not using, concurrently with the previous frame's ICP
+// (which occupies few CUs), so the per-frame critical path is ICP (with
+// frame_begin folded in) + integrate + raycast.  Measured cost of the two
+// cross-stream dependencies: ~9 us/frame for the wait on ev_prep, while
+// dropping the ev_free ordering (unsafe) is slower, as preprocess then
+// competes with integrate/raycast.
+int enqueue_frame_overlap(kfx_ctx *c, FrameInput in) {
+  const int p = c->par ^ 1;
+  set_par(c, p);
+  hipStream_t b = c->pstream;
+  HIPCHK(hipStreamWaitEvent(b, c->ev_free[p], 0));  // the frame before last is done with set p
+  const float *raw[kMaxLevels];
+  for (int l = 0; l < kMaxLevels; ++l) raw[l] = c->raw[l];
+  raw[0] = in.d32;
+  if (c->L > 1) {
+    launch_pyr_down(b, in.d32, in.d16, c->g[0].w, c->g[0].h, c->raw[1], nullptr, c->dl0);
+    for (int l = 2; l < c->L; ++l)
+      launch_pyr_down(b, c->raw[l - 1], nullptr, c->g[l - 1].w, c->g[l - 1].h, c->raw[l], nullptr,
+                      nullptr);
+  } else {
+    launch_frame_begin(b, nullptr, c->dl0, c->g[0]);
+  }
+  launch_preprocess_maps(b, c->L, raw, in.d16, c->g, c->cur, c->p.bfilter_kernel_size,
+                         c->p.bfilter_color_sigma, c->p.bfilter_spatial_sigma, c->p.dfilter_dist,
+                         c->inv_lambda, c->dl0);
+  HIPCHK(hipEventRecord(c->ev_prep, b));
+  HIPCHK(hipStreamWaitEvent(c->stream, c->ev_prep, 0));
+  enqueue_track(c, in, false, true);
+  int r = KFX_OK;
+  if (c->slab) r = enqueue_combine(c);
+  HIPCHK(hipEventRecord(c->ev_free[p], c->stream));
+  return r;
 }
 
 int build_graph(kfx_ctx *c, FrameInput in, hipGraphExec_t *out) {
@@ -310,10 +373,18 @@ int ensure_graph(kfx_ctx *c, FrameInput in, hipGraphExec_t *graph) {
 }
 
 // graph: the cached executable for this input (built on first use), or null
-int run_frame(kfx_ctx *c, FrameInput in, hipGraphExec_t *graph) {
+// overlap: the input stays valid until the frame completes (staged frames)
+int run_frame(kfx_ctx *c, FrameInput in, hipGraphExec_t *graph, bool overlap = false) {
   int r = ensure_pose_capacity(c, 1);
   if (r) return r;
   c->last_bgr = in.bgr;
+  if (overlap && c->overlap && !c->profiling) {
+    if ((r = enqueue_frame_overlap(c, in))) return r;
+    HIPCHK(hipGetLastError());
+    c->pending += 1;
+    return KFX_OK;
+  }
+  set_par(c, 0);  // single-stream frames (and their graphs) use set 0
   if (c->profiling) {
     if ((r = enqueue_frame(c, in, true))) return r;
     HIPCHK(hipGetLastError());
@@ -400,7 +471,7 @@ int do_reset(kfx_ctx *c) {
   HIPCHK(hipMemsetAsync(c->vol.rgb, 0, n * sizeof(uint32_t), c->stream));
   for (int l = 0; l < c->L; ++l) {
     const size_t np = (size_t)c->g[l].w * c->g[l].h;
-    for (FrameView *f : {&c->cur, &c->prev}) {
+    for (FrameView *f : {&c->curb[0], &c->curb[1], &c->prev}) {
       if (f->d[l]) HIPCHK(hipMemsetAsync(f->d[l], 0, np * 4, c->stream));
       HIPCHK(hipMemsetAsync(f->v[l], 0, np * 12, c->stream));
       HIPCHK(hipMemsetAsync(f->n[l], 0, np * 12, c->stream));
@@ -416,6 +487,7 @@ int do_reset(kfx_ctx *c) {
   HIPCHK(hipMemcpyAsync(c->st, &s, sizeof(s), hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipMemcpyAsync(c->pose_log, &I, sizeof(I), hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
+  set_par(c, 0);
   c->pending = 0;
   c->known_poses = 1;
   return KFX_OK;
@@ -529,13 +601,21 @@ static int create_impl(const kfx_intrinsics *intr, const kfx_params *params, int
     return fail(set_err(KFX_ERR_HIP, "hipStreamCreate failed"));
   for (auto &e : c->ev)
     if (hipEventCreate(&e) != hipSuccess) return fail(set_err(KFX_ERR_HIP, "hipEventCreate failed"));
+  if (hipStreamCreateWithFlags(&c->pstream, hipStreamNonBlocking) != hipSuccess)
+    return fail(set_err(KFX_ERR_HIP, "hipStreamCreate failed"));
+  // cross-stream ordering on one device: a device-scope release suffices
+  for (hipEvent_t *e : {&c->ev_prep, &c->ev_free[0], &c->ev_free[1]})
+    if (hipEventCreateWithFlags(e, hipEventDisableTiming | hipEventReleaseToDevice) != hipSuccess)
+      return fail(set_err(KFX_ERR_HIP, "hipEventCreate failed"));
 
   for (int l = 0; l < c->L; ++l) {
     const size_t np = (size_t)c->g[l].w * c->g[l].h;
     if ((r = dalloc(c, (void **)&c->raw[l], np * 4))) return fail(r);
-    if ((r = dalloc(c, (void **)&c->cur.d[l], np * 4))) return fail(r);
-    if ((r = dalloc(c, (void **)&c->cur.v[l], np * 12))) return fail(r);
-    if ((r = dalloc(c, (void **)&c->cur.n[l], np * 12))) return fail(r);
+    for (FrameView &f : c->curb) {
+      if ((r = dalloc(c, (void **)&f.d[l], np * 4))) return fail(r);
+      if ((r = dalloc(c, (void **)&f.v[l], np * 12))) return fail(r);
+      if ((r = dalloc(c, (void **)&f.n[l], np * 12))) return fail(r);
+    }
     // prev vmap|nmap of a level are one buffer (one collective in the slab combine)
     if ((r = dalloc(c, (void **)&c->prev.v[l], np * 24))) return fail(r);
     c->prev.n[l] = c->prev.v[l] + 3 * np;
@@ -548,7 +628,8 @@ static int create_impl(const kfx_intrinsics *intr, const kfx_params *params, int
   if ((r = dalloc(c, (void **)&c->raw0_u16, np0 * 2))) return fail(r);
   if ((r = dalloc(c, (void **)&c->bgr, np0 * 3))) return fail(r);
   if ((r = dalloc(c, (void **)&c->inv_lambda, np0 * 4))) return fail(r);
-  if ((r = dalloc(c, (void **)&c->dl0, np0 * 8))) return fail(r);
+  for (float2 *&d : c->dl0b)
+    if ((r = dalloc(c, (void **)&d, np0 * 8 + 64))) return fail(r);
   c->vol = make_vol(p, rank, world);
   const size_t n = nvox(c);
   if ((r = dalloc(c, (void **)&c->vol.tsdf, n * 2))) return fail(r);
@@ -561,8 +642,10 @@ static int create_impl(const kfx_intrinsics *intr, const kfx_params *params, int
     return fail(r);
   c->icp_ticket = reinterpret_cast<unsigned *>(c->icp_shards + 8 * 27);
   if ((r = dalloc(c, (void **)&c->icp_sync, sizeof(IcpSync)))) return fail(r);
-  c->icp_plan = make_icp_plan(c->L, c->g, c->p.icp_iter_count, c->cur, c->prev,
-                              c->p.icp_dist_threshold, c->angle_thr);
+  for (int b = 0; b < 2; ++b)
+    c->planb[b] = make_icp_plan(c->L, c->g, c->p.icp_iter_count, c->curb[b], c->prev,
+                                c->p.icp_dist_threshold, c->angle_thr);
+  set_par(c, 0);
   c->icp_persistent = icp_persistent_ok(c->icp_plan, c->device);
   if ((r = dalloc(c, (void **)&c->counters, sizeof(unsigned long long) * 32))) return fail(r);
   if ((r = dalloc(c, (void **)&c->xpose, sizeof(float) * 32))) return fail(r);
@@ -576,11 +659,15 @@ int kfx_destroy(kfx_ctx *c) {
   if (!c) return KFX_OK;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->pstream) (void)hipStreamSynchronize(c->pstream);
   destroy_graphs(c);
   if (c->comm) (void)ncclCommDestroy(c->comm);
   for (void *a : c->allocs) (void)hipFree(a);
   for (auto &e : c->ev)
     if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t e : {c->ev_prep, c->ev_free[0], c->ev_free[1]})
+    if (e) (void)hipEventDestroy(e);
+  if (c->pstream) (void)hipStreamDestroy(c->pstream);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return KFX_OK;
@@ -639,7 +726,8 @@ int kfx_stage_frames(kfx_ctx *c, int n, const uint8_t *bgr, const float *depth_m
   HIPCHK(hipStreamSynchronize(c->stream));
   c->n_staged = n;
   // capture every staged frame's graph now, outside any timed frame loop
-  for (int i = 0; i < n; ++i)
+  // (overlapped frames launch eagerly on two streams and need none)
+  for (int i = 0; i < n && !c->overlap; ++i)
     if ((r = ensure_graph(c, {c->staged_depth + np * i, nullptr, c->staged_bgr + np * 3 * i},
                           &c->staged_graph[i])))
       return r;
@@ -653,13 +741,22 @@ int kfx_pipeline_staged(kfx_ctx *c, int idx) {
   const size_t np = (size_t)c->intr.width * c->intr.height;
   // the captured graph for this staged frame reads it in place (no copy)
   return run_frame(c, {c->staged_depth + np * idx, nullptr, c->staged_bgr + np * 3 * idx},
-                   &c->staged_graph[idx]);
+                   &c->staged_graph[idx], true);
 }
 
 int kfx_synchronize(kfx_ctx *c) {
   int r = check_ctx(c);
   if (r) return r;
   HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(hipStreamSynchronize(c->pstream));
+  return KFX_OK;
+}
+
+int kfx_set_frame_overlap(kfx_ctx *c, int enabled) {
+  int r = check_ctx(c);
+  if (r) return r;
+  HIPCHK(hipStreamSynchronize(c->stream));
+  c->overlap = enabled != 0;
   return KFX_OK;
 }
 
@@ -885,15 +982,13 @@ int kfx_stage_preprocess(kfx_ctx *c, const uint8_t *bgr, const float *depth_mm) 
   HIPCHK(hipMemcpyAsync(c->raw[0], depth_mm, np * 4, hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipMemcpyAsync(c->bgr, bgr, np * 3, hipMemcpyHostToDevice, c->stream));
   c->last_bgr = c->bgr;
-  HIPCHK(hipMemsetAsync(reinterpret_cast<char *>(c->st) + offsetof(DevState, dmax_bits), 0,
-                        sizeof(((DevState *)nullptr)->dmax_bits), c->stream));
+  HIPCHK(hipMemsetAsync(c->dl0 + np, 0, 64, c->stream));  // the max-depth shards
   for (int l = 1; l < c->L; ++l)
     launch_pyr_down(c->stream, c->raw[l - 1], nullptr, c->g[l - 1].w, c->g[l - 1].h, c->raw[l],
-                    nullptr);
+                    nullptr, nullptr);
   launch_preprocess_maps(c->stream, c->L, c->raw, nullptr, c->g, c->cur,
                          c->p.bfilter_kernel_size, c->p.bfilter_color_sigma,
-                         c->p.bfilter_spatial_sigma, c->p.dfilter_dist, c->inv_lambda, c->dl0,
-                         c->st);
+                         c->p.bfilter_spatial_sigma, c->p.dfilter_dist, c->inv_lambda, c->dl0);
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(c->stream));
   return KFX_OK;

@@ -28,7 +28,6 @@ struct DevState {
   int pose_overflow;
   int n_base;           // n_poses at frame start (read-only during the frame)
   int last_fail;        // 1 if the last frame hit the ICP det check (reset applied)
-  unsigned dmax_bits[16];  // max valid level-0 depth of this frame (float bits), sharded
   DevPose icp_pose;     // camera_pose inside rigidTransform
   long long sums[27];   // last ICP sums (test seam)
   double x[6];          // last ICP increment
@@ -100,21 +99,23 @@ struct FrameView {
 };
 
 // ---- launchers (kfx_kernels.hip) -----------------------------------------
-void launch_frame_begin(hipStream_t s, DevState *st);
+// dl0: zero the frame's max-depth shards stored after that level-0 table
+void launch_frame_begin(hipStream_t s, DevState *st, float2 *dl0, LevelGeom g0);
 void launch_pyr_down(hipStream_t s, const float *src, const uint16_t *src16, int w, int h,
-                     float *dst, DevState *st_begin);
+                     float *dst, DevState *st_begin, float2 *dl0);
 // bilateral + truncation + vertex + normal maps, all levels (raw[l] = raw mm)
 void launch_preprocess_maps(hipStream_t s, int levels, const float *const raw[kMaxLevels],
                             const uint16_t *raw0_u16, const LevelGeom *g, FrameView cur, int ksz,
                             float sigma_color, float sigma_spatial, float max_dist,
-                            const float *inv_lambda, float2 *dl0, DevState *st);
+                            const float *inv_lambda, float2 *dl0);
 int icp_blocks(const LevelGeom &g);
 // one ICP iteration (rigid_icp.cu:135-169 + icp_registration.cpp:33-42) in a
 // single launch; shards = 8 x 27 int64 zeroed, ticket zeroed (both self-reset)
 IcpPlan make_icp_plan(int levels, const LevelGeom *g, const int *iters, FrameView cur,
                       FrameView prev, float dist_thr, float angle_thr);
 bool icp_persistent_ok(const IcpPlan &pl, int device);  // grid co-resident + slots fit
-void launch_icp_track(hipStream_t s, const IcpPlan &pl, DevState *st, IcpSync *sync);
+// begin: run the frame's frame_begin inside the launch (no separate kernel)
+void launch_icp_track(hipStream_t s, const IcpPlan &pl, DevState *st, IcpSync *sync, int begin = 0);
 void launch_icp(hipStream_t s, const LevelGeom &g, const float *cv, const float *cn,
                 const float *pv, const float *pn, float dist_thr, float angle_thr, DevState *st,
                 unsigned long long *shards, unsigned *ticket, int force, int update);

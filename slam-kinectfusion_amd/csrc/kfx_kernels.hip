@@ -156,7 +156,10 @@ __device__ __forceinline__ void frame_begin(DevState *st) {
   st->icp_fail = 0;
   st->n_base = st->n_poses;
   st->icp_pose = pose_identity();
-  for (int i = 0; i < kDmaxShards; ++i) st->dmax_bits[i] = 0u;
+}
+// the frame's max-depth shards live after the level-0 dl table (one per cur buffer)
+__device__ __forceinline__ unsigned *dmax_shards(const float2 *dl0, const LevelGeom &g0) {
+  return (unsigned *)(const_cast<float2 *>(dl0) + (size_t)g0.w * g0.h);
 }
 
 // z is the global slice; the view stores slices [zb, zb+zn)
@@ -195,17 +198,23 @@ LevelTiles make_tiles(int levels, const LevelGeom *g) {
 // ---------------------------------------------------------------------------
 // Preprocess
 
-__global__ void k_frame_begin(DevState *st) { frame_begin(st); }
+__global__ void k_frame_begin(DevState *st, unsigned *dmax) {
+  if (st) frame_begin(st);
+  if (dmax)
+    for (int i = 0; i < kDmaxShards; ++i) dmax[i] = 0u;
+}
 
 // cv::cuda::pyrDown (kinectfusion.cpp:54-55; OpenCV pyr_down.cu): vertical
 // 5-tap at src row 2y for the 5 source columns, then horizontal 5-tap.
 template <typename T>
 __global__ __launch_bounds__(256) void k_pyr_down(const T *__restrict__ src, int w, int h,
                                                   float *__restrict__ dst, int dw, int dh,
-                                                  DevState *st) {
-  if (st != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 &&
-      threadIdx.y == 0)
-    frame_begin(st);
+                                                  DevState *st, unsigned *dmax) {
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && threadIdx.y == 0) {
+    if (st) frame_begin(st);
+    if (dmax)
+      for (int i = 0; i < kDmaxShards; ++i) dmax[i] = 0u;
+  }
   const int x = blockIdx.x * blockDim.x + threadIdx.x;
   const int y = blockIdx.y * blockDim.y + threadIdx.y;
   if (x >= dw || y >= dh) return;
@@ -258,7 +267,7 @@ struct BilatArgs {
 // Level 0 also reduces the frame's max depth (conservative integrate bound).
 constexpr int kPreMaxR = 7;                    // ksz <= 15
 constexpr int kPreRaw = 16 + 2 * (kPreMaxR + 1);  // 32
-__global__ __launch_bounds__(256) void k_preprocess_maps(BilatArgs a, DevState *st) {
+__global__ __launch_bounds__(256) void k_preprocess_maps(BilatArgs a) {
   const int l = find_level(a.t, blockIdx.x);
   const int local = blockIdx.x - a.t.off[l];
   const LevelGeom g = a.t.g[l];
@@ -343,7 +352,7 @@ __global__ __launch_bounds__(256) void k_preprocess_maps(BilatArgs a, DevState *
     __syncthreads();
     if (threadIdx.x == 0) {
       const unsigned b = max(max(wm[0], wm[1]), max(wm[2], wm[3]));
-      if (b) atomicMax(&st->dmax_bits[blockIdx.x % kDmaxShards], b);
+      if (b) atomicMax(&dmax_shards(a.dl0, a.t.g[0])[blockIdx.x % kDmaxShards], b);
     }
   }
 }
@@ -601,14 +610,24 @@ __global__ __launch_bounds__(256) void k_icp_acc(LevelGeom g, int xe, int npix,
 // broadcast step).  Current-frame maps stay in registers across a level's
 // iterations.  A wall-clock watchdog turns a stalled barrier into a reported
 // error instead of a hang.
+// begin: the frame's frame_begin is folded in (overlapped frames): every block
+// derives the begun state itself and block 0's thread 0, the only writer of
+// these fields during the kernel, stores it first
 __global__ __launch_bounds__(256, 2) void k_icp_track(IcpPlan pl, DevState *__restrict__ st,
-                                                   IcpSync *__restrict__ sy) {
-  if (st->mode != MODE_TRACK || st->icp_fail) return;  // uniform across the grid
+                                                   IcpSync *__restrict__ sy, int begin) {
+  DevPose P;
+  if (begin) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) frame_begin(st);
+    if (st->frame_count == 1) return;  // MODE_BOOT
+    P = pose_identity();
+  } else {
+    if (st->mode != MODE_TRACK || st->icp_fail) return;  // uniform across the grid
+    P = st->icp_pose;
+  }
   __shared__ IcpRed red;
   __shared__ long long sums[27];
   __shared__ DevPose spose;
   __shared__ int sfail, sstall;
-  DevPose P = st->icp_pose;
   int fail = 0;
   unsigned target = 0;
   int slot = 0;
@@ -1081,8 +1100,9 @@ __global__ __launch_bounds__(256) void k_integrate(VolView v, LevelGeom g,
 
   // conservative interval [zlo, zhi] of z where any check can pass
   unsigned dm = 0u;
+  const unsigned *dmx = dmax_shards(dl, g);
 #pragma unroll
-  for (int i = 0; i < kDmaxShards; ++i) dm = max(dm, st->dmax_bits[i]);
+  for (int i = 0; i < kDmaxShards; ++i) dm = max(dm, dmx[i]);
   const float dmax = __uint_as_float(dm);
   // global z = 1..Z-1 (tsdf_volume.cu:53), restricted to the stored slab
   double lo = (double)max(1, v.zb), hi = (double)min(v.Z - 1, v.zb + v.zn - 1);
@@ -1867,24 +1887,26 @@ __global__ void k_export_soa(VolView v, int z0, int nz, int16_t *t, int16_t *w, 
 // ---------------------------------------------------------------------------
 // launchers
 
-void launch_frame_begin(hipStream_t s, DevState *st) {
-  hipLaunchKernelGGL(k_frame_begin, dim3(1), dim3(1), 0, s, st);
+void launch_frame_begin(hipStream_t s, DevState *st, float2 *dl0, LevelGeom g0) {
+  hipLaunchKernelGGL(k_frame_begin, dim3(1), dim3(1), 0, s, st,
+                     dl0 ? (unsigned *)(dl0 + (size_t)g0.w * g0.h) : nullptr);
 }
 
 void launch_pyr_down(hipStream_t s, const float *src, const uint16_t *src16, int w, int h,
-                     float *dst, DevState *st_begin) {
+                     float *dst, DevState *st_begin, float2 *dl0) {
+  unsigned *dmax = dl0 ? (unsigned *)(dl0 + (size_t)w * h) : nullptr;  // level-0 source dims
   const int dw = (w + 1) / 2, dh = (h + 1) / 2;
   dim3 blk(64, 4), grd((dw + 63) / 64, (dh + 3) / 4);
   if (src16)
-    hipLaunchKernelGGL(k_pyr_down<uint16_t>, grd, blk, 0, s, src16, w, h, dst, dw, dh, st_begin);
+    hipLaunchKernelGGL(k_pyr_down<uint16_t>, grd, blk, 0, s, src16, w, h, dst, dw, dh, st_begin, dmax);
   else
-    hipLaunchKernelGGL(k_pyr_down<float>, grd, blk, 0, s, src, w, h, dst, dw, dh, st_begin);
+    hipLaunchKernelGGL(k_pyr_down<float>, grd, blk, 0, s, src, w, h, dst, dw, dh, st_begin, dmax);
 }
 
 void launch_preprocess_maps(hipStream_t s, int levels, const float *const raw[kMaxLevels],
                             const uint16_t *raw0_u16, const LevelGeom *g, FrameView cur, int ksz,
                             float sigma_color, float sigma_spatial, float max_dist,
-                            const float *inv_lambda, float2 *dl0, DevState *st) {
+                            const float *inv_lambda, float2 *dl0) {
   BilatArgs a{};
   a.invl = inv_lambda;
   a.dl0 = dl0;
@@ -1900,7 +1922,7 @@ void launch_preprocess_maps(hipStream_t s, int levels, const float *const raw[kM
   a.s_half = -0.5f / (sigma_spatial * sigma_spatial);
   a.c_half = -0.5f / (sigma_color * sigma_color);
   a.max_dist = max_dist;
-  hipLaunchKernelGGL(k_preprocess_maps, dim3(a.t.off[levels]), dim3(256), 0, s, a, st);
+  hipLaunchKernelGGL(k_preprocess_maps, dim3(a.t.off[levels]), dim3(256), 0, s, a);
 }
 
 static int icp_npix(const LevelGeom &g, int *xe) {
@@ -1950,8 +1972,8 @@ bool icp_persistent_ok(const IcpPlan &pl, int device) {
   return (long long)per_cu * cus >= pl.nblocks;
 }
 
-void launch_icp_track(hipStream_t s, const IcpPlan &pl, DevState *st, IcpSync *sync) {
-  hipLaunchKernelGGL(k_icp_track, dim3(pl.nblocks), dim3(256), 0, s, pl, st, sync);
+void launch_icp_track(hipStream_t s, const IcpPlan &pl, DevState *st, IcpSync *sync, int begin) {
+  hipLaunchKernelGGL(k_icp_track, dim3(pl.nblocks), dim3(256), 0, s, pl, st, sync, begin);
 }
 
 void launch_icp(hipStream_t s, const LevelGeom &g, const float *cv, const float *cn,

@@ -28,7 +28,7 @@ LIB_PATH = os.environ.get("KFX_LIB_PATH") or os.path.join(_PKG, "lib", "libkfx.s
 EXPORTS = [
     "kfx_abi_version", "kfx_last_error", "kfx_default_params", "kfx_create", "kfx_destroy", "kfx_reset",
     "kfx_pipeline", "kfx_pipeline_u16", "kfx_stage_frames", "kfx_pipeline_staged", "kfx_synchronize",
-    "kfx_set_graph_mode", "kfx_set_icp_persistent", "kfx_get_icp_trace", "kfx_get_cur_camera_pose", "kfx_get_frame_count", "kfx_get_pose_record",
+    "kfx_set_graph_mode", "kfx_set_frame_overlap", "kfx_set_icp_persistent", "kfx_get_icp_trace", "kfx_get_cur_camera_pose", "kfx_get_frame_count", "kfx_get_pose_record",
     "kfx_write_poses_txt", "kfx_get_frame_maps", "kfx_set_frame_maps", "kfx_download_tsdf",
     "kfx_upload_tsdf", "kfx_download_volume_soa", "kfx_stage_preprocess", "kfx_stage_icp_accumulate",
     "kfx_stage_icp", "kfx_stage_integrate", "kfx_stage_raycast", "kfx_set_profiling", "kfx_get_stage_ms",
@@ -72,6 +72,7 @@ def lib():
         "kfx_pipeline_staged": ([vp, i], i),
         "kfx_synchronize": ([vp], i),
         "kfx_set_graph_mode": ([vp, i], i),
+        "kfx_set_frame_overlap": ([vp, i], i),
         "kfx_set_icp_persistent": ([vp, i], i),
         "kfx_get_icp_trace": ([vp, P(C.c_uint64), i], i),
         "kfx_get_cur_camera_pose": ([vp, P(Pose)], i),
@@ -226,6 +227,10 @@ class KinectFusion:
 
     def set_graph_mode(self, on: bool):
         _check(lib().kfx_set_graph_mode(self._h, int(on)), "kfx_set_graph_mode")
+
+    def set_frame_overlap(self, on: bool):
+        """Overlap staged frames' preprocess with the previous frame's tracking."""
+        _check(lib().kfx_set_frame_overlap(self._h, int(on)), "kfx_set_frame_overlap")
 
     def set_icp_persistent(self, on: bool) -> bool:
         """Toggle the one-launch persistent ICP kernel; returns whether it is usable here."""

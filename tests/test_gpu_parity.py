@@ -246,20 +246,30 @@ def test_pipeline_modes_and_inputs_identical(seq_qvga):
     bgr, dep, gt = seq_qvga
     intr = synth.Intrinsics.qvga()
     res = []
-    for mode in ("graph", "eager", "profile", "u16", "staged", "icp_per_iter"):
+    for mode in ("graph", "eager", "profile", "u16", "staged", "staged_graph", "staged_mixed",
+                 "staged_per_iter", "icp_per_iter"):
         kf, p = make(intr, dims=64)
+        if mode == "staged_graph":  # staged frames without the two-stream overlap
+            kf.set_frame_overlap(False)
         if mode == "eager":
             kf.set_graph_mode(False)
-        if mode == "icp_per_iter":
+        if mode in ("icp_per_iter", "staged_per_iter"):
             assert kf.set_icp_persistent(False)  # persistent path was the one in use
             kf.set_graph_mode(False)
         if mode == "profile":
             kf.set_profiling(True)
-        if mode == "staged":
+        if mode in ("staged", "staged_graph", "staged_per_iter"):
             kf.stage_frames(bgr, dep.astype(np.float32))
             for k in range(len(dep)):
                 kf.pipeline_staged(k)
             kf.synchronize()
+        elif mode == "staged_mixed":  # overlapped frames, then single-stream host frames
+            kf.stage_frames(bgr, dep.astype(np.float32))
+            half = 5  # odd: the last overlapped frame used set 1, the host frames set 0
+            for k in range(half):
+                kf.pipeline_staged(k)
+            for k in range(half, len(dep)):
+                kf.pipeline(bgr[k], dep[k].astype(np.float32))
         else:
             _run_pipeline(kf, bgr, dep, u16=(mode == "u16"))
         if mode == "profile":
