@@ -224,13 +224,15 @@ def main():
     # per-stage device ms + integrate roofline on further frames (profiled, eager)
     kf.set_profiling(True)
     stages = {k: [] for k in ("preprocess", "icp", "integrate", "raycast", "total")}
-    int_bytes, int_ms = [], []
+    int_bytes, int_ms, int_work = [], [], []
     for i in range(a.warmup + a.steps, a.warmup + a.steps + a.profile_frames):
         kf.pipeline_staged(order[i])
         ms = kf.stage_ms()
         for k in stages:
             stages[k].append(ms[k])
-        nu, nc = kf.integrate_counts()
+        wk = kf.integrate_stats()
+        nu, nc = wk["updated"], wk["colored"]
+        int_work.append(wk)
         int_bytes.append(8 * nu + 8 * nc + 7 * W * H)
         int_ms.append(ms["integrate"])
     kf.set_profiling(False)
@@ -278,6 +280,8 @@ def main():
             "reference_ms_per_frame": REF_MS_PER_FRAME,
         },
         "stage_ms": stage_med,
+        "integrate_voxels": ({k: int(np.mean([w[k] for w in int_work])) for k in int_work[0]}
+                             if int_work else None),
         "roofline": {
             "kernel": "k_integrate",
             "bound": "hbm",

@@ -182,6 +182,11 @@ int kfx_get_stage_ms(kfx_ctx *ctx, float out_ms[5]);
  * updated and those whose colour was also blended.  Count-only kernel, the
  * volume is not touched. */
 int kfx_integrate_counts(kfx_ctx *ctx, int64_t *n_updated, int64_t *n_colored);
+/* Work statistics of the same count-only pass: out = {updated, coloured,
+ * visited (voxels evaluated inside the per-column candidate z intervals),
+ * gathered (visited voxels that project into the image and read a depth),
+ * wave batches executed (4 voxels per lane each), 0, 0, 0}. */
+int kfx_integrate_stats(kfx_ctx *ctx, int64_t out[8]);
 
 /* ---- point cloud ------------------------------------------ */
 /* TSDFVolume::fetchPointCloud buffer size (tsdf_volume.cpp:67) */

@@ -647,7 +647,7 @@ static int create_impl(const kfx_intrinsics *intr, const kfx_params *params, int
                                 c->p.icp_dist_threshold, c->angle_thr);
   set_par(c, 0);
   c->icp_persistent = icp_persistent_ok(c->icp_plan, c->device);
-  if ((r = dalloc(c, (void **)&c->counters, sizeof(unsigned long long) * 32))) return fail(r);
+  if ((r = dalloc(c, (void **)&c->counters, sizeof(unsigned long long) * 128))) return fail(r);
   if ((r = dalloc(c, (void **)&c->xpose, sizeof(float) * 32))) return fail(r);
   launch_inv_lambda(c->stream, c->g[0], c->inv_lambda);
   if ((r = do_reset(c))) return fail(r);
@@ -1044,21 +1044,31 @@ int kfx_stage_icp(kfx_ctx *c, kfx_pose *out) {
   return failed ? KFX_TRACKING_LOST : KFX_OK;
 }
 
-static int integrate_counts_impl(kfx_ctx *c, int64_t *nu, int64_t *nc, const float *xpose) {
-  HIPCHK(hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * 32, c->stream));
+// out: {updated, coloured, visited, gathered, wave batches, 0, 0, 0} of the
+// last frame's integrate
+static int integrate_stats_impl(kfx_ctx *c, int64_t out[8], const float *xpose) {
+  HIPCHK(hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * 128, c->stream));
   launch_integrate(c->stream, c->vol, c->g[0], c->dl0, c->last_bgr ? c->last_bgr : c->bgr, c->st,
                    c->pose_log, to_dev(c->p.volu_pose), xpose, c->counters);
   HIPCHK(hipGetLastError());
-  unsigned long long h[32];
+  unsigned long long h[128];
   HIPCHK(hipMemcpyAsync(h, c->counters, sizeof(h), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
-  int64_t a = 0, b = 0;
+  for (int k = 0; k < 8; ++k) out[k] = 0;
   for (int i = 0; i < 16; ++i) {
-    a += (int64_t)h[2 * i];
-    b += (int64_t)h[2 * i + 1];
+    out[0] += (int64_t)h[2 * i];
+    out[1] += (int64_t)h[2 * i + 1];
+    for (int k = 2; k < 7; ++k) out[k] += (int64_t)h[16 * k + i];
   }
-  if (nu) *nu = a;
-  if (nc) *nc = b;
+  return KFX_OK;
+}
+
+static int integrate_counts_impl(kfx_ctx *c, int64_t *nu, int64_t *nc, const float *xpose) {
+  int64_t s[8];
+  const int r = integrate_stats_impl(c, s, xpose);
+  if (r) return r;
+  if (nu) *nu = s[0];
+  if (nc) *nc = s[1];
   return KFX_OK;
 }
 
@@ -1083,6 +1093,13 @@ int kfx_integrate_counts(kfx_ctx *c, int64_t *nu, int64_t *nc) {
   int r = check_ctx(c);
   if (r) return r;
   return integrate_counts_impl(c, nu, nc, nullptr);
+}
+
+int kfx_integrate_stats(kfx_ctx *c, int64_t out[8]) {
+  int r = check_ctx(c);
+  if (r) return r;
+  if (!out) return set_err(KFX_ERR_ARG, "null out");
+  return integrate_stats_impl(c, out, nullptr);
 }
 
 int kfx_stage_raycast(kfx_ctx *c, const kfx_pose *cam2vol, const float Rinv[9]) {

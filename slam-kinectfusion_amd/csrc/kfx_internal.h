@@ -90,6 +90,10 @@ struct VolView {
   int tsat;         // tsdf fixed point of a weight-64, ts = 1 update (integrate skip), or 1<<20
   size_t slice;    // voxels per z slice (= X*Y)
   __host__ __device__ size_t local_voxels() const { return slice * (size_t)zn; }
+  // Tile-column layout: the stored slices of one 8x8 column tile are one
+  // contiguous run of zn * 64 voxels, z-major inside:
+  //   index(x, y, z) = (tile(x, y) * zn + (z - zb)) * 64 + (y & 7) * 8 + (x & 7)
+  __host__ __device__ size_t tile_voxels() const { return (size_t)zn * 64; }
 };
 
 struct FrameView {

@@ -21,6 +21,15 @@
 #ifndef KFX_SINCOS
 #define KFX_SINCOS 1
 #endif
+#ifndef KFX_INT_BLOCK
+#define KFX_INT_BLOCK 256  // integrate: threads per block (one 8x8 column tile per wave)
+#endif
+#ifndef KFX_INT_CHUNKR
+#define KFX_INT_CHUNKR 65  // integrate: z-chunk c of a column gets weight (r/100)^c
+#endif
+#ifndef KFX_INT_MAXCHUNK
+#define KFX_INT_MAXCHUNK 8  // integrate: most z-chunks per column tile
+#endif
 #ifndef KFX_INT_WAVES
 #define KFX_INT_WAVES 16384  // integrate: target wave count (z-chunks per column tile)
 #endif
@@ -162,9 +171,10 @@ __device__ __forceinline__ unsigned *dmax_shards(const float2 *dl0, const LevelG
   return (unsigned *)(const_cast<float2 *>(dl0) + (size_t)g0.w * g0.h);
 }
 
-// z is the global slice; the view stores slices [zb, zb+zn)
+// z is the global slice; the view stores slices [zb, zb+zn) (tile-column
+// layout, kfx_internal.h VolView)
 __device__ __forceinline__ size_t vox_index(const VolView &v, int x, int y, int z) {
-  return (size_t)(z - v.zb) * v.slice + ((size_t)(y >> 3) * v.tiles_x + (x >> 3)) * 64 +
+  return (((size_t)(y >> 3) * v.tiles_x + (x >> 3)) * (size_t)v.zn + (size_t)(z - v.zb)) * 64 +
          ((y & 7) << 3) + (x & 7);
 }
 
@@ -1018,15 +1028,15 @@ struct RayMem;
 template <>
 struct RayMem<true> {
   __amdgpu_buffer_rsrc_t t;
-  unsigned slice, tiles_x;
+  unsigned zn, tiles_x;
   int zb;
   __device__ RayMem(const VolView &v)
-      : t(make_rsrc(v.tsdf, (unsigned)(2 * v.local_voxels()))), slice((unsigned)v.slice),
+      : t(make_rsrc(v.tsdf, (unsigned)(2 * v.local_voxels()))), zn((unsigned)v.zn),
         tiles_x((unsigned)v.tiles_x), zb(v.zb) {}
   __device__ int16_t ld(bool valid, int x, int y, int z) const {
     const unsigned ux = (unsigned)x, uy = (unsigned)y;
-    const unsigned in_slice = (__umul24(uy >> 3, tiles_x) + (ux >> 3)) * 64u + ((uy & 7u) << 3 | (ux & 7u));
-    const unsigned idx = __umul24((unsigned)(z - zb), slice) + in_slice;
+    const unsigned tile = __umul24(uy >> 3, tiles_x) + (ux >> 3);
+    const unsigned idx = ((__umul24(tile, zn) + (unsigned)(z - zb)) << 6) | ((uy & 7u) << 3 | (ux & 7u));
     return __builtin_amdgcn_raw_buffer_load_b16(t, valid ? idx * 2u : kOob, 0, 0);
   }
 };
@@ -1046,7 +1056,7 @@ struct RayMem<false> {
 // kCount: count-only variant (no voxel traffic) giving N_upd / N_col, the
 // algorithmic-byte inputs of the roofline.
 template <bool kCount, bool kIdx32>
-__global__ __launch_bounds__(256) void k_integrate(VolView v, LevelGeom g,
+__global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_integrate(VolView v, LevelGeom g,
                                                    const float2 *__restrict__ dl,
                                                    const uint8_t *__restrict__ bgr,
                                                    DevState *__restrict__ st, DevPose *log,
@@ -1056,7 +1066,7 @@ __global__ __launch_bounds__(256) void k_integrate(VolView v, LevelGeom g,
   __shared__ float rtab[66];
   __shared__ DevPose s_pose;
   __shared__ int s_kind;
-  if (threadIdx.x < 66) rtab[threadIdx.x] = 1.f / (float)max(1, (int)threadIdx.x);
+  for (int i = threadIdx.x; i < 66; i += KFX_INT_BLOCK) rtab[i] = 1.f / (float)max(1, i);
   if (threadIdx.x == 0) {
     if (xpose) {  // stage seam: explicit vol2cam
       s_kind = 1;
@@ -1074,19 +1084,22 @@ __global__ __launch_bounds__(256) void k_integrate(VolView v, LevelGeom g,
     }
   }
   __syncthreads();
+#ifdef KFX_INT_TRACE
+  const unsigned long long t_start = wall_clock64();
+#endif
   const int lane = threadIdx.x & 63;
-  const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int tile = blockIdx.x * (KFX_INT_BLOCK / 64) + (threadIdx.x >> 6);
   if (tile >= v.tiles_x * v.tiles_y) return;
   const int chunk = blockIdx.y, nchunk = gridDim.y;
   const int x = (tile % v.tiles_x) * 8 + (lane & 7);
   const int y = (tile / v.tiles_x) * 8 + (lane >> 3);
-  const size_t base = (size_t)tile * 64 + lane;
+  const size_t base = (size_t)tile * v.tile_voxels() + lane;  // this column's (x, y, zb)
   if (s_kind == 2) {  // reset(): whole volume zeroed (A5 D)
     if (kCount) return;
     const int z0 = (int)((long long)v.zn * chunk / nchunk);
     const int z1 = (int)((long long)v.zn * (chunk + 1) / nchunk);
     for (int z = z0; z < z1; ++z) {  // local slices
-      const size_t i = base + (size_t)z * v.slice;
+      const size_t i = base + (size_t)z * 64;
       v.tsdf[i] = 0;
       v.weight[i] = 0;
       v.rgb[i] = 0u;
@@ -1120,18 +1133,32 @@ __global__ __launch_bounds__(256) void k_integrate(VolView v, LevelGeom g,
     const double zfar = ((double)dmax + (double)v.trunc) * 1.02 + 0.01;
     clip_lin(zfar - az, -sz, lo, hi);
   }
-  if (!(hi >= lo)) return;
-  const int zlo = max((int)lo0, (int)floor(lo) - 2);
-  const int zhi = min((int)hi0, (int)ceil(hi) + 2);
-  if (zhi < zlo) return;
-  const int len = zhi - zlo + 1;
-  const int za = zlo + (int)((long long)len * chunk / nchunk);
-  const int zb = zlo + (int)((long long)len * (chunk + 1) / nchunk) - 1;
-  if (zb < za) return;
+  int za = 1, zb = 0;  // this lane's chunk of its column interval (empty: none)
+  if (hi >= lo) {
+    const int zlo = max((int)lo0, (int)floor(lo) - 2);
+    const int zhi = min((int)hi0, (int)ceil(hi) + 2);
+    if (zhi >= zlo) {
+      const int len = zhi - zlo + 1;
+#if KFX_INT_CHUNKR == 100
+      za = zlo + (int)((long long)len * chunk / nchunk);
+      zb = zlo + (int)((long long)len * (chunk + 1) / nchunk) - 1;
+#else
+      // chunk c gets weight r^c: the chunks dispatched last (highest
+      // blockIdx.y) are the shortest, so the kernel's tail waves are short
+      const float r = (float)KFX_INT_CHUNKR * 0.01f;
+      const float den = 1.f - __powf(r, (float)nchunk);
+      za = zlo + (int)((float)len * ((1.f - __powf(r, (float)chunk)) / den));
+      zb = chunk + 1 == nchunk ? zhi : zlo + (int)((float)len * ((1.f - __powf(r, (float)(chunk + 1))) / den)) - 1;
+#endif
+    }
+  }
+  const bool live = zb >= za;
+  if (__all(!live)) return;
 
   const float trunc = v.trunc;
   const float thres_color = trunc / 2;
-  unsigned cu = 0, cc = 0;
+  // kCount: updated, coloured, visited, gathered voxels; wave batches
+  unsigned cu = 0, cc = 0, cv = 0, cg = 0, cb = 0;
   int z = 1;
 #pragma unroll 8
   for (; z < za; ++z) vc = add(vc, zs);
@@ -1139,9 +1166,9 @@ __global__ __launch_bounds__(256) void k_integrate(VolView v, LevelGeom g,
   using Idx = typename Mem::Idx;
   const Mem mem(v);
   const __amdgpu_buffer_rsrc_t rdl = make_rsrc(dl, (unsigned)(8 * g.w * g.h));
-  const Idx slice = (Idx)v.slice;
+  constexpr Idx slice = 64;  // index step per z (tile-column layout)
   Idx iz = (Idx)base + (Idx)(za - v.zb) * slice;  // voxel index of (x, y, z)
-  const bool fast = __all(column_fast(vc, zs, v.Z));  // wave-uniform
+  const bool fast = __all(!live || column_fast(vc, zs, v.Z));  // wave-uniform
   const float fw = (float)g.w, fh = (float)g.h;
   // Batches of kB voxels: positions, projections, the kB {depth, 1/lambda}
   // gathers, then the kB tsdf/weight loads are issued back to back
@@ -1192,6 +1219,12 @@ __global__ __launch_bounds__(256) void k_integrate(VolView v, LevelGeom g,
     }
     if (kCount) {
       iz += (Idx)kB * slice;
+      ++cb;
+#pragma unroll
+      for (int j = 0; j < kB; ++j) {
+        cv += (z + j <= zb);
+        cg += (pix[j] != kOob);
+      }
 #pragma unroll
       for (int j = 0; j < kB; ++j)
         if (ok[j]) {
@@ -1245,10 +1278,25 @@ __global__ __launch_bounds__(256) void k_integrate(VolView v, LevelGeom g,
       }
     }
   }
+#ifdef KFX_INT_TRACE
+  if (!kCount && counters && lane == 0) {  // debug: per-wave timeline
+    unsigned long long *r = counters + 4 * ((size_t)(blockIdx.y * gridDim.x + blockIdx.x) * (KFX_INT_BLOCK / 64) + (threadIdx.x >> 6));
+    r[0] = t_start;
+    r[1] = wall_clock64();
+    r[2] = ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |
+           (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+    r[3] = (unsigned long long)tile | ((unsigned long long)chunk << 32);
+  }
+#endif
   if (kCount) {
     const int sh = (blockIdx.x + blockIdx.y) % 16;
     atomicAdd(&counters[2 * sh], (unsigned long long)cu);
     atomicAdd(&counters[2 * sh + 1], (unsigned long long)cc);
+    atomicAdd(&counters[32 + sh], (unsigned long long)cv);
+    atomicAdd(&counters[48 + sh], (unsigned long long)cg);
+    if (lane == 0) {  // per-wave counts (wave-uniform)
+      atomicAdd(&counters[64 + sh], (unsigned long long)cb);
+    }
   }
 }
 
@@ -1323,8 +1371,8 @@ __device__ __forceinline__ int xcd_remap(int b, int nb) {
 template <bool kIdx32>
 __device__ __forceinline__ size_t ray_index(const VolView &v, int x, int y, int z) {
   if (kIdx32)
-    return (size_t)((unsigned)(z - v.zb) * (unsigned)v.slice +
-                    (((unsigned)(y >> 3) * (unsigned)v.tiles_x + (unsigned)(x >> 3)) << 6) +
+    return (size_t)(((((unsigned)(y >> 3) * (unsigned)v.tiles_x + (unsigned)(x >> 3)) * (unsigned)v.zn +
+                      (unsigned)(z - v.zb)) << 6) |
                     (unsigned)(((y & 7) << 3) | (x & 7)));
   return vox_index(v, x, y, z);
 }
@@ -1887,6 +1935,22 @@ __global__ void k_export_soa(VolView v, int z0, int nz, int16_t *t, int16_t *w, 
 // ---------------------------------------------------------------------------
 // launchers
 
+#ifdef KFX_INT_TRACE
+static unsigned long long *g_int_trace = nullptr;
+static int g_int_trace_waves = 0;
+}  // namespace kfx
+// debug build only: the last integrate launch's per-wave records
+// {start, end, xcc_id<<32 | hw_id, chunk<<32 | tile} (wall clock, 100 MHz)
+extern "C" int kfx_debug_integrate_trace(unsigned long long *out, int cap) {
+  const int n = std::min(cap, kfx::g_int_trace_waves);
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpy(out, kfx::g_int_trace, sizeof(unsigned long long) * 4 * n, hipMemcpyDeviceToHost) != hipSuccess)
+    return -1;
+  return n;
+}
+namespace kfx {
+#endif
+
 void launch_frame_begin(hipStream_t s, DevState *st, float2 *dl0, LevelGeom g0) {
   hipLaunchKernelGGL(k_frame_begin, dim3(1), dim3(1), 0, s, st,
                      dl0 ? (unsigned *)(dl0 + (size_t)g0.w * g0.h) : nullptr);
@@ -1990,17 +2054,31 @@ void launch_integrate(hipStream_t s, VolView v, LevelGeom g0, const float2 *dl0,
                       const float *xpose, unsigned long long *counters) {
   const int tiles = v.tiles_x * v.tiles_y;
   // z-chunks so that >= KFX_INT_WAVES waves exist (16 per SIMD on 1024 SIMDs)
-  const int nchunk = std::max(1, std::min(8, (KFX_INT_WAVES + tiles - 1) / tiles));
-  dim3 grd((tiles + 3) / 4, nchunk);
+  const int nchunk = std::max(1, std::min(KFX_INT_MAXCHUNK, (KFX_INT_WAVES + tiles - 1) / tiles));
+  constexpr int wpb = KFX_INT_BLOCK / 64;  // waves (column tiles) per block
+  dim3 grd((tiles + wpb - 1) / wpb, nchunk);
   const bool idx32 = v.local_voxels() < (1ull << 30);
+#ifdef KFX_INT_TRACE
+  static unsigned long long *trace_buf = nullptr;
+  if (!trace_buf) {
+    (void)hipMalloc(&trace_buf, sizeof(unsigned long long) * 4 * (1 << 20));
+    g_int_trace = trace_buf;
+  }
+  g_int_trace_waves = (int)(grd.x * grd.y * wpb);
+  if (!counters) {
+    hipLaunchKernelGGL((k_integrate<false, true>), grd, dim3(KFX_INT_BLOCK), 0, s, v, g0, dl0, bgr, st, log,
+                       vpose, xpose, trace_buf);
+    return;
+  }
+#endif
   if (counters)
-    hipLaunchKernelGGL((k_integrate<true, false>), grd, dim3(256), 0, s, v, g0, dl0, bgr, st, log,
+    hipLaunchKernelGGL((k_integrate<true, false>), grd, dim3(KFX_INT_BLOCK), 0, s, v, g0, dl0, bgr, st, log,
                        vpose, xpose, counters);
   else if (idx32)
-    hipLaunchKernelGGL((k_integrate<false, true>), grd, dim3(256), 0, s, v, g0, dl0, bgr, st, log,
+    hipLaunchKernelGGL((k_integrate<false, true>), grd, dim3(KFX_INT_BLOCK), 0, s, v, g0, dl0, bgr, st, log,
                        vpose, xpose, counters);
   else
-    hipLaunchKernelGGL((k_integrate<false, false>), grd, dim3(256), 0, s, v, g0, dl0, bgr, st, log,
+    hipLaunchKernelGGL((k_integrate<false, false>), grd, dim3(KFX_INT_BLOCK), 0, s, v, g0, dl0, bgr, st, log,
                        vpose, xpose, counters);
 }
 
@@ -2016,7 +2094,8 @@ void launch_raycast(hipStream_t s, VolView v, int levels, const LevelGeom *g, Fr
   ra.levels = levels;
   for (int l = 0; l < levels; ++l) ra.g[l] = g[l];
   dim3 grd(((g[0].w + 15) / 16) * ((g[0].h + 15) / 16));
-  const bool idx32 = v.local_voxels() < (1ull << 31) && v.slice < (1ull << 24);
+  // 32-bit indices (24-bit tile * zn products)
+  const bool idx32 = v.local_voxels() < (1ull << 31) && (size_t)v.tiles_x * v.tiles_y * v.zn < (1ull << 24);
   if (keys) {
     if (idx32)
       hipLaunchKernelGGL((k_raycast<true, true>), grd, dim3(256), 0, s, v, ra, rc, cur, prev, st, log,

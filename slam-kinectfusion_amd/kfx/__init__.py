@@ -32,7 +32,7 @@ EXPORTS = [
     "kfx_write_poses_txt", "kfx_get_frame_maps", "kfx_set_frame_maps", "kfx_download_tsdf",
     "kfx_upload_tsdf", "kfx_download_volume_soa", "kfx_stage_preprocess", "kfx_stage_icp_accumulate",
     "kfx_stage_icp", "kfx_stage_integrate", "kfx_stage_raycast", "kfx_set_profiling", "kfx_get_stage_ms",
-    "kfx_integrate_counts", "kfx_create_slab", "kfx_slab_info", "kfx_comm_get_unique_id", "kfx_comm_init",
+    "kfx_integrate_counts", "kfx_integrate_stats", "kfx_create_slab", "kfx_slab_info", "kfx_comm_get_unique_id", "kfx_comm_init",
     "kfx_pipeline_group", "kfx_extract_points", "kfx_write_ply", "kfx_save_pointcloud",
 ]
 
@@ -92,6 +92,7 @@ def lib():
         "kfx_set_profiling": ([vp, i], i),
         "kfx_get_stage_ms": ([vp, P(f)], i),
         "kfx_integrate_counts": ([vp, P(C.c_int64), P(C.c_int64)], i),
+        "kfx_integrate_stats": ([vp, P(C.c_int64)], i),
         "kfx_create_slab": ([P(Intrinsics), P(Params), i, i, i, P(vp)], i),
         "kfx_slab_info": ([vp, P(i), P(i), P(i), P(i)], i),
         "kfx_comm_get_unique_id": ([P(C.c_uint8)], i),
@@ -258,6 +259,12 @@ class KinectFusion:
         a, b = C.c_int64(), C.c_int64()
         _check(lib().kfx_integrate_counts(self._h, C.byref(a), C.byref(b)), "kfx_integrate_counts")
         return a.value, b.value
+
+    def integrate_stats(self) -> dict:
+        """Work of the last frame's integrate: updated / coloured / visited / gathered voxels."""
+        a = (C.c_int64 * 8)()
+        _check(lib().kfx_integrate_stats(self._h, a), "kfx_integrate_stats")
+        return dict(zip(["updated", "colored", "visited", "gathered", "wave_batches"], a[:5]))
 
     # ---- point cloud (kinectfusion::extracePointcloud / savePointcloud) ---
     def extract_points(self, cap: int = 10_000_000) -> np.ndarray:

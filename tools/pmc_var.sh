@@ -1,0 +1,12 @@
+#!/bin/bash
+# One SQ counter pass per variant library: tools/pmc_var.sh "counters" var1 var2 ...
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
+cd /tmp && export TMPDIR=/tmp
+CTR=$1
+shift
+for v in "$@"; do
+  echo "=== $v"
+  KFX_LIB_PATH="$ROOT/slam-kinectfusion_amd/lib/var_$v/libkfx.so" timeout -k 10 120 rocprofv3 --pmc $CTR --output-format csv \
+      -d "$ROOT/gpurun_out/pmcv/$v" -- python3 "$ROOT/bench.py" --steps 20 --warmup 5 --profile-frames 2 --cpu-frames 0 \
+      > "$ROOT/gpurun_out/pmcv/$v.log" 2>&1 || { echo "rc=$?"; tail -5 "$ROOT/gpurun_out/pmcv/$v.log"; exit 1; }
+done
