@@ -113,6 +113,14 @@ int kfx_set_graph_mode(kfx_ctx *ctx, int enabled);
  * a second stream, over double-buffered frame maps (default on; staged frames
  * then launch eagerly instead of through graphs).  Results are identical. */
 int kfx_set_frame_overlap(kfx_ctx *ctx, int enabled);
+/* Sampled kernel timing inside a run of pipelined frames: every `every`-th
+ * frame (from now, up to max_samples frames) is bracketed by HIP events on
+ * the stream its kernels run on (such a frame launches eagerly instead of
+ * through its graph); kfx_get_kernel_timing returns the mean ms of ICP,
+ * integrate and raycast over the samples taken and starts a new sample set.
+ * every = 0 turns sampling off. */
+int kfx_set_kernel_timing(kfx_ctx *ctx, int every, int max_samples);
+int kfx_get_kernel_timing(kfx_ctx *ctx, float out_ms[3], int *n_samples);
 /* Run all ICP iterations of a frame as one persistent launch (default on; used
  * only when its grid fits co-resident on the device, else one launch per
  * iteration).  Returns 1 if the persistent kernel is usable on this context, 0

@@ -99,6 +99,13 @@ struct kfx_ctx {
   bool overlap = true;
   hipStream_t pstream = nullptr;
   hipEvent_t ev_prep = nullptr, ev_free[2]{};
+
+  // sampled kernel timing (kfx_set_kernel_timing): every `timing_every`-th
+  // pipelined frame records its stage events into the next unused set
+  int timing_every = 0;
+  unsigned long long frame_seq = 0;
+  std::vector<hipEvent_t> tsets;  // 5 per sample
+  size_t tnext = 0;
   VolView vol{};
   DevState *st = nullptr;
   DevPose *pose_log = nullptr;
@@ -182,18 +189,20 @@ struct FrameInput {
 };
 
 // The per-frame launch sequence (kinectfusion.cpp:78-127 with the frame-1 and
-// failure branches resolved on the device).  `events` records stage events.
+// failure branches resolved on the device).  `ev` (or null) receives the stage
+// events: [0] start, [1] after preprocess, [2] after ICP, [3] after integrate,
+// [4] after raycast (+ slab combine); [0..1] are absent for overlapped frames.
 // Slab contexts stop after their local raycast (enqueue_local) and then
 // combine the slabs' raycast results (enqueue_combine).
-void enqueue_local(kfx_ctx *c, FrameInput in, bool events);
-void enqueue_track(kfx_ctx *c, FrameInput in, bool events, bool begin);
+void enqueue_local(kfx_ctx *c, FrameInput in, hipEvent_t *ev);
+void enqueue_track(kfx_ctx *c, FrameInput in, hipEvent_t *ev, bool begin);
 int enqueue_combine(kfx_ctx *c);
 
-int enqueue_frame(kfx_ctx *c, FrameInput in, bool events) {
-  enqueue_local(c, in, events);
+int enqueue_frame(kfx_ctx *c, FrameInput in, hipEvent_t *ev) {
+  enqueue_local(c, in, ev);
   int r = KFX_OK;
   if (c->slab) r = enqueue_combine(c);
-  if (events) (void)hipEventRecord(c->ev[4], c->stream);
+  if (ev) (void)hipEventRecord(ev[4], c->stream);
   return r;
 }
 
@@ -220,9 +229,9 @@ int enqueue_combine(kfx_ctx *c) {
   return KFX_OK;
 }
 
-void enqueue_local(kfx_ctx *c, FrameInput in, bool events) {
+void enqueue_local(kfx_ctx *c, FrameInput in, hipEvent_t *ev) {
   hipStream_t s = c->stream;
-  if (events) (void)hipEventRecord(c->ev[0], s);
+  if (ev) (void)hipEventRecord(ev[0], s);
   // imageProcess (kinectfusion.cpp:48-76)
   const float *raw[kMaxLevels];
   for (int l = 0; l < kMaxLevels; ++l) raw[l] = c->raw[l];
@@ -238,13 +247,13 @@ void enqueue_local(kfx_ctx *c, FrameInput in, bool events) {
   launch_preprocess_maps(s, c->L, raw, in.d16, c->g, c->cur, c->p.bfilter_kernel_size,
                          c->p.bfilter_color_sigma, c->p.bfilter_spatial_sigma, c->p.dfilter_dist,
                          c->inv_lambda, c->dl0);
-  if (events) (void)hipEventRecord(c->ev[1], s);
-  enqueue_track(c, in, events, false);
+  if (ev) (void)hipEventRecord(ev[1], s);
+  enqueue_track(c, in, ev, false);
 }
 
 // ICP, integrate and raycast of the frame whose maps are in the current set;
 // begin: the frame's frame_begin has not run yet (overlapped frames)
-void enqueue_track(kfx_ctx *c, FrameInput in, bool events, bool begin) {
+void enqueue_track(kfx_ctx *c, FrameInput in, hipEvent_t *ev, bool begin) {
   hipStream_t s = c->stream;
   // ICPRegistration::rigidTransform (icp_registration.cpp:16-46)
   if (c->icp_persistent && c->icp_persistent_enabled) {
@@ -258,10 +267,10 @@ void enqueue_track(kfx_ctx *c, FrameInput in, bool events, bool begin) {
                    c->icp_shards, c->icp_ticket, 0, 1);
     }
   }
-  if (events) (void)hipEventRecord(c->ev[2], s);
+  if (ev) (void)hipEventRecord(ev[2], s);
   launch_integrate(s, c->vol, c->g[0], c->dl0, in.bgr, c->st, c->pose_log,
                    to_dev(c->p.volu_pose), nullptr, nullptr);
-  if (events) (void)hipEventRecord(c->ev[3], s);
+  if (ev) (void)hipEventRecord(ev[3], s);
   launch_raycast(s, c->vol, c->L, c->g, c->cur, c->prev, c->st, c->pose_log,
                  to_dev(c->p.volu_pose), nullptr, c->slab ? c->key_local : nullptr);
 }
@@ -273,7 +282,7 @@ void enqueue_track(kfx_ctx *c, FrameInput in, bool events, bool begin) {
 // cross-stream dependencies: ~9 us/frame for the wait on ev_prep, while
 // dropping the ev_free ordering (unsafe) is slower, as preprocess then
 // competes with integrate/raycast.
-int enqueue_frame_overlap(kfx_ctx *c, FrameInput in) {
+int enqueue_frame_overlap(kfx_ctx *c, FrameInput in, hipEvent_t *ev) {
   const int p = c->par ^ 1;
   set_par(c, p);
   hipStream_t b = c->pstream;
@@ -294,9 +303,11 @@ int enqueue_frame_overlap(kfx_ctx *c, FrameInput in) {
                          c->inv_lambda, c->dl0);
   HIPCHK(hipEventRecord(c->ev_prep, b));
   HIPCHK(hipStreamWaitEvent(c->stream, c->ev_prep, 0));
-  enqueue_track(c, in, false, true);
+  if (ev) HIPCHK(hipEventRecord(ev[1], c->stream));
+  enqueue_track(c, in, ev, true);
   int r = KFX_OK;
   if (c->slab) r = enqueue_combine(c);
+  if (ev) HIPCHK(hipEventRecord(ev[4], c->stream));
   HIPCHK(hipEventRecord(c->ev_free[p], c->stream));
   return r;
 }
@@ -304,7 +315,7 @@ int enqueue_frame_overlap(kfx_ctx *c, FrameInput in) {
 int build_graph(kfx_ctx *c, FrameInput in, hipGraphExec_t *out) {
   hipGraph_t graph = nullptr;
   HIPCHK(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-  const int r = enqueue_frame(c, in, false);
+  const int r = enqueue_frame(c, in, nullptr);
   const hipError_t ec = hipStreamEndCapture(c->stream, &graph);
   if (r) {
     if (graph) (void)hipGraphDestroy(graph);
@@ -378,15 +389,19 @@ int run_frame(kfx_ctx *c, FrameInput in, hipGraphExec_t *graph, bool overlap = f
   int r = ensure_pose_capacity(c, 1);
   if (r) return r;
   c->last_bgr = in.bgr;
+  hipEvent_t *tev = nullptr;  // this frame's timing sample, if sampled
+  if (c->timing_every > 0 && !c->profiling && c->frame_seq++ % c->timing_every == 0 &&
+      5 * (c->tnext + 1) <= c->tsets.size())
+    tev = &c->tsets[5 * c->tnext++];
   if (overlap && c->overlap && !c->profiling) {
-    if ((r = enqueue_frame_overlap(c, in))) return r;
+    if ((r = enqueue_frame_overlap(c, in, tev))) return r;
     HIPCHK(hipGetLastError());
     c->pending += 1;
     return KFX_OK;
   }
   set_par(c, 0);  // single-stream frames (and their graphs) use set 0
   if (c->profiling) {
-    if ((r = enqueue_frame(c, in, true))) return r;
+    if ((r = enqueue_frame(c, in, c->ev))) return r;
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventSynchronize(c->ev[4]));
     for (int i = 0; i < 4; ++i) HIPCHK(hipEventElapsedTime(&c->stage_ms[i], c->ev[i], c->ev[i + 1]));
@@ -395,10 +410,10 @@ int run_frame(kfx_ctx *c, FrameInput in, hipGraphExec_t *graph, bool overlap = f
     // raycast(+slab combine, +resize)
   } else {
     if ((r = ensure_graph(c, in, graph))) return r;
-    if (c->graph_mode && graph && *graph) {
+    if (c->graph_mode && graph && *graph && !tev) {
       HIPCHK(hipGraphLaunch(*graph, c->stream));
-    } else {
-      if ((r = enqueue_frame(c, in, false))) return r;
+    } else {  // eager (a timing sample is launched eagerly with its events)
+      if ((r = enqueue_frame(c, in, tev))) return r;
       HIPCHK(hipGetLastError());
     }
   }
@@ -667,6 +682,7 @@ int kfx_destroy(kfx_ctx *c) {
     if (e) (void)hipEventDestroy(e);
   for (hipEvent_t e : {c->ev_prep, c->ev_free[0], c->ev_free[1]})
     if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t e : c->tsets) (void)hipEventDestroy(e);
   if (c->pstream) (void)hipStreamDestroy(c->pstream);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -757,6 +773,43 @@ int kfx_set_frame_overlap(kfx_ctx *c, int enabled) {
   if (r) return r;
   HIPCHK(hipStreamSynchronize(c->stream));
   c->overlap = enabled != 0;
+  return KFX_OK;
+}
+
+int kfx_set_kernel_timing(kfx_ctx *c, int every, int max_samples) {
+  int r = check_ctx(c);
+  if (r) return r;
+  if (every < 0 || max_samples < 0) return set_err(KFX_ERR_ARG, "negative timing argument");
+  HIPCHK(hipStreamSynchronize(c->stream));
+  for (hipEvent_t e : c->tsets) (void)hipEventDestroy(e);
+  c->tsets.clear();
+  c->tnext = 0;
+  c->frame_seq = 0;
+  c->timing_every = every;
+  if (every == 0) return KFX_OK;
+  c->tsets.assign(5 * (size_t)max_samples, nullptr);
+  // timing-only events: no system-scope fence on record (a fence per event
+  // cost ~6 us of GPU time each)
+  for (hipEvent_t &e : c->tsets) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
+  return KFX_OK;
+}
+
+int kfx_get_kernel_timing(kfx_ctx *c, float out_ms[3], int *n_samples) {
+  int r = check_ctx(c);
+  if (r) return r;
+  if (!out_ms) return set_err(KFX_ERR_ARG, "null out");
+  HIPCHK(hipStreamSynchronize(c->stream));
+  double acc[3] = {0, 0, 0};
+  for (size_t k = 0; k < c->tnext; ++k) {
+    for (int i = 0; i < 3; ++i) {
+      float ms = 0.f;
+      HIPCHK(hipEventElapsedTime(&ms, c->tsets[5 * k + 1 + i], c->tsets[5 * k + 2 + i]));
+      acc[i] += ms;
+    }
+  }
+  for (int i = 0; i < 3; ++i) out_ms[i] = c->tnext ? (float)(acc[i] / (double)c->tnext) : 0.f;
+  if (n_samples) *n_samples = (int)c->tnext;
+  c->tnext = 0;
   return KFX_OK;
 }
 
@@ -1251,7 +1304,7 @@ int kfx_pipeline_group(kfx_ctx **cs, int n, const uint8_t *bgr, const float *dep
     HIPCHK(hipMemcpyAsync(c->raw[0], depth_mm, np * 4, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(c->bgr, bgr, np * 3, hipMemcpyHostToDevice, c->stream));
     c->last_bgr = c->bgr;
-    enqueue_local(c, {c->raw[0], nullptr, c->bgr}, false);
+    enqueue_local(c, {c->raw[0], nullptr, c->bgr}, nullptr);
     HIPCHK(hipGetLastError());
   }
   for (int k = 0; k < n; ++k) {

@@ -113,6 +113,24 @@ __device__ __forceinline__ float div_rn(float x, float d, float y) {
   return fmaf(r, y, q0);
 }
 
+// The same sequences on two independent operands (v_pk_mul/v_pk_fma_f32: the
+// per-element IEEE operations of the scalar forms, two per instruction).
+typedef float pf2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ pf2 pfma(pf2 a, pf2 b, pf2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ pf2 rcp_rn2(pf2 d) {
+  const pf2 r = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  return pfma(pfma(-d, r, pf2{1.f, 1.f}), r, r);
+}
+__device__ __forceinline__ pf2 div_rn2(pf2 x, pf2 d, pf2 y) {
+  const pf2 q0 = x * y;
+  return pfma(pfma(-q0, d, x), y, q0);
+}
+__device__ __forceinline__ pf2 sqrt_rn2(pf2 x) {
+  const pf2 y = {__builtin_amdgcn_rsqf(x.x), __builtin_amdgcn_rsqf(x.y)};
+  const pf2 s0 = x * y;
+  return pfma(pfma(-s0, s0, x), pf2{0.5f, 0.5f} * y, s0);
+}
+
 // Pixel coordinate rn((a / d) * f + c) as a float, with a / d from one
 // reciprocal y = RN(1/d) shared by both image axes: div_rn(a, d, y) is the
 // correctly rounded quotient (Markstein; checked on 2e10 random general pairs,
@@ -1187,36 +1205,49 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(8
     float sdf[kB];
     unsigned pix[kB];
     bool ok[kB];
-    if (fast) {  // the cheap exact sequences
+    // projection: ok = in the image in front of the camera (tsdf_volume.cu:56-66)
+    if (fast) {  // the cheap exact sequences, two voxels per packed-FP32 op
+      static_assert(kB % 2 == 0, "voxel pairs");
 #pragma unroll
-      for (int j = 0; j < kB; ++j) {
-        const float yv = rcp_rn(p[j].z);
-        const float uf = rintf(div_rn(p[j].x, p[j].z, yv) * g.fx + g.cx);
-        const float vf = rintf(div_rn(p[j].y, p[j].z, yv) * g.fy + g.cy);
-        ok[j] = (z + j <= zb) & (p[j].z > 0) & (uf >= 0.f) & (uf < fw) & (vf >= 0.f) & (vf < fh);
-        pix[j] = ok[j] ? ((unsigned)(int)vf * (unsigned)g.w + (unsigned)(int)uf) * 8u : kOob;
+      for (int j = 0; j < kB; j += 2) {
+        const pf2 pz = {p[j].z, p[j + 1].z}, px = {p[j].x, p[j + 1].x}, py = {p[j].y, p[j + 1].y};
+        const pf2 yv = rcp_rn2(pz);
+        const pf2 uu = div_rn2(px, pz, yv) * pf2{g.fx, g.fx} + pf2{g.cx, g.cx};
+        const pf2 vv = div_rn2(py, pz, yv) * pf2{g.fy, g.fy} + pf2{g.cy, g.cy};
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const float uf = rintf(uu[k]), vf = rintf(vv[k]);
+          ok[j + k] = (z + j + k <= zb) & (pz[k] > 0) & (uf >= 0.f) & (uf < fw) & (vf >= 0.f) & (vf < fh);
+          pix[j + k] = ok[j + k] ? ((unsigned)(int)vf * (unsigned)g.w + (unsigned)(int)uf) * 8u : kOob;
+        }
       }
-      float2 d[kB];
-#pragma unroll
-      for (int j = 0; j < kB; ++j)
-        d[j] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rdl, pix[j], 0, 0));
-#pragma unroll
-      for (int j = 0; j < kB; ++j) {
-        sdf[j] = -(d[j].y * sqrt_rn(n2[j]) - d[j].x);
-        ok[j] = ok[j] & (d[j].x > 0) & (sdf[j] >= -trunc);
-      }
-    } else {  // IEEE division / sqrt (tiny or huge operands)
+    } else {  // IEEE division (tiny or huge operands)
 #pragma unroll
       for (int j = 0; j < kB; ++j) {
         const float uf = rintf((p[j].x / p[j].z) * g.fx + g.cx);
         const float vf = rintf((p[j].y / p[j].z) * g.fy + g.cy);
         ok[j] = (z + j <= zb) & (p[j].z > 0) & (uf >= 0.f) & (uf < fw) & (vf >= 0.f) & (vf < fh);
         pix[j] = ok[j] ? ((unsigned)(int)vf * (unsigned)g.w + (unsigned)(int)uf) * 8u : kOob;
-        const float2 d = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rdl, pix[j], 0, 0));
-        sdf[j] = -(d.y * sqrtf(n2[j]) - d.x);
-        ok[j] = ok[j] & (d.x > 0) & (sdf[j] >= -trunc);
       }
     }
+    float2 d[kB];
+#pragma unroll
+    for (int j = 0; j < kB; ++j)
+      d[j] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rdl, pix[j], 0, 0));
+    // sdf and the depth test (tsdf_volume.cu:67-71)
+    if (fast) {
+#pragma unroll
+      for (int j = 0; j < kB; j += 2) {
+        const pf2 sd = -(pf2{d[j].y, d[j + 1].y} * sqrt_rn2(pf2{n2[j], n2[j + 1]}) - pf2{d[j].x, d[j + 1].x});
+        sdf[j] = sd.x;
+        sdf[j + 1] = sd.y;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < kB; ++j) sdf[j] = -(d[j].y * sqrtf(n2[j]) - d[j].x);
+    }
+#pragma unroll
+    for (int j = 0; j < kB; ++j) ok[j] = ok[j] & (d[j].x > 0) & (sdf[j] >= -trunc);
     if (kCount) {
       iz += (Idx)kB * slice;
       ++cb;
@@ -1233,6 +1264,9 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(8
         }
       continue;
     }
+    // tsdf/weight of the voxels that pass (issuing them with the depth
+    // gathers, before the depth test, measured slower: the rejected voxels'
+    // extra reads cost more than the saved round trip)
     int16_t t0[kB], w0[kB];
     Idx vi[kB];
 #pragma unroll

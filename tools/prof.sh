@@ -9,7 +9,8 @@
 set -o pipefail
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 cd /tmp && export TMPDIR=/tmp
-ARGS=${@:-"--steps 100 --warmup 20 --profile-frames 4 --cpu-frames 0"}
+ARGS="$*"   # the stats pass runs bench.py with these (default: its defaults)
+PMC_ARGS="--steps 100 --warmup 20 --profile-frames 4 --cpu-frames 0"
 OUT="$ROOT/gpurun_out/prof"
 mkdir -p "$OUT"
 run() {  # name, timeout, rocprof args...
@@ -21,11 +22,13 @@ run() {  # name, timeout, rocprof args...
   echo "rc=$rc"
   [ $rc -eq 0 ] || { tail -20 "$OUT/$name.log"; exit $rc; }
 }
-run stats 240 --kernel-trace --stats --output-format csv -d "$OUT/stats" -o run -- python3 "$ROOT/bench.py" $ARGS
+run stats 300 --kernel-trace --stats --output-format csv -d "$OUT/stats" -o run -- python3 "$ROOT/bench.py" $ARGS
+grep "^{\"metric\"" "$OUT/stats.log" | tail -1 > "$OUT/stats_bench.json"
+python3 "$ROOT/tools/prof_summary.py" "$OUT/stats/run_kernel_trace.csv" 20 300 "$OUT/kernel_summary.json" > /dev/null
 if [ -x "$ROOT/tools/build/pmc_calib" ]; then
   run calib_fetch 90 --pmc FETCH_SIZE --output-format csv -d "$OUT/calib/FETCH_SIZE" -- "$ROOT/tools/build/pmc_calib"
   run calib_write 90 --pmc WRITE_SIZE --output-format csv -d "$OUT/calib/WRITE_SIZE" -- "$ROOT/tools/build/pmc_calib"
 fi
-run pmc_fetch 240 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc/FETCH_SIZE" -- python3 "$ROOT/bench.py" $ARGS
-run pmc_write 240 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc/WRITE_SIZE" -- python3 "$ROOT/bench.py" $ARGS
+run pmc_fetch 240 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc/FETCH_SIZE" -- python3 "$ROOT/bench.py" $PMC_ARGS
+run pmc_write 240 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc/WRITE_SIZE" -- python3 "$ROOT/bench.py" $PMC_ARGS
 python3 "$ROOT/tools/traffic.py" "$OUT"
