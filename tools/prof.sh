@@ -10,7 +10,7 @@ set -o pipefail
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 cd /tmp && export TMPDIR=/tmp
 ARGS="$*"   # the stats pass runs bench.py with these (default: its defaults)
-PMC_ARGS="--steps 100 --warmup 20 --profile-frames 4 --cpu-frames 0"
+PMC_ARGS="--cpu-frames 0"  # the bench defaults: same frames as the stats pass
 OUT="$ROOT/gpurun_out/prof"
 mkdir -p "$OUT"
 run() {  # name, timeout, rocprof args...
