@@ -215,6 +215,28 @@ int kfx_write_ply(const char *path, const float *xyz, int64_t n);
 /* extract (cap <= 0: KFX_DEFAULT_CLOUD_POINTS) + kfx_write_ply */
 int kfx_save_pointcloud(kfx_ctx *ctx, const char *path, int64_t cap);
 
+/* ---- dataset front-end (host only; no GPU needed) --------------------------
+ * depth_sensor in its DATASET build (depth_sensor.cpp:11-46 open, :186-196
+ * getFrame) without OpenCV: the PNG files of `<dir>/color` and `<dir>/depth` in
+ * sorted name order (cv::glob), `<dir>/intr.txt` = the 3x3 camera matrix of
+ * which the values > 0.1 are fx, cx, fy, cy, 1.  Frames come out as the
+ * reference feeds them to kinectfusion::pipeline: colour = imread(IMREAD_COLOR)
+ * (8-bit BGR: 16-bit samples keep the high byte, alpha dropped, grey
+ * replicated, palette expanded), depth = imread(IMREAD_UNCHANGED) converted to
+ * float (millimetres, one channel required).  Without intr.txt the camera is
+ * left 640x480 with zero focal lengths and has_intr = 0. */
+typedef struct kfx_dataset kfx_dataset;
+int kfx_dataset_open(const char *dir, kfx_dataset **out);
+int kfx_dataset_info(const kfx_dataset *ds, kfx_intrinsics *intr, int *n_frames, int *has_intr);
+int kfx_dataset_read(const kfx_dataset *ds, int index, uint8_t *bgr, float *depth_mm);
+int kfx_dataset_close(kfx_dataset *ds);
+/* The PNG decoder and intr.txt parse underneath (any PNG colour type / bit
+ * depth, Adam7, CRC-checked; sizes must match). */
+int kfx_png_info(const char *path, int *width, int *height, int *channels, int *bit_depth);
+int kfx_png_read_bgr8(const char *path, uint8_t *bgr, int width, int height);
+int kfx_png_read_depth(const char *path, float *depth, int width, int height);
+int kfx_parse_intr(const char *path, float out5[5]);
+
 /* ---- Z-slab sharding (new; the reference is single-GPU) -------------------
  * One kf::kinectfusion stream split over `world` GPUs: slab
  * `rank` owns global z slices [cut(rank), cut(rank+1)) of the volume, cut(r) =

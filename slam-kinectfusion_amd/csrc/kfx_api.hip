@@ -27,6 +27,14 @@ int set_err(int code, const std::string &msg) {
   return code;
 }
 
+}  // namespace
+
+namespace kfx {
+void set_error_text(const std::string &msg) { g_err = msg; }
+}  // namespace kfx
+
+namespace {
+
 #define HIPCHK(expr)                                                                      \
   do {                                                                                    \
     hipError_t e_ = (expr);                                                               \

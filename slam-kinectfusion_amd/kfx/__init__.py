@@ -18,7 +18,8 @@ import numpy as np
 from .abi import (KFX_FRAME_CUR, KFX_FRAME_PREV, KFX_OK, KFX_TRACKING_LOST, Intrinsics, Params, Pose,
                   default_params, fptr, i16ptr, i64ptr, u8ptr, u16ptr)
 
-__all__ = ["KinectFusion", "KfxError", "comm_unique_id", "pipeline_group", "write_ply", "lib", "build", "LIB_PATH", "Intrinsics", "Params", "Pose",
+__all__ = ["KinectFusion", "KfxError", "Dataset", "png_info", "png_read_bgr8", "png_read_depth", "parse_intr",
+           "comm_unique_id", "pipeline_group", "write_ply", "lib", "build", "LIB_PATH", "Intrinsics", "Params", "Pose",
            "default_params", "KFX_FRAME_CUR", "KFX_FRAME_PREV", "KFX_OK", "KFX_TRACKING_LOST", "EXPORTS"]
 
 _PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -34,6 +35,8 @@ EXPORTS = [
     "kfx_stage_icp", "kfx_stage_integrate", "kfx_stage_raycast", "kfx_set_profiling", "kfx_get_stage_ms",
     "kfx_integrate_counts", "kfx_integrate_stats", "kfx_create_slab", "kfx_slab_info", "kfx_comm_get_unique_id", "kfx_comm_init",
     "kfx_pipeline_group", "kfx_extract_points", "kfx_write_ply", "kfx_save_pointcloud",
+    "kfx_dataset_open", "kfx_dataset_info", "kfx_dataset_read", "kfx_dataset_close", "kfx_png_info",
+    "kfx_png_read_bgr8", "kfx_png_read_depth", "kfx_parse_intr",
 ]
 
 
@@ -103,6 +106,14 @@ def lib():
         "kfx_extract_points": ([vp, P(f), C.c_int64, P(C.c_int64)], i),
         "kfx_write_ply": ([C.c_char_p, P(f), C.c_int64], i),
         "kfx_save_pointcloud": ([vp, C.c_char_p, C.c_int64], i),
+        "kfx_dataset_open": ([C.c_char_p, P(vp)], i),
+        "kfx_dataset_info": ([vp, P(Intrinsics), P(i), P(i)], i),
+        "kfx_dataset_read": ([vp, i, P(C.c_uint8), P(f)], i),
+        "kfx_dataset_close": ([vp], i),
+        "kfx_png_info": ([C.c_char_p, P(i), P(i), P(i), P(i)], i),
+        "kfx_png_read_bgr8": ([C.c_char_p, P(C.c_uint8), i, i], i),
+        "kfx_png_read_depth": ([C.c_char_p, P(f), i, i], i),
+        "kfx_parse_intr": ([C.c_char_p, P(f)], i),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -122,6 +133,72 @@ def write_ply(path: str, xyz: np.ndarray):
     """kinectfusion::savePointcloud's ASCII PLY for an (N, 3) float32 array."""
     xyz = np.ascontiguousarray(xyz, np.float32)
     _check(lib().kfx_write_ply(path.encode(), fptr(xyz), xyz.shape[0]), "kfx_write_ply")
+
+
+def png_info(path: str) -> tuple:
+    """(width, height, channels, bit_depth) of a PNG file."""
+    w, h, c, b = C.c_int(), C.c_int(), C.c_int(), C.c_int()
+    _check(lib().kfx_png_info(path.encode(), C.byref(w), C.byref(h), C.byref(c), C.byref(b)), "kfx_png_info")
+    return w.value, h.value, c.value, b.value
+
+
+def png_read_bgr8(path: str) -> np.ndarray:
+    """imread(path, IMREAD_COLOR): (H, W, 3) uint8 BGR."""
+    w, h, _, _ = png_info(path)
+    out = np.empty((h, w, 3), np.uint8)
+    _check(lib().kfx_png_read_bgr8(path.encode(), out.ctypes.data_as(C.POINTER(C.c_uint8)), w, h),
+           "kfx_png_read_bgr8")
+    return out
+
+
+def png_read_depth(path: str) -> np.ndarray:
+    """imread(path, IMREAD_UNCHANGED).convertTo(CV_32F): (H, W) float32."""
+    w, h, _, _ = png_info(path)
+    out = np.empty((h, w), np.float32)
+    _check(lib().kfx_png_read_depth(path.encode(), fptr(out), w, h), "kfx_png_read_depth")
+    return out
+
+
+def parse_intr(path: str) -> tuple:
+    """intr.txt (depth_sensor.cpp:22-35): (fx, cx, fy, cy, c)."""
+    out = (C.c_float * 5)()
+    _check(lib().kfx_parse_intr(path.encode(), out), "kfx_parse_intr")
+    return tuple(out)
+
+
+class Dataset:
+    """depth_sensor's DATASET mode (depth_sensor.cpp:11-46, 186-196) over the C-ABI:
+    frames as kinectfusion::pipeline receives them (BGR uint8, depth float mm)."""
+
+    def __init__(self, path: str):
+        h = C.c_void_p()
+        _check(lib().kfx_dataset_open(path.encode(), C.byref(h)), "kfx_dataset_open")
+        self._h = h
+        intr, n, has = Intrinsics(), C.c_int(), C.c_int()
+        _check(lib().kfx_dataset_info(self._h, C.byref(intr), C.byref(n), C.byref(has)), "kfx_dataset_info")
+        self.intrinsics, self.n_frames, self.has_intr = intr, n.value, bool(has.value)
+
+    def __len__(self):
+        return self.n_frames
+
+    def read(self, index: int):
+        w, hgt = self.intrinsics.width, self.intrinsics.height
+        bgr = np.empty((hgt, w, 3), np.uint8)
+        dep = np.empty((hgt, w), np.float32)
+        _check(lib().kfx_dataset_read(self._h, int(index), bgr.ctypes.data_as(C.POINTER(C.c_uint8)), fptr(dep)),
+               "kfx_dataset_read")
+        return bgr, dep
+
+    def close(self):
+        if self._h:
+            lib().kfx_dataset_close(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def comm_unique_id() -> bytes:
