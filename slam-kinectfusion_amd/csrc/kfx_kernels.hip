@@ -1001,26 +1001,28 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *p, unsig
 }
 constexpr unsigned kOob = 0xFFFFFFFFu;
 
-// Voxel storage access of k_integrate: kIdx32 (local volume < 2^30 voxels)
-// uses buffer loads/stores with 32-bit byte offsets, else 64-bit pointers.
+// Voxel storage access of k_integrate: kIdx32 (local volume <= 2^31 voxels)
+// uses buffer loads/stores with 32-bit byte offsets for tsdf/weight (the
+// colour array, touched only in the colour band, through a 64-bit pointer),
+// else 64-bit pointers throughout.
 template <bool kIdx32>
 struct VoxMem;
 template <>
 struct VoxMem<true> {
   using Idx = unsigned;
-  __amdgpu_buffer_rsrc_t t, w, c;
-  __device__ VoxMem(const VolView &v) {
+  __amdgpu_buffer_rsrc_t t, w;
+  uint32_t *c;
+  __device__ VoxMem(const VolView &v) : c(v.rgb) {
     const size_t n = v.local_voxels();
-    t = make_rsrc(v.tsdf, (unsigned)(2 * n));
-    w = make_rsrc(v.weight, (unsigned)(2 * n));
-    c = make_rsrc(v.rgb, (unsigned)(4 * n));
+    t = make_rsrc(v.tsdf, (unsigned)min(2 * n, (size_t)0xFFFFFFFFu));
+    w = make_rsrc(v.weight, (unsigned)min(2 * n, (size_t)0xFFFFFFFFu));
   }
   __device__ int16_t ld_t(Idx i) const { return __builtin_amdgcn_raw_buffer_load_b16(t, i << 1, 0, 0); }
   __device__ int16_t ld_w(Idx i) const { return __builtin_amdgcn_raw_buffer_load_b16(w, i << 1, 0, 0); }
-  __device__ uint32_t ld_c(Idx i) const { return __builtin_amdgcn_raw_buffer_load_b32(c, i << 2, 0, 0); }
+  __device__ uint32_t ld_c(Idx i) const { return c[i]; }  // only for voxels that pass
   __device__ void st_t(Idx i, int16_t x) const { __builtin_amdgcn_raw_buffer_store_b16(x, t, i << 1, 0, 0); }
   __device__ void st_w(Idx i, int16_t x) const { __builtin_amdgcn_raw_buffer_store_b16(x, w, i << 1, 0, 0); }
-  __device__ void st_c(Idx i, uint32_t x) const { __builtin_amdgcn_raw_buffer_store_b32(x, c, i << 2, 0, 0); }
+  __device__ void st_c(Idx i, uint32_t x) const { c[i] = x; }
   static constexpr Idx kNone = 0x7FFFFFFFu;  // byte offsets past every buffer
 };
 template <>
@@ -2091,7 +2093,7 @@ void launch_integrate(hipStream_t s, VolView v, LevelGeom g0, const float2 *dl0,
   const int nchunk = std::max(1, std::min(KFX_INT_MAXCHUNK, (KFX_INT_WAVES + tiles - 1) / tiles));
   constexpr int wpb = KFX_INT_BLOCK / 64;  // waves (column tiles) per block
   dim3 grd((tiles + wpb - 1) / wpb, nchunk);
-  const bool idx32 = v.local_voxels() < (1ull << 30);
+  const bool idx32 = v.local_voxels() < (1ull << 31);  // 32-bit tsdf/weight byte offsets
 #ifdef KFX_INT_TRACE
   static unsigned long long *trace_buf = nullptr;
   if (!trace_buf) {
@@ -2128,8 +2130,9 @@ void launch_raycast(hipStream_t s, VolView v, int levels, const LevelGeom *g, Fr
   ra.levels = levels;
   for (int l = 0; l < levels; ++l) ra.g[l] = g[l];
   dim3 grd(((g[0].w + 15) / 16) * ((g[0].h + 15) / 16));
-  // 32-bit indices (24-bit tile * zn products)
-  const bool idx32 = v.local_voxels() < (1ull << 31) && (size_t)v.tiles_x * v.tiles_y * v.zn < (1ull << 24);
+  // 32-bit tsdf byte offsets (24-bit operands of the tile * zn products)
+  const bool idx32 = v.local_voxels() < (1ull << 31) && (size_t)v.tiles_x * v.tiles_y < (1ull << 24) &&
+                     v.zn < (1 << 24);
   if (keys) {
     if (idx32)
       hipLaunchKernelGGL((k_raycast<true, true>), grd, dim3(256), 0, s, v, ra, rc, cur, prev, st, log,

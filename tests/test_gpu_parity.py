@@ -147,13 +147,15 @@ def test_integrate_bit_exact_128(seq_qvga):
     kf.close()
 
 
-def test_integrate_512_column_spot_check(seq_vga):
-    """Full BASELINE size (512^3 @ 4 mm): GPU volume vs the oracle on 3000
-    sampled columns (the oracle restates any column independently)."""
+@pytest.mark.parametrize("n", [512, 1024])
+def test_integrate_512_column_spot_check(n, seq_vga):
+    """Full BASELINE sizes (C2 512^3 @ 4 mm; C3 1024^3 @ 2 mm, 2^30 voxels on
+    the 32-bit-offset path): GPU volume vs the oracle on 3000 sampled columns
+    (the oracle restates any column independently)."""
     bgr, dep, gt = seq_vga
     intr = synth.Intrinsics.vga()
     I = Intrinsics.from_any(intr)
-    kf, p = make(intr, dims=512)
+    kf, p = make(intr, dims=n)
     d = dep[0].astype(np.float32)
     kf.stage_preprocess(bgr[0], d)
     ds, _, _ = O.preprocess(d, I, p)
@@ -161,12 +163,12 @@ def test_integrate_512_column_spot_check(seq_vga):
     gu, gc = kf.stage_integrate(vol2cam)
     t, w, c = kf.volume_soa()
     rng = np.random.default_rng(5)
-    cols = np.stack([rng.integers(0, 512, 3000), rng.integers(0, 512, 3000)], 1).astype(np.int32)
-    cols = np.concatenate([cols, np.array([[256, 256], [0, 0], [511, 511], [255, 300]], np.int32)])
+    cols = np.stack([rng.integers(0, n, 3000), rng.integers(0, n, 3000)], 1).astype(np.int32)
+    cols = np.concatenate([cols, np.array([[n // 2, n // 2], [0, 0], [n - 1, n - 1], [n // 2 - 1, 300]], np.int32)])
     cols = np.unique(cols, axis=0)  # a repeated column would be integrated twice
-    vol = O.Volume((512,) * 3, (L_VOL,) * 3)
+    vol = O.Volume((n,) * 3, (L_VOL,) * 3)
     O.integrate(vol, p.volu_trun_dist, I, vol2cam, ds[0], bgr[0], cols=cols)
-    idx = (cols[:, 0][None, :] + 512 * cols[:, 1][None, :] + 512 * 512 * np.arange(512)[:, None]).ravel()
+    idx = (cols[:, 0][None, :] + n * cols[:, 1][None, :] + n * n * np.arange(n, dtype=np.int64)[:, None]).ravel()
     assert np.array_equal(t[idx], vol.tsdf[idx])
     assert np.array_equal(w[idx], vol.weight[idx])
     c4 = c.reshape(-1, 4)
