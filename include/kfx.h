@@ -199,6 +199,14 @@ int kfx_integrate_stats(kfx_ctx *ctx, int64_t out[8]);
 /* ---- point cloud ------------------------------------------ */
 /* TSDFVolume::fetchPointCloud buffer size (tsdf_volume.cpp:67) */
 #define KFX_DEFAULT_CLOUD_POINTS 10000000
+/* kinectfusion::getRenderMap (kinectfusion.cpp:33-47; kernel_renderPhong /
+ * kernel_renderNormals, image_process.cu:137-221): the previous frame's
+ * level-0 raycast maps shaded on the device, lit from the last pose's camera
+ * position; out = width*height uchar3, pixels without a surface 0. */
+#define KFX_RENDER_PHONG 0
+#define KFX_RENDER_NORMAL 1
+int kfx_render(kfx_ctx *ctx, int type, uint8_t *out);
+
 /* kinectfusion::extracePointcloud (kinectfusion.cpp:142-147) ->
  * TSDFVolume::fetchPointCloud (tsdf_volume.cpp:63-84) -> device::extract_points
  * (FullScan6, tsdf_volume.cu:307-499): zero crossings of the volume along +x,

@@ -705,6 +705,54 @@ int64_t kfo_extract_points(const int16_t *tsdf, const int16_t *weight, const int
   return n;
 }
 
+// kernel_renderNormals / kernel_renderPhong (image_process.cu:137-221) on the
+// previous frame's level-0 maps.  D: __fsqrt_rn and IEEE division for
+// __m_normalize's __fdividef (device_utils.cuh:50-54), pow(h, 10) as the
+// product chain h2 = h*h, h4 = h2*h2, h8 = h4*h4, h8*h2; the double promotion
+// of `0.5*light_coffi` is kept.  Pixels the kernel returns early on stay 0
+// (the zeroed cmap).  type 0 = PHONG, 1 = NORMAL; out = w*h uchar3.
+// (uchar)(x) of a value in [0, 255] (truncation); D: NaN (normals of the
+// frame-1 measured maps, A8) gives 0, as the GPU conversion does
+static uint8_t to_u8(float x) { return x >= 1.f ? (uint8_t)std::fmin(x, 255.f) : 0; }
+void kfo_render(const float *vmap, const float *nmap, int w, int h, const float eye[3], int type,
+                uint8_t *out) {
+  for (int i = 0; i < w * h; ++i) {
+    const V3 n = ld3(nmap, i), v = ld3(vmap, i);
+    uint8_t *o = out + 3 * (size_t)i;
+    o[0] = o[1] = o[2] = 0;
+    if (type == 1) {
+      o[0] = to_u8(std::fabs(n.x) * 255);
+      o[1] = to_u8(std::fabs(n.y) * 255);
+      o[2] = to_u8(std::fabs(n.z) * 255);
+      continue;
+    }
+    if (n.x == 0 && n.y == 0 && n.z == 0) continue;
+    if (v.x == 0 && v.y == 0 && v.z == 0) continue;
+    const V3 kd = {0.3843f, 0.4745f, 0.580f};
+    const V3 light = {500.f, 500.f, -500.f};
+    const float intensity = 0.9f;
+    const V3 e = normalized(sub({eye[0], eye[1], eye[2]}, v));
+    const V3 l = normalized(sub(light, v));
+    float lc = dot(n, l);
+    if (lc <= 0) lc = -lc;
+    float coef = intensity * lc;
+    const V3 diffuse = scl(kd, coef);
+    const V3 hv = normalized(add(l, e));
+    float hc = dot(n, hv);
+    if (hc < 0) hc = -hc;
+    const float h2 = hc * hc, h4 = h2 * h2, h8 = h4 * h4;
+    coef = intensity * (h8 * h2);
+    const double spec = 0.5 * (double)coef;
+    const float amb = 0.1f;
+    const float k0 = (float)std::fmin(1.0, (double)(amb + diffuse.x) + spec);
+    const float k1 = (float)std::fmin(1.0, (double)(amb + diffuse.y) + spec);
+    const float k2 = (float)std::fmin(1.0, (double)(amb + diffuse.z) + spec);
+    o[0] = to_u8(k0 * 255);
+    o[1] = to_u8(k1 * 255);
+    o[2] = to_u8(k2 * 255);
+  }
+}
+
 int kfo_format_pose(const kfx_pose *p, char *buf, int cap) {
   return std::snprintf(buf, cap,
                        "[%.8g, %.8g, %.8g, %.8g;\n %.8g, %.8g, %.8g, %.8g;\n %.8g, %.8g, "

@@ -106,6 +106,11 @@ int64_t kfo_extract_points(const int16_t *tsdf, const int16_t *weight, const int
                            const float vs[3], const kfx_pose *aff, int zlo, int zhi, float *out,
                            int64_t cap);
 
+/* renderPhong (type 0) / renderNormals (type 1), image_process.cu:137-221:
+ * w*h uchar3 from the level-0 vmap/nmap and the camera position. */
+void kfo_render(const float *vmap, const float *nmap, int w, int h, const float eye[3], int type,
+                uint8_t *out);
+
 typedef struct kfo_pipe kfo_pipe;
 kfo_pipe *kfo_pipe_create(const kfx_intrinsics *intr, const kfx_params *p);
 void kfo_pipe_destroy(kfo_pipe *pp);

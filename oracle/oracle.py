@@ -80,6 +80,8 @@ def lib():
         L.kfo_pipe_map.restype = P(f)
         L.kfo_pipe_last_counts.argtypes = [C.c_void_p, P(C.c_int64), P(C.c_int64)]
         L.kfo_format_pose.argtypes = [P(Pose), C.c_char_p, i]
+        L.kfo_render.argtypes = [P(f), P(f), i, i, P(f), i, P(C.c_uint8)]
+        L.kfo_render.restype = None
         _lib = L
     return _lib
 
@@ -269,6 +271,18 @@ def extract_points(vol: Volume, vpose: Pose, zlo: int = 0, zhi: int | None = Non
         lib().kfo_extract_points(i16ptr(t), i16ptr(w), vol.dims.ctypes.data_as(C.POINTER(C.c_int)),
                                  fptr(vol.voxel_size), C.byref(vpose), zlo, zhi, fptr(out), m)
     return out, n
+
+
+def render(vmap: np.ndarray, nmap: np.ndarray, eye, kind: str = "phong") -> np.ndarray:
+    """kfo_render: renderPhong / renderNormals of (H, W, 3) level-0 maps."""
+    h, w = vmap.shape[:2]
+    v = np.ascontiguousarray(vmap, np.float32)
+    n = np.ascontiguousarray(nmap, np.float32)
+    e = np.ascontiguousarray(eye, np.float32)
+    out = np.zeros((h, w, 3), np.uint8)
+    lib().kfo_render(fptr(v), fptr(n), w, h, fptr(e), 0 if kind == "phong" else 1,
+                     out.ctypes.data_as(C.POINTER(C.c_uint8)))
+    return out
 
 
 def ply_text(xyz: np.ndarray) -> str:

@@ -7,8 +7,7 @@
 // kfusion/src/{kinectfusion,icp_registration,tsdf_volume}.cpp and *.cu from the build and link
 // libkfx.so.  Needs OpenCV core (cv::Mat, cv::Affine3f); OpenCV-CUDA is no longer required.
 //
-// Display helpers (getRenderMap) are not on the hot path: they shade the downloaded raycast
-// maps on the host with the reference's formulas (image_process.cu:137-221).
+// getRenderMap shades the last raycast on the device (kfx_render, image_process.cu:137-221).
 #pragma once
 
 #include <opencv2/core.hpp>
@@ -134,33 +133,11 @@ class kinectfusion {
     kfx_reset(ctx_);
     sync_host_state();
   }
+  // kinectfusion.cpp:33-47: renderPhong / renderNormals (image_process.cu:137-221) on the device
   cv::Mat getRenderMap(DISPLAY_TYPES V = PHONG) {
-    const int w = intr_.width, h = intr_.height;
-    std::vector<float> v(3 * (size_t)w * h), n(3 * (size_t)w * h);
-    kfx_get_frame_maps(ctx_, KFX_FRAME_PREV, 0, nullptr, v.data(), n.data());
-    cv::Mat out(h, w, CV_8UC3, cv::Scalar(0, 0, 0));
-    const cv::Vec3f eye = pose_record.back().translation();
-    for (int y = 0; y < h; ++y)
-      for (int x = 0; x < w; ++x) {
-        const float *nv = &n[3 * ((size_t)y * w + x)], *vv = &v[3 * ((size_t)y * w + x)];
-        cv::Vec3b &px = out.at<cv::Vec3b>(y, x);
-        if (V == NORMAL) {  // image_process.cu:137-147
-          px = cv::Vec3b((uchar)(std::fabs(nv[0]) * 255), (uchar)(std::fabs(nv[1]) * 255),
-                         (uchar)(std::fabs(nv[2]) * 255));
-          continue;
-        }
-        // image_process.cu:159-211
-        if ((nv[0] == 0 && nv[1] == 0 && nv[2] == 0) || (vv[0] == 0 && vv[1] == 0 && vv[2] == 0)) continue;
-        cv::Vec3f nrm(nv[0], nv[1], nv[2]), vert(vv[0], vv[1], vv[2]);
-        cv::Vec3f e = cv::normalize(eye - vert), l = cv::normalize(cv::Vec3f(500.f, 500.f, -500.f) - vert);
-        const float lc = std::fabs(nrm.dot(l));
-        cv::Vec3f diffuse = cv::Vec3f(0.3843f, 0.4745f, 0.580f) * (0.9f * lc);
-        const float hc = std::fabs(nrm.dot(cv::normalize(l + e)));
-        const float spec = 0.5f * 0.9f * std::pow(hc, 10.f);
-        px = cv::Vec3b((uchar)(std::fmin(1.f, 0.1f + diffuse[0] + spec) * 255),
-                       (uchar)(std::fmin(1.f, 0.1f + diffuse[1] + spec) * 255),
-                       (uchar)(std::fmin(1.f, 0.1f + diffuse[2] + spec) * 255));
-      }
+    cv::Mat out(intr_.height, intr_.width, CV_8UC3);
+    if (kfx_render(ctx_, V == NORMAL ? KFX_RENDER_NORMAL : KFX_RENDER_PHONG, out.ptr<uint8_t>()) != KFX_OK)
+      throw std::runtime_error(kfx_last_error());
     return out;
   }
   // kinectfusion.cpp:142-147: 1 x N CV_32FC3 zero-crossing cloud (world frame),

@@ -145,6 +145,7 @@ struct kfx_ctx {
   // Z-slab sharding: this context owns slab `rank` of `world`
   bool slab = false;
   int rank = 0, world = 1;
+  uint8_t *render = nullptr;      // kfx_render output (allocated on first use)
   uint32_t *key_local = nullptr;  // per-pixel sample index of this slab's decisive event
   uint32_t *key_min = nullptr;    // all-reduce MIN of key_local over the slabs
   ncclComm_t comm = nullptr;      // RCCL communicator over the slab ranks (one process per GPU)
@@ -1177,6 +1178,19 @@ int kfx_stage_raycast(kfx_ctx *c, const kfx_pose *cam2vol, const float Rinv[9]) 
                  to_dev(c->p.volu_pose), c->xpose, c->slab ? c->key_local : nullptr);
   if (c->slab) launch_resize(c->stream, c->L, c->g, c->cur, c->prev, c->st, c->xpose);
   HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return KFX_OK;
+}
+
+int kfx_render(kfx_ctx *c, int type, uint8_t *out) {
+  int r = check_ctx(c);
+  if (r) return r;
+  if (!out || (type != KFX_RENDER_PHONG && type != KFX_RENDER_NORMAL)) return set_err(KFX_ERR_ARG, "bad argument");
+  const int n = c->g[0].w * c->g[0].h;
+  if (!c->render && (r = dalloc(c, (void **)&c->render, 3 * (size_t)n))) return r;
+  launch_render(c->stream, c->prev.v[0], c->prev.n[0], n, c->st, c->pose_log, type, c->render);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(out, c->render, 3 * (size_t)n, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   return KFX_OK;
 }

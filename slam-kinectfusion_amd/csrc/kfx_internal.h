@@ -142,6 +142,9 @@ void launch_raycast(hipStream_t s, VolView v, int levels, const LevelGeom *g, Fr
 void launch_resize(hipStream_t s, int levels, const LevelGeom *g, FrameView cur, FrameView prev,
                    const DevState *st, const float *xpose);
 // cross-slab combine: clear maps where the local key lost the MIN
+// renderPhong (type 0) / renderNormals (type 1) of the level-0 maps into w*h uchar3
+void launch_render(hipStream_t s, const float *vmap, const float *nmap, int n, const DevState *st,
+                   const DevPose *log, int type, uint8_t *out);
 void launch_slab_mask(hipStream_t s, const uint32_t *key_local, const uint32_t *key_min,
                       float *vmap, float *nmap, int n);
 constexpr int kMaxGroup = 16;

@@ -1966,6 +1966,52 @@ __global__ void k_export_soa(VolView v, int z0, int nz, int16_t *t, int16_t *w, 
   }
 }
 
+// kernel_renderNormals / kernel_renderPhong (image_process.cu:137-221) on the
+// previous frame's level-0 maps, lit from the last pose's camera position
+// (kinectfusion.cpp:33-47).  D as in the oracle (kfo_render): IEEE sqrt and
+// division in __m_normalize, pow(h, 10) as h8 * h2, NaN → 0 in the uchar
+// conversion; `0.5*light_coffi` stays double as in the source.
+__device__ __forceinline__ uint8_t render_u8(float x) { return x >= 1.f ? (uint8_t)fminf(x, 255.f) : 0; }
+__device__ __forceinline__ f3 normalized_ieee(f3 v) {
+  const float t = sqrtf(dot(v, v));
+  return {v.x / t, v.y / t, v.z / t};
+}
+__global__ __launch_bounds__(256) void k_render(const float *__restrict__ vmap, const float *__restrict__ nmap,
+                                                int n, const DevState *st, const DevPose *log, int type,
+                                                uint8_t *__restrict__ out) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const f3 nv = ld3(nmap, i), vv = ld3(vmap, i);
+  uint8_t o[3] = {0, 0, 0};
+  if (type == 1) {
+    o[0] = render_u8(fabsf(nv.x) * 255);
+    o[1] = render_u8(fabsf(nv.y) * 255);
+    o[2] = render_u8(fabsf(nv.z) * 255);
+  } else if (!(nv.x == 0 && nv.y == 0 && nv.z == 0) && !(vv.x == 0 && vv.y == 0 && vv.z == 0)) {
+    const DevPose &P = log[st->n_poses - 1];
+    const f3 kd = {0.3843f, 0.4745f, 0.580f};
+    const float intensity = 0.9f;
+    const f3 e = normalized_ieee(sub({P.t[0], P.t[1], P.t[2]}, vv));
+    const f3 l = normalized_ieee(sub({500.f, 500.f, -500.f}, vv));
+    float lc = dot(nv, l);
+    if (lc <= 0) lc = -lc;
+    float coef = intensity * lc;
+    const f3 diffuse = scl(kd, coef);
+    const f3 hv = normalized_ieee(add(l, e));
+    float hc = dot(nv, hv);
+    if (hc < 0) hc = -hc;
+    const float h2 = hc * hc, h4 = h2 * h2, h8 = h4 * h4;
+    coef = intensity * (h8 * h2);
+    const double spec = 0.5 * (double)coef;
+    o[0] = render_u8((float)fmin(1.0, (double)(0.1f + diffuse.x) + spec) * 255);
+    o[1] = render_u8((float)fmin(1.0, (double)(0.1f + diffuse.y) + spec) * 255);
+    o[2] = render_u8((float)fmin(1.0, (double)(0.1f + diffuse.z) + spec) * 255);
+  }
+  out[3 * (size_t)i] = o[0];
+  out[3 * (size_t)i + 1] = o[1];
+  out[3 * (size_t)i + 2] = o[2];
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -2156,6 +2202,11 @@ void launch_resize(hipStream_t s, int levels, const LevelGeom *g, FrameView cur,
   for (int l = 0; l < levels; ++l) ra.g[l] = g[l];
   dim3 grd(((g[0].w + 15) / 16) * ((g[0].h + 15) / 16));
   hipLaunchKernelGGL(k_resize, grd, dim3(256), 0, s, ra, cur, prev, st, xpose);
+}
+
+void launch_render(hipStream_t s, const float *vmap, const float *nmap, int n, const DevState *st,
+                   const DevPose *log, int type, uint8_t *out) {
+  hipLaunchKernelGGL(k_render, dim3((n + 255) / 256), dim3(256), 0, s, vmap, nmap, n, st, log, type, out);
 }
 
 void launch_slab_mask(hipStream_t s, const uint32_t *key_local, const uint32_t *key_min,

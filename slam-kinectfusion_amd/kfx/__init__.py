@@ -34,7 +34,7 @@ EXPORTS = [
     "kfx_upload_tsdf", "kfx_download_volume_soa", "kfx_stage_preprocess", "kfx_stage_icp_accumulate",
     "kfx_stage_icp", "kfx_stage_integrate", "kfx_stage_raycast", "kfx_set_profiling", "kfx_get_stage_ms",
     "kfx_integrate_counts", "kfx_integrate_stats", "kfx_create_slab", "kfx_slab_info", "kfx_comm_get_unique_id", "kfx_comm_init",
-    "kfx_pipeline_group", "kfx_extract_points", "kfx_write_ply", "kfx_save_pointcloud",
+    "kfx_pipeline_group", "kfx_render", "kfx_extract_points", "kfx_write_ply", "kfx_save_pointcloud",
     "kfx_dataset_open", "kfx_dataset_info", "kfx_dataset_read", "kfx_dataset_close", "kfx_png_info",
     "kfx_png_read_bgr8", "kfx_png_read_depth", "kfx_parse_intr",
 ]
@@ -104,6 +104,7 @@ def lib():
         "kfx_comm_init": ([vp, P(C.c_uint8)], i),
         "kfx_pipeline_group": ([P(vp), i, P(C.c_uint8), P(f)], i),
         "kfx_extract_points": ([vp, P(f), C.c_int64, P(C.c_int64)], i),
+        "kfx_render": ([vp, i, P(C.c_uint8)], i),
         "kfx_write_ply": ([C.c_char_p, P(f), C.c_int64], i),
         "kfx_save_pointcloud": ([vp, C.c_char_p, C.c_int64], i),
         "kfx_dataset_open": ([C.c_char_p, P(vp)], i),
@@ -354,6 +355,13 @@ class KinectFusion:
         a = (C.c_int64 * 8)()
         _check(lib().kfx_integrate_stats(self._h, a), "kfx_integrate_stats")
         return dict(zip(["updated", "colored", "visited", "gathered", "wave_batches"], a[:5]))
+
+    def render(self, kind: str = "phong") -> np.ndarray:
+        """getRenderMap(PHONG / NORMAL): (H, W, 3) uint8 from the last raycast."""
+        out = np.empty((self.intr.height, self.intr.width, 3), np.uint8)
+        _check(lib().kfx_render(self._h, 0 if kind == "phong" else 1, out.ctypes.data_as(C.POINTER(C.c_uint8))),
+               "kfx_render")
+        return out
 
     # ---- point cloud (kinectfusion::extracePointcloud / savePointcloud) ---
     def extract_points(self, cap: int = 10_000_000) -> np.ndarray:

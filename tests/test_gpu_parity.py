@@ -348,3 +348,22 @@ def test_full_size_pipeline_512(seq_vga):
     # A3 bias bounds accuracy to ~2 voxels (8 mm) against the analytic truth
     assert np.abs(gp[:, :3, 3] - gt[:n, :3, 3]).max() < 0.012
     kf.close()
+
+
+def test_render_matches_oracle(seq_qvga):
+    """getRenderMap(PHONG / NORMAL) on the device vs kfo_render on the same
+    previous-frame maps: after frame 1 (the measured maps, NaN normals) and
+    after tracking frames (raycast maps)."""
+    bgr, dep, gt = seq_qvga
+    intr = synth.Intrinsics.qvga()
+    kf, p = make(intr, dims=64)
+    for k in range(4):
+        kf.pipeline(bgr[k], dep[k].astype(np.float32))
+        _, v, n = kf.frame_maps(KFX_FRAME_PREV, 0)
+        eye = kf.pose_record[-1][:3, 3].astype(np.float32)
+        for kind in ("phong", "normal"):
+            got = kf.render(kind)
+            want = O.render(v, n, eye, kind)
+            assert np.array_equal(got, want), (k, kind, int((got != want).sum()))
+        assert (kf.render("phong") > 0).any()
+    kf.close()

@@ -357,3 +357,53 @@ def test_ply_text_format(oracle_lib):
     txt = oracle_lib.ply_text(np.array([[0.1, -2.5, 1234567.0], [1e-7, 0.0, 3.0]], np.float32))
     assert txt == ("ply\nformat ascii 1.0\nelement vertex 2\nproperty float x\nproperty float y\n"
                    "property float z\nend_header\n0.1 -2.5 1.23457e+06\n1e-07 0 3\n")
+
+
+def _render_ref(v, n, eye):
+    """numpy float32 restatement of renderPhong for one pixel (image_process.cu:159-211)."""
+    f = np.float32
+    v, n, eye = (np.asarray(a, f) for a in (v, n, eye))
+
+    def norm(a):
+        t = np.sqrt(f(f(a[0] * a[0]) + f(a[1] * a[1])) + f(a[2] * a[2]), dtype=f)
+        return np.array([a[0] / t, a[1] / t, a[2] / t], f)
+
+    def dot(a, b):
+        return f(f(f(a[0] * b[0]) + f(a[1] * b[1])) + f(a[2] * b[2]))
+    e = norm(eye - v)
+    li = norm(np.array([500, 500, -500], f) - v)
+    lc = abs(dot(n, li))
+    coef = f(f(0.9) * lc)
+    diff = np.array([0.3843, 0.4745, 0.580], f) * coef
+    h = norm(li + e)
+    hc = abs(dot(n, h))
+    h2 = f(hc * hc)
+    h4 = f(h2 * h2)
+    h8 = f(h4 * h4)
+    spec = 0.5 * float(f(f(0.9) * f(h8 * h2)))
+    k = [f(min(1.0, float(f(f(0.1) + d)) + spec)) for d in diff]
+    return [int(x * f(255)) if x >= 1 / 255 else 0 for x in k]
+
+
+def test_render_kat(oracle_lib):
+    """renderPhong / renderNormals (image_process.cu:137-221): hand-restated
+    pixels, the early returns (zero normal or vertex stay 0) and NaN normals."""
+    rng = np.random.default_rng(3)
+    h, w = 4, 5
+    v = rng.uniform(-1, 1, (h, w, 3)).astype(np.float32)
+    v[..., 2] += 2
+    n = rng.normal(size=(h, w, 3)).astype(np.float32)
+    n /= np.linalg.norm(n, axis=2, keepdims=True)
+    n[0, 0] = 0          # zero normal: early return
+    v[0, 1] = 0          # zero vertex: early return
+    n[1, 1] = np.nan     # NaN normal (frame-1 measured maps)
+    eye = np.array([0.1, -0.2, 0.3], np.float32)
+    ph = oracle_lib.render(v, n, eye, "phong")
+    nm = oracle_lib.render(v, n, eye, "normal")
+    assert (ph[0, 0] == 0).all() and (ph[0, 1] == 0).all() and (nm[1, 1] == 0).all()
+    for y in range(h):
+        for x in range(w):
+            if (y, x) in ((0, 0), (0, 1), (1, 1)):
+                continue
+            assert list(ph[y, x]) == _render_ref(v[y, x], n[y, x], eye), (y, x)
+            assert list(nm[y, x]) == [int(np.float32(abs(c)) * np.float32(255)) for c in n[y, x]]
