@@ -207,6 +207,13 @@ int kfx_integrate_stats(kfx_ctx *ctx, int64_t out[8]);
 #define KFX_RENDER_NORMAL 1
 int kfx_render(kfx_ctx *ctx, int type, uint8_t *out);
 
+/* Order-free checksum of the (owned part of the) volume: out[0] = sum mod
+ * 2^64 of a 64-bit mix of (x-fastest global voxel index, tsdf, weight,
+ * colour) over every voxel, out[1] = voxels with weight > 0.  The sums of a
+ * volume's Z-slabs equal the single volume's: a full-size property check
+ * without downloading the volume. */
+int kfx_volume_checksum(kfx_ctx *ctx, uint64_t out[2]);
+
 /* kinectfusion::extracePointcloud (kinectfusion.cpp:142-147) ->
  * TSDFVolume::fetchPointCloud (tsdf_volume.cpp:63-84) -> device::extract_points
  * (FullScan6, tsdf_volume.cu:307-499): zero crossings of the volume along +x,

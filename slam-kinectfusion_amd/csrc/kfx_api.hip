@@ -1182,6 +1182,21 @@ int kfx_stage_raycast(kfx_ctx *c, const kfx_pose *cam2vol, const float Rinv[9]) 
   return KFX_OK;
 }
 
+int kfx_volume_checksum(kfx_ctx *c, uint64_t out[2]) {
+  int r = check_ctx(c);
+  if (r) return r;
+  if (!out) return set_err(KFX_ERR_ARG, "null out");
+  HIPCHK(hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * 2, c->stream));
+  launch_checksum(c->stream, c->vol, c->counters);
+  HIPCHK(hipGetLastError());
+  unsigned long long h[2];
+  HIPCHK(hipMemcpyAsync(h, c->counters, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  out[0] = h[0];
+  out[1] = h[1];
+  return KFX_OK;
+}
+
 int kfx_render(kfx_ctx *c, int type, uint8_t *out) {
   int r = check_ctx(c);
   if (r) return r;

@@ -142,6 +142,8 @@ void launch_raycast(hipStream_t s, VolView v, int levels, const LevelGeom *g, Fr
 void launch_resize(hipStream_t s, int levels, const LevelGeom *g, FrameView cur, FrameView prev,
                    const DevState *st, const float *xpose);
 // cross-slab combine: clear maps where the local key lost the MIN
+// out[0] += sum of per-voxel hashes, out[1] += voxels with weight > 0 (owned slices)
+void launch_checksum(hipStream_t s, VolView v, unsigned long long *out);
 // renderPhong (type 0) / renderNormals (type 1) of the level-0 maps into w*h uchar3
 void launch_render(hipStream_t s, const float *vmap, const float *nmap, int n, const DevState *st,
                    const DevPose *log, int type, uint8_t *out);

@@ -1952,6 +1952,38 @@ __global__ void k_import_records(VolView v, int z0, int nz, const uint64_t *src)
   }
 }
 
+// Order-free volume checksum over the owned slices: sum of a 64-bit mix of
+// (global x-fastest index, tsdf, weight, colour) per voxel, and the count of
+// voxels with weight > 0 — slab sums add up to the single volume's.
+__device__ __forceinline__ unsigned long long mix64(unsigned long long z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__global__ __launch_bounds__(256) void k_checksum(VolView v, unsigned long long *out) {
+  const size_t n = v.local_voxels(), per_tile = v.tile_voxels();
+  unsigned long long h = 0, cnt = 0;
+  for (size_t li = (size_t)blockIdx.x * 256 + threadIdx.x; li < n; li += (size_t)gridDim.x * 256) {
+    const size_t tile = li / per_tile, rem = li % per_tile;
+    const int z = v.zb + (int)(rem >> 6), inner = (int)(rem & 63);
+    if (z < v.own0 || z >= v.own1) continue;
+    const int x = (int)(tile % v.tiles_x) * 8 + (inner & 7), y = (int)(tile / v.tiles_x) * 8 + (inner >> 3);
+    const unsigned long long g = (unsigned long long)x + (unsigned long long)v.X * ((unsigned long long)y + (unsigned long long)v.Y * z);
+    const unsigned long long rec = ((unsigned long long)(uint16_t)v.tsdf[li] << 48) |
+                                   ((unsigned long long)(uint16_t)v.weight[li] << 32) | (v.rgb[li] & 0xffffffu);
+    h += mix64(g * 0x9E3779B97F4A7C15ull ^ rec);
+    cnt += v.weight[li] > 0;
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    h += __shfl_xor(h, off);
+    cnt += __shfl_xor(cnt, off);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicAdd(&out[0], h);
+    atomicAdd(&out[1], cnt);
+  }
+}
+
 __global__ void k_export_soa(VolView v, int z0, int nz, int16_t *t, int16_t *w, uint32_t *c) {
   const size_t n = v.slice * (size_t)nz;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
@@ -2277,6 +2309,10 @@ void launch_export_records(hipStream_t s, VolView v, int z0, int nz, uint64_t *d
 void launch_import_records(hipStream_t s, VolView v, int z0, int nz, const uint64_t *src) {
   hipLaunchKernelGGL(k_import_records, slab_grid(v, nz), dim3(256), 0, s, v, z0, nz, src);
 }
+void launch_checksum(hipStream_t s, VolView v, unsigned long long *out) {
+  hipLaunchKernelGGL(k_checksum, dim3(2048), dim3(256), 0, s, v, out);
+}
+
 void launch_export_soa(hipStream_t s, VolView v, int z0, int nz, int16_t *t, int16_t *w,
                        uint32_t *c) {
   hipLaunchKernelGGL(k_export_soa, slab_grid(v, nz), dim3(256), 0, s, v, z0, nz, t, w, c);

@@ -34,7 +34,7 @@ EXPORTS = [
     "kfx_upload_tsdf", "kfx_download_volume_soa", "kfx_stage_preprocess", "kfx_stage_icp_accumulate",
     "kfx_stage_icp", "kfx_stage_integrate", "kfx_stage_raycast", "kfx_set_profiling", "kfx_get_stage_ms",
     "kfx_integrate_counts", "kfx_integrate_stats", "kfx_create_slab", "kfx_slab_info", "kfx_comm_get_unique_id", "kfx_comm_init",
-    "kfx_pipeline_group", "kfx_render", "kfx_extract_points", "kfx_write_ply", "kfx_save_pointcloud",
+    "kfx_pipeline_group", "kfx_render", "kfx_volume_checksum", "kfx_extract_points", "kfx_write_ply", "kfx_save_pointcloud",
     "kfx_dataset_open", "kfx_dataset_info", "kfx_dataset_read", "kfx_dataset_close", "kfx_png_info",
     "kfx_png_read_bgr8", "kfx_png_read_depth", "kfx_parse_intr",
 ]
@@ -105,6 +105,7 @@ def lib():
         "kfx_pipeline_group": ([P(vp), i, P(C.c_uint8), P(f)], i),
         "kfx_extract_points": ([vp, P(f), C.c_int64, P(C.c_int64)], i),
         "kfx_render": ([vp, i, P(C.c_uint8)], i),
+        "kfx_volume_checksum": ([vp, P(C.c_uint64)], i),
         "kfx_write_ply": ([C.c_char_p, P(f), C.c_int64], i),
         "kfx_save_pointcloud": ([vp, C.c_char_p, C.c_int64], i),
         "kfx_dataset_open": ([C.c_char_p, P(vp)], i),
@@ -355,6 +356,12 @@ class KinectFusion:
         a = (C.c_int64 * 8)()
         _check(lib().kfx_integrate_stats(self._h, a), "kfx_integrate_stats")
         return dict(zip(["updated", "colored", "visited", "gathered", "wave_batches"], a[:5]))
+
+    def volume_checksum(self) -> tuple:
+        """(hash sum mod 2^64, voxels with weight > 0) over the owned slices."""
+        out = (C.c_uint64 * 2)()
+        _check(lib().kfx_volume_checksum(self._h, out), "kfx_volume_checksum")
+        return int(out[0]), int(out[1])
 
     def render(self, kind: str = "phong") -> np.ndarray:
         """getRenderMap(PHONG / NORMAL): (H, W, 3) uint8 from the last raycast."""

@@ -138,3 +138,67 @@ def test_slab_rccl_single_rank_matches(graph, seq_qvga):
     _compare(single, [m])
     m.close()
     single.close()
+
+
+M64 = (1 << 64) - 1
+
+
+def _np_checksum(t, w, c, X, Y, z0, z1):
+    """numpy restatement of kfx_volume_checksum over slices [z0, z1) of an
+    x-fastest SoA volume (the property: order-free, additive over slabs)."""
+    s = slice(z0 * X * Y, z1 * X * Y)
+    g = np.arange(z0 * X * Y, z1 * X * Y, dtype=np.uint64)
+    c4 = c.reshape(-1, 4)[s].astype(np.uint64)
+    rec = ((t[s].view(np.uint16).astype(np.uint64) << np.uint64(48)) |
+           (w[s].view(np.uint16).astype(np.uint64) << np.uint64(32)) |
+           c4[:, 0] | (c4[:, 1] << np.uint64(8)) | (c4[:, 2] << np.uint64(16)))
+    with np.errstate(over="ignore"):
+        z = (g * np.uint64(0x9E3779B97F4A7C15)) ^ rec
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    return int(z.sum(dtype=np.uint64)), int((w[s] > 0).sum())
+
+
+def test_volume_checksum_adds_over_slabs(seq_qvga):
+    bgr, dep, _ = seq_qvga
+    intr = synth.Intrinsics.qvga()
+    p = default_params(dims=64, range_m=L_VOL)
+    single, st = _single(intr, p, bgr, dep)
+    t, w, c = single.volume_soa()
+    want = _np_checksum(t, w, c, 64, 64, 0, 64)
+    assert single.volume_checksum() == want and want[1] > 0
+    members = [KinectFusion(Intrinsics.from_any(intr), p, slab=(r, 3)) for r in range(3)]
+    for k in range(len(dep)):
+        pipeline_group(members, bgr[k], dep[k].astype(np.float32))
+    sums = [m.volume_checksum() for m in members]
+    assert (sum(s[0] for s in sums) & M64, sum(s[1] for s in sums)) == want
+    for m in members:
+        m.close()
+    single.close()
+
+
+def test_c5_full_size_slabs_on_one_gpu():
+    """C5 shape (1280x720, 2048^3 @ 2 mm = 64 GiB) as 8 Z-slabs held on one
+    GPU (288 GB): poses, the combined model maps and the volume checksum of
+    the 8 slabs equal the single 2048^3 volume's, frame by frame."""
+    intr = synth.Intrinsics.hd720()
+    L = 4.096
+    bgr, dep, _ = synth.sequence(3, intr, L=L, noise=True, dropout=0.005)
+    p = default_params(dims=2048, range_m=L)
+    single, st = _single(intr, p, bgr, dep)
+    ref = single.volume_checksum()
+    _, gv, gn = single.frame_maps(KFX_FRAME_PREV, 0)
+    poses = single.pose_record
+    single.close()  # 64 GiB back before the slabs allocate theirs
+    members = [KinectFusion(Intrinsics.from_any(intr), p, slab=(r, 8)) for r in range(8)]
+    gst = [pipeline_group(members, bgr[k], dep[k].astype(np.float32)) for k in range(len(dep))]
+    assert gst == st == [KFX_OK] * len(dep)
+    sums = [m.volume_checksum() for m in members]
+    assert (sum(s[0] for s in sums) & M64, sum(s[1] for s in sums)) == ref and ref[1] > 10**7
+    for m in members:
+        assert np.array_equal(m.pose_record, poses)
+        _, mv, mn = m.frame_maps(KFX_FRAME_PREV, 0)
+        assert bits_equal(mv, gv) and bits_equal(mn, gn)
+    for m in members:
+        m.close()
