@@ -230,6 +230,19 @@ int kfx_write_ply(const char *path, const float *xyz, int64_t n);
 /* extract (cap <= 0: KFX_DEFAULT_CLOUD_POINTS) + kfx_write_ply */
 int kfx_save_pointcloud(kfx_ctx *ctx, const char *path, int64_t cap);
 
+/* Marching-cubes mesh of the zero level set (C5 asks for a mesh;
+ * the reference has no counterpart).  A cube is 8 neighbouring voxels, all
+ * with weight > 0; corners with tsdf < 0 are inside; the triangle table is
+ * derived at run time (each face cuts off every run of inside corners, so
+ * ambiguous faces resolve the same way from both sides: a crack-free mesh).
+ * Edge vertices interpolate voxel centres as the point cloud does, in world
+ * coordinates.  Triangles are 9 floats (3 vertices), in the point cloud's
+ * canonical order; writes min(cap, total), *n_tris = total.  A slab meshes
+ * its owned cubes: slab meshes concatenate to the single volume's. */
+int kfx_extract_mesh(kfx_ctx *ctx, float *tri_xyz, int64_t cap_tris, int64_t *n_tris);
+/* ASCII PLY of a triangle soup: 3n vertices (%g), n faces "3 i j k". */
+int kfx_write_ply_mesh(const char *path, const float *tri_xyz, int64_t n_tris);
+
 /* ---- dataset front-end (host only; no GPU needed) --------------------------
  * depth_sensor in its DATASET build (depth_sensor.cpp:11-46 open, :186-196
  * getFrame) without OpenCV: the PNG files of `<dir>/color` and `<dir>/depth` in

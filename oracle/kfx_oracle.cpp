@@ -6,6 +6,7 @@
 // "D" = a defined deviation from the CUDA original.
 #include "kfx_oracle.h"
 
+#include <algorithm>
 #include <climits>
 #include <cmath>
 #include <cstdio>
@@ -700,6 +701,123 @@ int64_t kfo_extract_points(const int16_t *tsdf, const int16_t *weight, const int
                   if (n < cap) st3(out, n, add(rmul(aff->R, p), t));
                   ++n;
                 }
+              }
+            }
+  return n;
+}
+
+// Marching cubes (D, no reference counterpart).  Table: for
+// every corner pattern, each face (corner cycle counter-clockwise seen from
+// outside) links the edge where a run of inside corners begins to the edge
+// where it ends; following the links gives closed loops over the cut edges,
+// each fanned from its smallest edge.  Edge numbering: axis-major, within an
+// axis by ascending lower corner (corner bits x | y<<1 | z<<2).
+void kfo_mc_table(uint8_t *tab) {
+  int ends[12][2];
+  int ne = 0;
+  for (int axis = 0; axis < 3; ++axis)
+    for (int corner = 0; corner < 8; ++corner)
+      if (((corner >> axis) & 1) == 0) {
+        ends[ne][0] = corner;
+        ends[ne][1] = corner + (1 << axis);
+        ne++;
+      }
+  auto edge_of = [&](int p, int q) {
+    const int a = std::min(p, q), b = std::max(p, q);
+    for (int e = 0; e < 12; e++)
+      if (ends[e][0] == a && ends[e][1] == b) return e;
+    return -1;
+  };
+  std::vector<std::vector<int>> faces;
+  for (int axis = 0; axis < 3; axis++) {
+    const int u = (axis + 1) % 3, w = (axis + 2) % 3;
+    for (int side = 0; side < 2; side++) {
+      std::vector<int> f = {side << axis, (side << axis) | (1 << u), (side << axis) | (1 << u) | (1 << w),
+                            (side << axis) | (1 << w)};  // CCW about +e_axis
+      if (side == 0) std::reverse(f.begin(), f.end());
+      faces.push_back(f);
+    }
+  }
+  for (int pat = 0; pat < 256; pat++) {
+    auto in = [&](int corner) { return ((pat >> corner) & 1) != 0; };
+    std::vector<int> link(12, -1);
+    for (const auto &f : faces)
+      for (int i = 0; i < 4; i++) {
+        const int prev = f[(i + 3) % 4], cur = f[i];
+        if (!in(cur) || in(prev)) continue;
+        int last = i;
+        while (in(f[(last + 1) % 4])) last = (last + 1) % 4;
+        link[edge_of(prev, cur)] = edge_of(f[last], f[(last + 1) % 4]);
+      }
+    std::vector<int> tris;
+    std::vector<bool> used(12, false);
+    for (int e0 = 0; e0 < 12; e0++) {
+      if (link[e0] < 0 || used[e0]) continue;
+      std::vector<int> loop;
+      int e = e0;
+      do {
+        used[e] = true;
+        loop.push_back(e);
+        e = link[e];
+      } while (e != e0);
+      for (size_t k = 1; k + 1 < loop.size(); k++) {
+        tris.push_back(loop[0]);
+        tris.push_back(loop[k]);
+        tris.push_back(loop[k + 1]);
+      }
+    }
+    uint8_t *row = tab + 16 * pat;
+    std::fill(row, row + 16, (uint8_t)0);
+    row[0] = (uint8_t)(tris.size() / 3);
+    for (size_t k = 0; k < tris.size(); k++) row[1 + k] = (uint8_t)tris[k];
+  }
+}
+
+int64_t kfo_extract_mesh(const int16_t *tsdf, const int16_t *weight, const int dims[3], const float vs[3],
+                         const kfx_pose *aff, int zlo, int zhi, float *out, int64_t cap) {
+  uint8_t tab[256 * 16];
+  kfo_mc_table(tab);
+  const int X = dims[0], Y = dims[1];
+  const int64_t slice = (int64_t)X * Y;
+  auto idx = [&](int x, int y, int z) { return (int64_t)x + (int64_t)y * X + (int64_t)z * slice; };
+  const V3 t = {aff->t[0], aff->t[1], aff->t[2]};
+  int64_t n = 0;
+  for (int c0 = (zlo / 8) * 8; c0 < zhi; c0 += 8)
+    for (int ty = 0; ty < Y / 8; ++ty)
+      for (int tx = 0; tx < X / 8; ++tx)
+        for (int z = std::max(zlo, c0); z < std::min(zhi, c0 + 8); ++z)
+          for (int yy = 0; yy < 8; ++yy)
+            for (int xx = 0; xx < 8; ++xx) {
+              const int x = tx * 8 + xx, y = ty * 8 + yy;
+              if (x + 1 >= X || y + 1 >= Y) continue;
+              float F[8];
+              int pat = 0;
+              bool ok = true;
+              for (int c = 0; c < 8; c++) {
+                const int64_t i = idx(x + (c & 1), y + ((c >> 1) & 1), z + (c >> 2));
+                ok = ok && weight[i] > 0;
+                F[c] = (float)tsdf[i] * kDivShortMax;
+                if (F[c] < 0.f) pat |= 1 << c;
+              }
+              if (!ok) continue;
+              const uint8_t *row = tab + 16 * pat;
+              for (int k = 0; k < 3 * row[0]; k++, n += (k % 3 == 0)) {
+                if (n >= cap) continue;
+                const int e = row[1 + k], axis = e / 4;
+                int lo = -1;  // lower corner: the (e%4)-th corner with the axis bit clear
+                for (int c = 0, m = 0; c < 8; c++)
+                  if (!((c >> axis) & 1) && m++ == e % 4) lo = c;
+                const int hi = lo | (1 << axis);
+                V3 p = {((float)(x + (lo & 1)) + 0.5f) * vs[0], ((float)(y + ((lo >> 1) & 1)) + 0.5f) * vs[1],
+                        ((float)(z + (lo >> 2)) + 0.5f) * vs[2]};
+                const float Va = axis == 0 ? p.x : (axis == 1 ? p.y : p.z);
+                const float Vn = Va + vs[axis];
+                const float d_inv = 1.f / (std::fabs(F[lo]) + std::fabs(F[hi]));
+                const float cc = (Va * std::fabs(F[hi]) + Vn * std::fabs(F[lo])) * d_inv;
+                if (axis == 0) p.x = cc;
+                else if (axis == 1) p.y = cc;
+                else p.z = cc;
+                st3(out, 3 * n + k % 3, add(rmul(aff->R, p), t));
               }
             }
   return n;

@@ -106,6 +106,13 @@ int64_t kfo_extract_points(const int16_t *tsdf, const int16_t *weight, const int
                            const float vs[3], const kfx_pose *aff, int zlo, int zhi, float *out,
                            int64_t cap);
 
+/* Marching cubes: 256 x 16 table {n_tri, 3 n_tri edges}; triangle soup of the
+ * zero level set over cubes z in [zlo, zhi) in the canonical order (9 floats
+ * per triangle; writes min(cap, total), returns total). */
+void kfo_mc_table(uint8_t *tab);
+int64_t kfo_extract_mesh(const int16_t *tsdf, const int16_t *weight, const int dims[3], const float vs[3],
+                         const kfx_pose *aff, int zlo, int zhi, float *out, int64_t cap);
+
 /* renderPhong (type 0) / renderNormals (type 1), image_process.cu:137-221:
  * w*h uchar3 from the level-0 vmap/nmap and the camera position. */
 void kfo_render(const float *vmap, const float *nmap, int w, int h, const float eye[3], int type,

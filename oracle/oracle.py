@@ -81,6 +81,10 @@ def lib():
         L.kfo_pipe_last_counts.argtypes = [C.c_void_p, P(C.c_int64), P(C.c_int64)]
         L.kfo_format_pose.argtypes = [P(Pose), C.c_char_p, i]
         L.kfo_render.argtypes = [P(f), P(f), i, i, P(f), i, P(C.c_uint8)]
+        L.kfo_mc_table.argtypes = [P(C.c_uint8)]
+        L.kfo_mc_table.restype = None
+        L.kfo_extract_mesh.argtypes = [P(C.c_int16), P(C.c_int16), P(i), P(f), P(Pose), i, i, P(f), C.c_int64]
+        L.kfo_extract_mesh.restype = C.c_int64
         L.kfo_render.restype = None
         _lib = L
     return _lib
@@ -270,6 +274,30 @@ def extract_points(vol: Volume, vpose: Pose, zlo: int = 0, zhi: int | None = Non
     if m:
         lib().kfo_extract_points(i16ptr(t), i16ptr(w), vol.dims.ctypes.data_as(C.POINTER(C.c_int)),
                                  fptr(vol.voxel_size), C.byref(vpose), zlo, zhi, fptr(out), m)
+    return out, n
+
+
+def mc_table() -> np.ndarray:
+    """(256, 16) uint8: {n_tri, 3 n_tri edge indices} per corner pattern."""
+    t = np.zeros((256, 16), np.uint8)
+    lib().kfo_mc_table(t.ctypes.data_as(C.POINTER(C.c_uint8)))
+    return t
+
+
+def extract_mesh(vol: Volume, vpose: Pose, zlo: int = 0, zhi: int | None = None, cap: int = 50_000_000,
+                 tsdf: np.ndarray | None = None, weight: np.ndarray | None = None):
+    """Marching-cubes triangles (canonical order), (N, 3, 3) float32, and the total."""
+    Z = int(vol.dims[2])
+    zhi = Z - 1 if zhi is None else zhi
+    t = np.ascontiguousarray(vol.tsdf if tsdf is None else tsdf, np.int16)
+    w = np.ascontiguousarray(vol.weight if weight is None else weight, np.int16)
+    dims = vol.dims.ctypes.data_as(C.POINTER(C.c_int))
+    n = lib().kfo_extract_mesh(i16ptr(t), i16ptr(w), dims, fptr(vol.voxel_size), C.byref(vpose), zlo, zhi, None, 0)
+    m = min(n, cap)
+    out = np.zeros((m, 3, 3), np.float32)
+    if m:
+        lib().kfo_extract_mesh(i16ptr(t), i16ptr(w), dims, fptr(vol.voxel_size), C.byref(vpose), zlo, zhi,
+                               fptr(out), m)
     return out, n
 
 

@@ -146,6 +146,7 @@ struct kfx_ctx {
   bool slab = false;
   int rank = 0, world = 1;
   uint8_t *render = nullptr;      // kfx_render output (allocated on first use)
+  uint8_t *mc_tab = nullptr;      // marching-cubes table (uploaded on first use)
   uint32_t *key_local = nullptr;  // per-pixel sample index of this slab's decisive event
   uint32_t *key_min = nullptr;    // all-reduce MIN of key_local over the slabs
   ncclComm_t comm = nullptr;      // RCCL communicator over the slab ranks (one process per GPU)
@@ -1253,6 +1254,134 @@ int kfx_extract_points(kfx_ctx *c, float *xyz, int64_t cap, int64_t *n_points) {
     if (e != hipSuccess) return set_err(KFX_ERR_HIP, std::string("extract_points: ") + hipGetErrorString(e));
   }
   if (n_points) *n_points = total;
+  return KFX_OK;
+}
+
+// Marching-cubes triangle table, derived instead of typed in: for each of the
+// 256 inside/outside corner patterns, every cube face contributes one segment
+// per run of inside corners along its cycle (counter-clockwise seen from
+// outside), from the edge entering the run to the edge leaving it — so on an
+// ambiguous face the two inside corners are cut off separately, the same way
+// from both cubes sharing the face (no cracks).  Each cut edge then starts one
+// segment and ends one; the segments close into loops, each loop is fanned
+// from its smallest edge index.  At most 5 triangles per cube.
+static void build_mc_table(uint8_t tab[256 * 16]) {
+  int lo[12], hi[12], n = 0;
+  for (int a = 0; a < 3; ++a)
+    for (int c = 0; c < 8; ++c)
+      if (!((c >> a) & 1)) {
+        lo[n] = c;
+        hi[n] = c | (1 << a);
+        ++n;
+      }
+  auto eid = [&](int u, int v) {
+    for (int e = 0; e < 12; ++e)
+      if ((lo[e] == u && hi[e] == v) || (lo[e] == v && hi[e] == u)) return e;
+    return -1;
+  };
+  int cyc[6][4];
+  for (int a = 0, f = 0; a < 3; ++a) {
+    const int b = (a + 1) % 3, c = (a + 2) % 3;
+    static const int pb[4] = {0, 1, 1, 0}, pc[4] = {0, 0, 1, 1};
+    for (int s = 0; s < 2; ++s, ++f)
+      for (int i = 0; i < 4; ++i) {
+        const int k = s ? i : 3 - i;  // the x=0 / y=0 / z=0 face reversed: outward normal -e_a
+        cyc[f][i] = (s << a) | (pb[k] << b) | (pc[k] << c);
+      }
+  }
+  std::memset(tab, 0, 256 * 16);
+  for (int cfg = 0; cfg < 256; ++cfg) {
+    int nxt[12];
+    for (int &x : nxt) x = -1;
+    for (int f = 0; f < 6; ++f) {
+      bool ins[4];
+      for (int i = 0; i < 4; ++i) ins[i] = (cfg >> cyc[f][i]) & 1;
+      for (int i = 0; i < 4; ++i) {
+        if (!ins[i] || ins[(i + 3) % 4]) continue;  // start of a run of inside corners
+        int j = i;
+        while (ins[(j + 1) % 4]) j = (j + 1) % 4;
+        nxt[eid(cyc[f][(i + 3) % 4], cyc[f][i])] = eid(cyc[f][j], cyc[f][(j + 1) % 4]);
+      }
+    }
+    bool seen[12] = {};
+    int nt = 0;
+    for (int s = 0; s < 12; ++s) {
+      if (nxt[s] < 0 || seen[s]) continue;
+      int loop[12], m = 0;
+      for (int e = s; !seen[e]; e = nxt[e]) {
+        seen[e] = true;
+        loop[m++] = e;
+      }
+      for (int k = 1; k + 1 < m; ++k, ++nt) {
+        tab[16 * cfg + 1 + 3 * nt] = (uint8_t)loop[0];
+        tab[16 * cfg + 2 + 3 * nt] = (uint8_t)loop[k];
+        tab[16 * cfg + 3 + 3 * nt] = (uint8_t)loop[k + 1];
+      }
+    }
+    tab[16 * cfg] = (uint8_t)nt;
+  }
+}
+
+int kfx_extract_mesh(kfx_ctx *c, float *tri_xyz, int64_t cap, int64_t *n_tris) {
+  int r = check_ctx(c);
+  if (r) return r;
+  if (cap < 0 || (cap > 0 && !tri_xyz)) return set_err(KFX_ERR_ARG, "bad triangle buffer");
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (!c->mc_tab) {
+    uint8_t tab[256 * 16];
+    build_mc_table(tab);
+    if ((r = dalloc(c, (void **)&c->mc_tab, sizeof(tab)))) return r;
+    HIPCHK(hipMemcpy(c->mc_tab, tab, sizeof(tab), hipMemcpyHostToDevice));
+  }
+  // cubes z .. z+1 for z in the owned slices below Z-1
+  const int zlo = std::max(0, c->vol.own0), zhi = std::min(c->vol.own1, c->vol.Z - 1);
+  const size_t waves = extract_waves(c->vol, zlo, zhi);
+  int64_t total = 0;
+  if (waves > 0) {
+    const size_t nb = scan_blocks(waves);
+    char *ws = nullptr;
+    HIPCHK(hipMalloc(&ws, waves * 4 + waves * 8 + nb * 8 + 64));
+    unsigned *counts = (unsigned *)ws;
+    unsigned long long *offsets = (unsigned long long *)(ws + ((waves * 4 + 7) & ~(size_t)7));
+    unsigned long long *bsum = offsets + waves;
+    unsigned long long *dtot = bsum + nb;
+    const DevPose vp = to_dev(c->p.volu_pose);
+    launch_mesh(c->stream, c->vol, vp, zlo, zhi, c->mc_tab, counts, nullptr, nullptr, 0);
+    launch_scan(c->stream, counts, offsets, bsum, waves, dtot);
+    unsigned long long ht = 0;
+    hipError_t e = hipMemcpyAsync(&ht, dtot, 8, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    total = (int64_t)ht;
+    const int64_t n = std::min<int64_t>(total, cap);
+    float *dout = nullptr;
+    if (e == hipSuccess && n > 0) {
+      e = hipMalloc(&dout, (size_t)n * 36);
+      if (e == hipSuccess) {
+        launch_mesh(c->stream, c->vol, vp, zlo, zhi, c->mc_tab, counts, offsets, dout, (unsigned long long)n);
+        e = hipMemcpyAsync(tri_xyz, dout, (size_t)n * 36, hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        (void)hipFree(dout);
+      }
+    }
+    (void)hipFree(ws);
+    if (e != hipSuccess) return set_err(KFX_ERR_HIP, std::string("extract_mesh: ") + hipGetErrorString(e));
+  }
+  if (n_tris) *n_tris = total;
+  return KFX_OK;
+}
+
+int kfx_write_ply_mesh(const char *path, const float *tri_xyz, int64_t n) {
+  if (!path || n < 0 || (n > 0 && !tri_xyz)) return set_err(KFX_ERR_ARG, "bad argument");
+  FILE *f = std::fopen(path, "w");
+  if (!f) return set_err(KFX_ERR_ARG, std::string("cannot open ") + path);
+  std::fprintf(f, "ply\nformat ascii 1.0\nelement vertex %lld\nproperty float x\nproperty float y\n"
+               "property float z\nelement face %lld\nproperty list uchar int vertex_indices\nend_header\n",
+               (long long)(3 * n), (long long)n);
+  for (int64_t i = 0; i < 3 * n; ++i)
+    std::fprintf(f, "%g %g %g\n", tri_xyz[3 * i], tri_xyz[3 * i + 1], tri_xyz[3 * i + 2]);
+  for (int64_t i = 0; i < n; ++i)
+    std::fprintf(f, "3 %lld %lld %lld\n", (long long)(3 * i), (long long)(3 * i + 1), (long long)(3 * i + 2));
+  std::fclose(f);
   return KFX_OK;
 }
 

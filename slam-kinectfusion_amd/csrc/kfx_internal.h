@@ -161,6 +161,10 @@ size_t extract_waves(const VolView &v, int zlo, int zhi);
 void launch_extract(hipStream_t s, const VolView &v, DevPose vpose, int zlo, int zhi,
                     unsigned *counts, const unsigned long long *offsets, float *out,
                     unsigned long long cap);
+// marching cubes over z in [zlo, zhi) (same waves / chunks as launch_extract);
+// tab: 256 x 16 bytes {n_tri, 3*n_tri edge indices}
+void launch_mesh(hipStream_t s, const VolView &v, DevPose vpose, int zlo, int zhi, const uint8_t *tab,
+                 unsigned *counts, const unsigned long long *offsets, float *out, unsigned long long cap);
 size_t scan_blocks(size_t n);  // bsum entries launch_scan needs (<= 65536)
 void launch_scan(hipStream_t s, const unsigned *counts, unsigned long long *offsets,
                  unsigned long long *bsum, size_t n, unsigned long long *total);

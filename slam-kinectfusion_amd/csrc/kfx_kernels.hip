@@ -393,7 +393,13 @@ __global__ __launch_bounds__(256) void k_preprocess_maps(BilatArgs a) {
 // exact int64 fixed point (D; order-independent, so any reduction tree gives
 // the oracle's sums).  Each lane takes kIcpPix pixels whose loads are issued
 // together; the block reduces through LDS and writes one 27-word partial.
-constexpr int kIcpPix = 4;
+#ifndef KFX_ICP_XCD
+#define KFX_ICP_XCD 1  // ICP: XCD-banded pixel rows per block
+#endif
+#ifndef KFX_ICP_PIX
+#define KFX_ICP_PIX 4
+#endif
+constexpr int kIcpPix = KFX_ICP_PIX;
 constexpr int kIcpBlockPix = 256 * kIcpPix;
 constexpr unsigned long long kIcpWatchdogTicks = 20000000ull;  // >= 0.2 s of s_memrealtime
 __device__ int icp_update(const long long *sums, DevPose &pose, double *xo);
@@ -463,6 +469,16 @@ __device__ __forceinline__ void icp_lane(const LevelGeom &g, const DevPose &P,
 }
 
 // Current-frame vertex/normal of the lane's pixels of pixel group grp.
+// Blocks are dealt round-robin to the 8 XCDs; remap so that each XCD gets a
+// contiguous band of work (raycast: 16x16 pixel tiles whose rays gather the
+// same voxel lines; ICP: pixel rows whose correspondences gather the same
+// rows of the previous maps), which then hits in that XCD's L2.  Bijective
+// for any count.
+__device__ __forceinline__ int xcd_remap(int b, int nb) {
+  const int q = nb / 8, r = nb % 8, xcd = b % 8;
+  return xcd * q + min(xcd, r) + b / 8;
+}
+
 __device__ __forceinline__ void icp_load_cur(const LevelGeom &g, int xe, int npix, int grp,
                                              int ppl, const float *__restrict__ cv,
                                              const float *__restrict__ cn, f3 (&n0)[kIcpPix],
@@ -665,7 +681,8 @@ __global__ __launch_bounds__(256, 2) void k_icp_track(IcpPlan pl, DevState *__re
     f3 n0[kIcpPix], v0[kIcpPix];
     bool ok[kIcpPix];
     if (mine)
-      icp_load_cur(g, pl.xe[l], pl.npix[l], blockIdx.x, pl.ppl[l], pl.cv[l], pl.cn[l], n0, v0, ok);
+      icp_load_cur(g, pl.xe[l], pl.npix[l], KFX_ICP_XCD ? xcd_remap(blockIdx.x, pl.groups[l]) : (int)blockIdx.x,
+                   pl.ppl[l], pl.cv[l], pl.cn[l], n0, v0, ok);
     for (int it = 0; it < pl.iters[l] && !fail; ++it, ++slot) {
       unsigned long long *sh = sy->sums + (size_t)slot * kIcpShards * 27;
       target += pl.groups[l];
@@ -1396,13 +1413,6 @@ __device__ f3 compute_normal(const VolView &v, const RayConsts &rc, f3 p) {
 
 // One wave = an 8x8 pixel tile (rays of a wave sample neighbouring voxels).
 // BOOT frames copy the measured level-0 maps instead (kinectfusion.cpp:88-89).
-// Blocks are dealt round-robin to the 8 XCDs; remap so that each XCD gets a
-// contiguous band of 16x16 tiles (rays of neighbouring tiles gather the same
-// voxel lines, which then hit in that XCD's L2).  Bijective for any count.
-__device__ __forceinline__ int xcd_remap(int b, int nb) {
-  const int q = nb / 8, r = nb % 8, xcd = b % 8;
-  return xcd * q + min(xcd, r) + b / 8;
-}
 
 template <bool kIdx32>
 __device__ __forceinline__ size_t ray_index(const VolView &v, int x, int y, int z) {
@@ -1855,6 +1865,92 @@ __global__ __launch_bounds__(256) void k_extract(VolView v, DevPose aff, int zlo
   if (!kEmit && lane == 0) counts[wave] = total;
 }
 
+// Marching cubes (§8 f5; C5 asks for a mesh, the reference has none).  Cube
+// (x, y, z) = the 8 voxels (x+dx, y+dy, z+dz); all 8 must have weight > 0;
+// corner c = dx | dy<<1 | dz<<2 is inside when its tsdf < 0.  `tab` (256 x
+// 16 bytes, built by the host, kfx_api.hip mc_table) lists per configuration
+// the triangles as edge indices (edge e: axis e/4, the 4 edges of an axis in
+// ascending lower-corner order).  An edge vertex interpolates the two voxel
+// centres as the point extraction does (FullScan6, tsdf_volume.cu:341-360),
+// then the volume pose.  Triangles come out in the canonical order of the
+// point cloud (8-slice chunk, tile, z, lane, triangle), 9 floats each.
+__device__ __forceinline__ f3 mc_vertex(const VolView &v, const DevPose &aff, int x, int y, int z, int e,
+                                        const float (&F)[8]) {
+  const int a = e >> 2, k = e & 3;
+  // lower corner of edge e: the k-th corner (ascending) with bit a clear
+  int c = 0, m = 0;
+  for (int q = 0; q < 8; ++q)
+    if (!((q >> a) & 1)) {
+      if (m == k) c = q;
+      ++m;
+    }
+  const int cn = c | (1 << a);
+  f3 V = {((float)(x + (c & 1)) + 0.5f) * v.vs[0], ((float)(y + ((c >> 1) & 1)) + 0.5f) * v.vs[1],
+          ((float)(z + ((c >> 2) & 1)) + 0.5f) * v.vs[2]};
+  const float Fa = F[c], Fb = F[cn];
+  const float Va = a == 0 ? V.x : (a == 1 ? V.y : V.z);
+  const float Vn = Va + v.vs[a];
+  const float d_inv = 1.f / (fabsf(Fa) + fabsf(Fb));
+  const float cc = (Va * fabsf(Fb) + Vn * fabsf(Fa)) * d_inv;
+  if (a == 0) V.x = cc;
+  else if (a == 1) V.y = cc;
+  else V.z = cc;
+  return add(rmul(aff.R, V), {aff.t[0], aff.t[1], aff.t[2]});
+}
+
+template <bool kEmit>
+__global__ __launch_bounds__(256) void k_mesh(VolView v, DevPose aff, int zlo, int zhi,
+                                              const uint8_t *__restrict__ tab, unsigned *counts,
+                                              const unsigned long long *offsets, float *out,
+                                              unsigned long long cap) {
+  const int lane = threadIdx.x & 63;
+  const int ntiles = v.tiles_x * v.tiles_y;
+  const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (tile >= ntiles) return;
+  const size_t wave = (size_t)blockIdx.y * ntiles + tile;
+  const int x = (tile % v.tiles_x) * 8 + (lane & 7);
+  const int y = (tile / v.tiles_x) * 8 + (lane >> 3);
+  const int c0 = (zlo / kExtractZ) * kExtractZ + (int)blockIdx.y * kExtractZ;
+  const int z0 = max(zlo, c0), z1 = min(zhi, c0 + kExtractZ);
+  unsigned long long base = kEmit ? offsets[wave] : 0ull;
+  unsigned total = 0;
+  for (int z = z0; z < z1; ++z) {
+    float F[8];
+    int cfg = 0, nt = 0;
+    if (x + 1 < v.X && y + 1 < v.Y) {
+      bool all = true;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const size_t i = vox_index(v, x + (c & 1), y + ((c >> 1) & 1), z + ((c >> 2) & 1));
+        all = all && v.weight[i] > 0;
+        F[c] = (float)v.tsdf[i] * kDivShortMax;
+        cfg |= (F[c] < 0.f ? 1 : 0) << c;
+      }
+      if (all) nt = tab[16 * cfg];
+    }
+    // wave prefix of the triangle counts (lane order)
+    int incl = nt;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int o = __shfl_up(incl, off);
+      if (lane >= off) incl += o;
+    }
+    if (kEmit) {
+      const unsigned long long r0 = base + (unsigned long long)(incl - nt);
+      for (int t = 0; t < nt; ++t) {
+        if (r0 + t >= cap) break;
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+          st3(out, (size_t)(3 * (r0 + t) + k), mc_vertex(v, aff, x, y, z, tab[16 * cfg + 1 + 3 * t + k], F));
+      }
+    }
+    const unsigned wt = (unsigned)__shfl(incl, 63);
+    base += wt;
+    total += wt;
+  }
+  if (!kEmit && lane == 0) counts[wave] = total;
+}
+
 // Exclusive scan of n u32 counts into u64 offsets (one 1024-thread block per
 // 4096 counts, then the block totals, then the fix-up); *total = the sum.
 __global__ __launch_bounds__(1024) void k_scan_local(const unsigned *in, unsigned long long *out,
@@ -2281,6 +2377,17 @@ void launch_extract(hipStream_t s, const VolView &v, DevPose vpose, int zlo, int
   else
     hipLaunchKernelGGL(k_extract<false>, grd, dim3(256), 0, s, v, vpose, zlo, zhi, counts, offsets,
                        out, cap);
+}
+void launch_mesh(hipStream_t s, const VolView &v, DevPose vpose, int zlo, int zhi, const uint8_t *tab,
+                 unsigned *counts, const unsigned long long *offsets, float *out, unsigned long long cap) {
+  const int nc = extract_chunks(zlo, zhi);
+  if (nc == 0) return;
+  const int tiles = v.tiles_x * v.tiles_y;
+  dim3 grd((tiles + 3) / 4, nc);
+  if (offsets)
+    hipLaunchKernelGGL(k_mesh<true>, grd, dim3(256), 0, s, v, vpose, zlo, zhi, tab, counts, offsets, out, cap);
+  else
+    hipLaunchKernelGGL(k_mesh<false>, grd, dim3(256), 0, s, v, vpose, zlo, zhi, tab, counts, offsets, out, cap);
 }
 size_t scan_blocks(size_t n) { return (n + 4095) / 4096; }
 void launch_scan(hipStream_t s, const unsigned *counts, unsigned long long *offsets,

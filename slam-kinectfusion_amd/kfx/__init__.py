@@ -35,6 +35,7 @@ EXPORTS = [
     "kfx_stage_icp", "kfx_stage_integrate", "kfx_stage_raycast", "kfx_set_profiling", "kfx_get_stage_ms",
     "kfx_integrate_counts", "kfx_integrate_stats", "kfx_create_slab", "kfx_slab_info", "kfx_comm_get_unique_id", "kfx_comm_init",
     "kfx_pipeline_group", "kfx_render", "kfx_volume_checksum", "kfx_extract_points", "kfx_write_ply", "kfx_save_pointcloud",
+    "kfx_extract_mesh", "kfx_write_ply_mesh",
     "kfx_dataset_open", "kfx_dataset_info", "kfx_dataset_read", "kfx_dataset_close", "kfx_png_info",
     "kfx_png_read_bgr8", "kfx_png_read_depth", "kfx_parse_intr",
 ]
@@ -108,6 +109,8 @@ def lib():
         "kfx_volume_checksum": ([vp, P(C.c_uint64)], i),
         "kfx_write_ply": ([C.c_char_p, P(f), C.c_int64], i),
         "kfx_save_pointcloud": ([vp, C.c_char_p, C.c_int64], i),
+        "kfx_extract_mesh": ([vp, P(f), C.c_int64, P(C.c_int64)], i),
+        "kfx_write_ply_mesh": ([C.c_char_p, P(f), C.c_int64], i),
         "kfx_dataset_open": ([C.c_char_p, P(vp)], i),
         "kfx_dataset_info": ([vp, P(Intrinsics), P(i), P(i)], i),
         "kfx_dataset_read": ([vp, i, P(C.c_uint8), P(f)], i),
@@ -201,6 +204,12 @@ class Dataset:
             self.close()
         except Exception:
             pass
+
+
+def write_ply_mesh(path: str, tris: np.ndarray):
+    """ASCII PLY of an (N, 3, 3) float32 triangle soup."""
+    t = np.ascontiguousarray(tris, np.float32)
+    _check(lib().kfx_write_ply_mesh(path.encode(), fptr(t), t.shape[0]), "kfx_write_ply_mesh")
 
 
 def comm_unique_id() -> bytes:
@@ -368,6 +377,16 @@ class KinectFusion:
         out = np.empty((self.intr.height, self.intr.width, 3), np.uint8)
         _check(lib().kfx_render(self._h, 0 if kind == "phong" else 1, out.ctypes.data_as(C.POINTER(C.c_uint8))),
                "kfx_render")
+        return out
+
+    def extract_mesh(self, cap: int = 50_000_000) -> np.ndarray:
+        """Marching-cubes triangles, (N, 3, 3) float32 world coordinates (canonical order)."""
+        n = C.c_int64()
+        _check(lib().kfx_extract_mesh(self._h, None, 0, C.byref(n)), "kfx_extract_mesh")
+        m = min(n.value, cap)
+        out = np.zeros((m, 3, 3), np.float32)
+        if m:
+            _check(lib().kfx_extract_mesh(self._h, fptr(out), m, C.byref(n)), "kfx_extract_mesh")
         return out
 
     # ---- point cloud (kinectfusion::extracePointcloud / savePointcloud) ---

@@ -69,3 +69,32 @@ def test_slab_clouds_concatenate(fused):
     assert np.array_equal(np.concatenate(parts), kf.extract_points())
     for m in members:
         m.close()
+
+
+def test_mesh_matches_oracle(fused, tmp_path):
+    """Marching cubes on the device vs the oracle on the downloaded volume:
+    identical triangle arrays (bit for bit, canonical order), capped prefix,
+    slab meshes concatenating to the single volume's, and the PLY mesh text."""
+    from kfx import write_ply_mesh
+    kf, p, (bgr, dep, intr) = fused
+    g = kf.extract_mesh()
+    t, w, _ = kf.volume_soa()
+    vol = O.Volume(kf.dims, (L_VOL,) * 3)
+    o, n = O.extract_mesh(vol, p.volu_pose, tsdf=t, weight=w)
+    assert n == len(o) > 10000 and g.shape == o.shape
+    assert np.array_equal(g.view(np.uint32), o.view(np.uint32))
+    assert np.array_equal(kf.extract_mesh(cap=999), o[:999])
+    members = [KinectFusion(Intrinsics.from_any(intr), p, slab=(r, 2)) for r in range(2)]
+    for k in range(len(dep)):
+        pipeline_group(members, bgr[k], dep[k].astype(np.float32))
+    parts = [m.extract_mesh() for m in members]
+    assert all(len(x) > 0 for x in parts) and np.array_equal(np.concatenate(parts), g)
+    for m in members:
+        m.close()
+    path = tmp_path / "mesh.ply"
+    write_ply_mesh(str(path), o[:3])
+    txt = path.read_text().splitlines()
+    assert txt[:10] == ["ply", "format ascii 1.0", "element vertex 9", "property float x", "property float y",
+                        "property float z", "element face 3", "property list uchar int vertex_indices",
+                        "end_header", "%g %g %g" % tuple(float(v) for v in o[0, 0])]
+    assert txt[-1] == "3 6 7 8"
