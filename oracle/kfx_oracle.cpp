@@ -349,44 +349,38 @@ int kfo_icp_update(const int64_t sums[27], kfx_pose *pose, double x_out[6]) {
       else
         A[i][j] = A[j][i] = v;
     }
-  int sign = 1;
-  double rdiag[6];
-  for (int k = 0; k < 6; ++k) {
-    int p = k;
-    double best = std::fabs(A[k][k]);
-    for (int i = k + 1; i < 6; ++i)
-      if (std::fabs(A[i][k]) > best) {
-        best = std::fabs(A[i][k]);
-        p = i;
-      }
-    if (p != k) {
-      for (int j = 0; j < 6; ++j) {
-        const double tmp = A[k][j];
-        A[k][j] = A[p][j];
-        A[p][j] = tmp;
-      }
-      const double tb = b[k];
-      b[k] = b[p];
-      b[p] = tb;
-      sign = -sign;
+  // D: A = JᵀJ is symmetric: LDLᵀ factorisation (no pivoting, one division
+  // per column) instead of cv::solve(DECOMP_SVD); det = d0·…·d5 as
+  // cv::determinant's value of A.
+  double L[6][6] = {}, d[6], rd[6];
+  for (int j = 0; j < 6; ++j) {
+    double w[6];
+    double dj = A[j][j];
+    for (int k = 0; k < j; ++k) {
+      w[k] = L[j][k] * d[k];
+      dj = dj - L[j][k] * w[k];
     }
-    rdiag[k] = 1.0 / A[k][k];  // pivot reciprocal (D: multiplied, one division per step)
-    if (A[k][k] != 0.0) {
-      for (int i = k + 1; i < 6; ++i) {
-        const double f = A[i][k] * rdiag[k];
-        for (int j = k + 1; j < 6; ++j) A[i][j] = A[i][j] - f * A[k][j];
-        b[i] = b[i] - f * b[k];
-      }
+    d[j] = dj;
+    rd[j] = 1.0 / dj;
+    for (int i = j + 1; i < 6; ++i) {
+      double s = A[i][j];
+      for (int k = 0; k < j; ++k) s = s - L[i][k] * w[k];
+      L[i][j] = s * rd[j];
     }
   }
-  double det = (double)sign;
-  for (int k = 0; k < 6; ++k) det = det * A[k][k];
+  double det = d[0];
+  for (int k = 1; k < 6; ++k) det = det * d[k];
   if (std::fabs(det) < 1e-15 || std::isnan(det)) return 1;
-  double x[6];
-  for (int i = 5; i >= 0; --i) {
+  double y[6], x[6];
+  for (int i = 0; i < 6; ++i) {  // L y = b
     double acc = b[i];
-    for (int j = i + 1; j < 6; ++j) acc = acc - A[i][j] * x[j];
-    x[i] = acc * rdiag[i];
+    for (int k = 0; k < i; ++k) acc = acc - L[i][k] * y[k];
+    y[i] = acc;
+  }
+  for (int i = 5; i >= 0; --i) {  // Lᵀ x = D⁻¹ y
+    double acc = y[i] * rd[i];
+    for (int k = i + 1; k < 6; ++k) acc = acc - L[k][i] * x[k];
+    x[i] = acc;
   }
   if (x_out)
     for (int i = 0; i < 6; ++i) x_out[i] = x[i];

@@ -809,15 +809,14 @@ __device__ __forceinline__ double bcast(double v, int src) {
 }
 
 // icp_registration.cpp:33-42 on the device: A/b unpack (rigid_icp.cu:156-165),
-// partial-pivot LU with det check, LU solve (D: instead of SVD), Rodrigues,
-// pose = pose * Tinc (the LU multiplies by pivot reciprocals, as the oracle
-// does).  Every lane runs the whole solve on its own registers
-// (identical, wave-uniform values: no cross-lane traffic on the critical
-// path); the pivot row is made uniform so the row swap is a scalar branch.
-// Each double operation is the oracle's (kfo_icp_update) in the same order,
-// so the result is bit-identical.  Columns left of the pivot are dead after
-// their step and are not swapped.  sums: 27 int64 (any memory, read by all
-// lanes).
+// LDLᵀ factorisation with det check and the triangular solves (D: instead of
+// SVD; A = JᵀJ is symmetric), Rodrigues, pose = pose * Tinc.  Every lane
+// runs the whole solve on its own registers (identical, wave-uniform values:
+// no cross-lane traffic on the critical path).  Each double operation is the
+// oracle's (kfo_icp_update) in the same order, so the result is
+// bit-identical.  (The earlier partial-pivot LU spent most of its ~3.4k
+// cycles on data-dependent row moves.)  sums: 27 int64 (any memory, read by
+// all lanes).
 __device__ int icp_update(const long long *sums, DevPose &pose, double *xo) {
   double A[6][7];  // column 6 = b
   {
@@ -831,55 +830,46 @@ __device__ int icp_update(const long long *sums, DevPose &pose, double *xo) {
         if (j < 6) A[j][i] = v;
       }
   }
-  int sign = 1;
-  double rdiag[6];
+  // LDLᵀ of the symmetric A (no pivoting: no data-dependent register moves;
+  // one division per column), det = d0·…·d5
+  double L[6][6], d[6], rd[6];
 #pragma unroll
-  for (int k = 0; k < 6; ++k) {
-    int p = k;
-    double best = fabs(A[k][k]);
+  for (int j = 0; j < 6; ++j) {
+    double w[6];
+    double dj = A[j][j];
 #pragma unroll
-    for (int i = k + 1; i < 6; ++i) {
-      const double t = fabs(A[i][k]);
-      if (t > best) {
-        best = t;
-        p = i;
-      }
+    for (int k = 0; k < j; ++k) {
+      w[k] = L[j][k] * d[k];
+      dj = dj - L[j][k] * w[k];
     }
-    p = __builtin_amdgcn_readfirstlane(p);  // identical in every lane
-    if (p != k) {
+    d[j] = dj;
+    rd[j] = 1.0 / dj;
 #pragma unroll
-      for (int i = k + 1; i < 6; ++i)
-        if (p == i) {
+    for (int i = j + 1; i < 6; ++i) {
+      double s = A[i][j];
 #pragma unroll
-          for (int j = k; j < 7; ++j) {
-            const double tmp = A[k][j];
-            A[k][j] = A[i][j];
-            A[i][j] = tmp;
-          }
-        }
-      sign = -sign;
-    }
-    rdiag[k] = 1.0 / A[k][k];  // pivot reciprocal (D: one division per step)
-    if (A[k][k] != 0.0) {
-#pragma unroll
-      for (int i = k + 1; i < 6; ++i) {
-        const double f = A[i][k] * rdiag[k];
-#pragma unroll
-        for (int j = k + 1; j < 7; ++j) A[i][j] = A[i][j] - f * A[k][j];
-      }
+      for (int k = 0; k < j; ++k) s = s - L[i][k] * w[k];
+      L[i][j] = s * rd[j];
     }
   }
-  double det = (double)sign;
+  double det = d[0];
 #pragma unroll
-  for (int k = 0; k < 6; ++k) det = det * A[k][k];
+  for (int k = 1; k < 6; ++k) det = det * d[k];
   if (fabs(det) < 1e-15 || isnan(det)) return 1;
-  double x[6];
+  double y[6], x[6];
 #pragma unroll
-  for (int r = 5; r >= 0; --r) {
-    double acc = A[r][6];
+  for (int i = 0; i < 6; ++i) {  // L y = b
+    double acc = A[i][6];
 #pragma unroll
-    for (int c = r + 1; c < 6; ++c) acc = acc - A[r][c] * x[c];
-    x[r] = acc * rdiag[r];
+    for (int k = 0; k < i; ++k) acc = acc - L[i][k] * y[k];
+    y[i] = acc;
+  }
+#pragma unroll
+  for (int i = 5; i >= 0; --i) {  // Lᵀ x = D⁻¹ y
+    double acc = y[i] * rd[i];
+#pragma unroll
+    for (int k = i + 1; k < 6; ++k) acc = acc - L[k][i] * x[k];
+    x[i] = acc;
   }
 #pragma unroll
   for (int r = 0; r < 6; ++r) xo[r] = x[r];
