@@ -15,11 +15,17 @@
 #ifndef KFX_INT_KB
 #define KFX_INT_KB 4  // integrate: voxels per batch (loads in flight per lane)
 #endif
+#ifndef KFX_RAY_OCC
+#define KFX_RAY_OCC 5  // raycast: waves per SIMD the register budget must allow (4800 waves at VGA: one round at 5)
+#endif
 #ifndef KFX_RAY_KR
-#define KFX_RAY_KR 16  // raycast: samples per batch (loads in flight per lane)
+#define KFX_RAY_KR 14  // raycast: samples per batch (loads in flight per lane)
 #endif
 #ifndef KFX_SINCOS
 #define KFX_SINCOS 1
+#endif
+#ifndef KFX_INT_OCC
+#define KFX_INT_OCC 8  // integrate: waves per SIMD the register budget is sized for
 #endif
 #ifndef KFX_INT_BLOCK
 #define KFX_INT_BLOCK 256  // integrate: threads per block (one 8x8 column tile per wave)
@@ -1083,7 +1089,7 @@ struct RayMem<false> {
 // kCount: count-only variant (no voxel traffic) giving N_upd / N_col, the
 // algorithmic-byte inputs of the roofline.
 template <bool kCount, bool kIdx32>
-__global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_integrate(VolView v, LevelGeom g,
+__global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(KFX_INT_OCC, KFX_INT_OCC))) void k_integrate(VolView v, LevelGeom g,
                                                    const float2 *__restrict__ dl,
                                                    const uint8_t *__restrict__ bgr,
                                                    DevState *__restrict__ st, DevPose *log,
@@ -1431,7 +1437,7 @@ __device__ void resize_tile(const RayArgs &ra, int kind, int tx0, int ty0, int l
 // sample i reads samples i-1 and i and the trilinear normal at most 4 slices
 // from sample i, all inside the stored halo.  Resize runs after the combine.
 template <bool kIdx32, bool kSlab>
-__global__ __launch_bounds__(256) void k_raycast(VolView v, RayArgs ra, RayConsts rc,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KFX_RAY_OCC))) void k_raycast(VolView v, RayArgs ra, RayConsts rc,
                                                     FrameView cur, FrameView prev,
                                                     const DevState *__restrict__ st,
                                                     const DevPose *__restrict__ log, DevPose vpose,
