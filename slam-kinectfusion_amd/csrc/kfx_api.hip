@@ -1183,6 +1183,16 @@ int kfx_stage_raycast(kfx_ctx *c, const kfx_pose *cam2vol, const float Rinv[9]) 
   return KFX_OK;
 }
 
+#ifdef KFX_ICP_BLOCK_TRACE
+// debug build only: per-iteration, per-block {lane-phase start, arrival} stamps
+int kfx_debug_icp_blocks(kfx_ctx *c, uint64_t *out, int max_slots) {
+  const int n = std::min(max_slots, c->icp_plan.slots);
+  HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(hipMemcpy(out, c->icp_sync->blk, sizeof(uint64_t) * 1024 * (size_t)n, hipMemcpyDeviceToHost));
+  return n;
+}
+#endif
+
 int kfx_volume_checksum(kfx_ctx *c, uint64_t out[2]) {
   int r = check_ctx(c);
   if (r) return r;

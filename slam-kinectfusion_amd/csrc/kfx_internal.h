@@ -64,6 +64,9 @@ struct IcpSync {
   // s_memrealtime stamps of the last frame, per iteration: block 0 start /
   // arrived / released / solved, last block arrived (kfx_get_icp_trace)
   unsigned long long trace[kIcpMaxSlots][12];
+#ifdef KFX_ICP_BLOCK_TRACE
+  unsigned long long blk[kIcpMaxSlots][512][2];  // debug: per-block lane-phase start / arrival
+#endif
 };
 
 // SoA TSDF volume.  Each z slice is tiled in 8x8 (x,y) tiles; voxel (x,y,z)

@@ -694,6 +694,9 @@ __global__ __launch_bounds__(256, 2) void k_icp_track(IcpPlan pl, DevState *__re
       target += pl.groups[l];
       const bool tr = threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x - 1);
       if (tr && blockIdx.x == 0) sy->trace[slot][0] = wall_clock64();
+#ifdef KFX_ICP_BLOCK_TRACE
+      if (threadIdx.x == 0 && blockIdx.x < 512) sy->blk[slot][blockIdx.x][0] = wall_clock64();
+#endif
       if (mine) {
         double acc[27];
         icp_lane(g, P, n0, v0, ok, pl.ppl[l], pl.pv[l], pl.pn[l], pl.dist_thr, pl.angle_thr, acc);
@@ -711,6 +714,9 @@ __global__ __launch_bounds__(256, 2) void k_icp_track(IcpPlan pl, DevState *__re
           // load, so no L2 writeback/invalidate fence is needed
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           if (tr && blockIdx.x == 0) sy->trace[slot][10] = wall_clock64();
+#ifdef KFX_ICP_BLOCK_TRACE
+          if (threadIdx.x == 0 && blockIdx.x < 512) sy->blk[slot][blockIdx.x][1] = wall_clock64();
+#endif
           if (threadIdx.x == 0) {
             // the last arriver releases the iteration: spinners poll 8 flag
             // copies instead of the contended arrival counter

@@ -1,0 +1,34 @@
+#!/usr/bin/env python3
+"""Per-block ICP phase stamps (debug library built with -DKFX_ICP_BLOCK_TRACE):
+for each iteration, the spread of block lane-phase starts and arrivals (us,
+relative to block 0's start), and which blocks arrive last.
+usage: KFX_LIB_PATH=<debug lib> python3 tools/icp_blocks.py"""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "slam-kinectfusion_amd"))
+import kfx  # noqa: E402
+from kfx import synth  # noqa: E402
+from kfx.abi import default_params  # noqa: E402
+
+intr = synth.Intrinsics.vga()
+kf = kfx.KinectFusion(intr, default_params())
+bgr, dep, _ = synth.sequence(8, intr)
+for k in range(len(dep)):
+    kf.pipeline(bgr[k], dep[k].astype(np.float32))
+buf = (C.c_uint64 * (19 * 1024))()
+n = kfx.lib().kfx_debug_icp_blocks(kf._h, buf, 19)
+a = np.frombuffer(buf, np.uint64)[: n * 1024].reshape(n, 512, 2).astype(np.int64)
+for s in range(n):
+    st, ar = a[s, :, 0], a[s, :, 1]
+    used = st > 0
+    t0 = st[0]
+    sts, ars = (st[used] - t0) / 100.0, (ar[used] - t0) / 100.0
+    lane = ars - sts
+    last = np.argsort(-ar[used])[:5]
+    print(f"it {s:2d} blocks {used.sum():3d} start spread {sts.min():6.2f}..{sts.max():6.2f}  "
+          f"arrive {ars.min():6.2f}..{ars.max():6.2f}  phase med {np.median(lane):5.2f} max {lane.max():5.2f}  "
+          f"last {list(np.nonzero(used)[0][last])}")
