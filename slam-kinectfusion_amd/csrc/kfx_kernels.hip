@@ -12,6 +12,9 @@
 
 #include "kfx_internal.h"
 
+#ifndef KFX_INT_ICHECK
+#define KFX_INT_ICHECK 1  // integrate fast path: integer image-range tests
+#endif
 #ifndef KFX_INT_KB
 #define KFX_INT_KB 4  // integrate: voxels per batch (loads in flight per lane)
 #endif
@@ -1237,9 +1240,19 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
         const pf2 vv = div_rn2(py, pz, yv) * pf2{g.fy, g.fy} + pf2{g.cy, g.cy};
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
+#if KFX_INT_ICHECK
+          // uu, vv are finite here (|vc| components in {0} u [2^-40, 2^40]);
+          // the conversion saturates out-of-range values, so one unsigned
+          // compare per axis is the float range test [0, w) of the rounded
+          // value; 24-bit multiply (w, h < 2^24)
+          const int iu = (int)rintf(uu[k]), iv = (int)rintf(vv[k]);
+          ok[j + k] = (z + j + k <= zb) & (pz[k] > 0) & ((unsigned)iu < (unsigned)g.w) & ((unsigned)iv < (unsigned)g.h);
+          pix[j + k] = ok[j + k] ? __umul24((unsigned)iv, 8u * (unsigned)g.w) + ((unsigned)iu << 3) : kOob;
+#else
           const float uf = rintf(uu[k]), vf = rintf(vv[k]);
           ok[j + k] = (z + j + k <= zb) & (pz[k] > 0) & (uf >= 0.f) & (uf < fw) & (vf >= 0.f) & (vf < fh);
           pix[j + k] = ok[j + k] ? ((unsigned)(int)vf * (unsigned)g.w + (unsigned)(int)uf) * 8u : kOob;
+#endif
         }
       }
     } else {  // IEEE division (tiny or huge operands)
