@@ -244,6 +244,7 @@ def main():
         int_bytes.append(8 * nu + 8 * nc + 7 * W * H)
         int_ms.append(ms["integrate"])
     kf.set_profiling(False)
+    ray_work = kf.raycast_stats() if a.profile_frames else None
     kf.synchronize()
     kf.close()
     stage_med = {k: round(statistics.median(v), 4) for k, v in stages.items()} if a.profile_frames else {}
@@ -297,6 +298,7 @@ def main():
                                    if ktime else None),
         "integrate_voxels": ({k: int(np.mean([w[k] for w in int_work])) for k in int_work[0]}
                              if int_work else None),
+        "raycast_work": ray_work,
         "roofline": {
             "kernel": "k_integrate",
             "bound": "hbm",

@@ -195,6 +195,11 @@ int kfx_integrate_counts(kfx_ctx *ctx, int64_t *n_updated, int64_t *n_colored);
  * gathered (visited voxels that project into the image and read a depth),
  * wave batches executed (4 voxels per lane each), 0, 0, 0}. */
 int kfx_integrate_stats(kfx_ctx *ctx, int64_t out[8]);
+/* Work statistics of the last processed frame's raycast (re-run on the same
+ * state, nothing written): out = {rays marched, empty-space skip lookups,
+ * samples skipped by them, lookups that found an occupied brick, 14-sample
+ * batches marched (per ray), hit candidates whose normal was computed, 0, 0}. */
+int kfx_raycast_stats(kfx_ctx *ctx, int64_t out[8]);
 
 /* ---- point cloud ------------------------------------------ */
 /* TSDFVolume::fetchPointCloud buffer size (tsdf_volume.cpp:67) */

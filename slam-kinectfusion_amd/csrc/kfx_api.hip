@@ -468,6 +468,16 @@ VolView make_vol(const kfx_params &p, int rank, int world) {
   v.tiles_x = v.X / 8;
   v.tiles_y = v.Y / 8;
   v.slice = (size_t)v.X * v.Y;
+  // occupancy maps over the stored slices (bricks on global multiples of 8 / 32)
+  const int zl = v.zb + v.zn - 1;
+  v.bz0 = v.zb >> 3;
+  v.nbz = (zl >> 3) - v.bz0 + 1;
+  v.bw = (v.nbz + 63) / 64;
+  v.sz0 = v.zb >> 5;
+  v.nsz = (zl >> 5) - v.sz0 + 1;
+  v.sw = (v.nsz + 31) / 32;
+  v.stx = (v.tiles_x + 3) / 4;
+  v.sty = (v.tiles_y + 3) / 4;
   for (int i = 0; i < 3; ++i) {
     v.vs[i] = p.volu_range[i] / (float)p.volu_dims[i];  // tsdf_volume.cpp:16
     v.range[i] = p.volu_range[i];
@@ -497,6 +507,8 @@ int do_reset(kfx_ctx *c) {
   HIPCHK(hipMemsetAsync(c->vol.tsdf, 0, n * sizeof(int16_t), c->stream));
   HIPCHK(hipMemsetAsync(c->vol.weight, 0, n * sizeof(int16_t), c->stream));
   HIPCHK(hipMemsetAsync(c->vol.rgb, 0, n * sizeof(uint32_t), c->stream));
+  HIPCHK(hipMemsetAsync(c->vol.bocc, 0, c->vol.bocc_bytes(), c->stream));
+  HIPCHK(hipMemsetAsync(c->vol.socc, 0, c->vol.socc_bytes(), c->stream));
   for (int l = 0; l < c->L; ++l) {
     const size_t np = (size_t)c->g[l].w * c->g[l].h;
     for (FrameView *f : {&c->curb[0], &c->curb[1], &c->prev}) {
@@ -670,6 +682,8 @@ static int create_impl(const kfx_intrinsics *intr, const kfx_params *params, int
     c->vol.weight = (int16_t *)((char *)c->vol.tsdf + off);
   }
   if ((r = dalloc(c, (void **)&c->vol.rgb, n * 4))) return fail(r);
+  if ((r = dalloc(c, (void **)&c->vol.bocc, c->vol.bocc_bytes()))) return fail(r);
+  if ((r = dalloc(c, (void **)&c->vol.socc, c->vol.socc_bytes()))) return fail(r);
   if ((r = dalloc(c, (void **)&c->st, sizeof(DevState)))) return fail(r);
   c->pose_cap = kInitialPoseCap;
   if ((r = dalloc(c, (void **)&c->pose_log, sizeof(DevPose) * (size_t)c->pose_cap))) return fail(r);
@@ -1015,6 +1029,9 @@ int kfx_upload_tsdf(kfx_ctx *c, const void *src) {
     }
   }
   HIPCHK(hipFree(tmp));
+  launch_occ_rebuild(c->stream, c->vol);  // the raycast's skip maps of the new contents
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(c->stream));
   return KFX_OK;
 }
 
@@ -1166,6 +1183,21 @@ int kfx_integrate_counts(kfx_ctx *c, int64_t *nu, int64_t *nc) {
   int r = check_ctx(c);
   if (r) return r;
   return integrate_counts_impl(c, nu, nc, nullptr);
+}
+
+int kfx_raycast_stats(kfx_ctx *c, int64_t out[8]) {
+  int r = check_ctx(c);
+  if (r) return r;
+  if (!out) return set_err(KFX_ERR_ARG, "null out");
+  HIPCHK(hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * 8, c->stream));
+  launch_raycast(c->stream, c->vol, c->L, c->g, c->cur, c->prev, c->st, c->pose_log,
+                 to_dev(c->p.volu_pose), nullptr, c->slab ? c->key_local : nullptr, c->counters);
+  HIPCHK(hipGetLastError());
+  unsigned long long h[8];
+  HIPCHK(hipMemcpyAsync(h, c->counters, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  for (int i = 0; i < 8; ++i) out[i] = i < 6 ? (int64_t)h[i] : 0;
+  return KFX_OK;
 }
 
 int kfx_integrate_stats(kfx_ctx *c, int64_t out[8]) {

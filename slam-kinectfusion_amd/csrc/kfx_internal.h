@@ -92,6 +92,19 @@ struct VolView {
   float inv_trunc;  // RN(1/trunc), for the exact FMA division (kfx_kernels.hip div_rn)
   int tsat;         // tsdf fixed point of a weight-64, ts = 1 update (integrate skip), or 1<<20
   size_t slice;    // voxels per z slice (= X*Y)
+  // Dilated occupancy of negative tsdf (raycast empty-space skipping, DESIGN.md
+  // §4): bit set <=> some voxel within one brick of this brick may hold a
+  // negative tsdf (a superset: integrate only ever sets bits; reset clears).
+  // Bricks are 8x8x8 voxels = one 8x8 column tile x 8 global slices (brick z
+  // = z >> 3); super-bricks are 4x4x4 bricks (32^3 voxels).  Words per column:
+  //   bocc[tile * bw + (lbz >> 6)] bit (lbz & 63), lbz = (z >> 3) - bz0 in [0, nbz)
+  //   socc[(sy * stx + sx) * sw + (lsz >> 5)] bit (lsz & 31), lsz = (z >> 5) - sz0
+  unsigned long long *bocc;
+  uint32_t *socc;
+  int bz0, nbz, bw;
+  int sz0, nsz, sw, stx, sty;
+  __host__ __device__ size_t bocc_bytes() const { return (size_t)tiles_x * tiles_y * bw * 8; }
+  __host__ __device__ size_t socc_bytes() const { return (size_t)stx * sty * sw * 4; }
   __host__ __device__ size_t local_voxels() const { return slice * (size_t)zn; }
   // Tile-column layout: the stored slices of one 8x8 column tile are one
   // contiguous run of zn * 64 voxels, z-major inside:
@@ -138,9 +151,10 @@ void launch_integrate(hipStream_t s, VolView v, LevelGeom g0, const float2 *dl0,
                       unsigned long long *counters /* non-null: count-only, 32 words */);
 // raycast of level 0 + resizePointsNormals of levels >= 1 in one launch; with
 // keys != null the slab variant (owned events only, key per pixel, no resize)
+// stats (non-null): the statistics variant (6 counters added, nothing stored)
 void launch_raycast(hipStream_t s, VolView v, int levels, const LevelGeom *g, FrameView cur,
                     FrameView prev, const DevState *st, const DevPose *log, DevPose vpose,
-                    const float *xpose, uint32_t *keys);
+                    const float *xpose, uint32_t *keys, unsigned long long *stats = nullptr);
 // resizePointsNormals of levels >= 1 from the level-0 model maps
 void launch_resize(hipStream_t s, int levels, const LevelGeom *g, FrameView cur, FrameView prev,
                    const DevState *st, const float *xpose);
@@ -175,5 +189,8 @@ void launch_export_records(hipStream_t s, VolView v, int z0, int nz, uint64_t *d
 void launch_import_records(hipStream_t s, VolView v, int z0, int nz, const uint64_t *src);
 void launch_export_soa(hipStream_t s, VolView v, int z0, int nz, int16_t *t, int16_t *w,
                        uint32_t *c);
+// clear the occupancy maps and re-mark every brick holding a negative tsdf
+// (after a volume upload)
+void launch_occ_rebuild(hipStream_t s, VolView v);
 
 }  // namespace kfx

@@ -205,6 +205,47 @@ __device__ __forceinline__ size_t vox_index(const VolView &v, int x, int y, int 
          ((y & 7) << 3) + (x & 7);
 }
 
+// Occupancy marking (VolView::bocc / socc): some voxel of column tile (tx, ty)
+// in global slices [zlo, zhi] holds a negative tsdf.  Sets, dilated by one,
+// the bricks (zlo>>3)-1 .. (zhi>>3)+1 of the 3x3 tiles around (tx, ty) (lanes
+// 0..8 of the calling wave) and the super-bricks (zlo>>5)-1 .. (zhi>>5)+1 of
+// the 3x3 super tiles around (tx>>2, ty>>2) (lanes 9..17).  A plain read
+// first skips the atomic when the bits are already set (bits are never
+// cleared inside a launch, so a stale read is a subset).
+template <typename W>
+__device__ __forceinline__ void occ_set_bits(W *base, int lo, int hi) {
+  constexpr int kb = 8 * sizeof(W);
+  for (int b = lo; b <= hi;) {
+    const int wi = b / kb, e = min(hi, wi * kb + kb - 1);
+    const W m = (e - b == kb - 1 ? ~(W)0 : (((W)1 << (e - b + 1)) - (W)1)) << (b % kb);
+    if ((base[wi] & m) != m) atomicOr(&base[wi], m);
+    b = e + 1;
+  }
+}
+__device__ void occ_mark(const VolView &v, int tx, int ty, int zlo, int zhi, int lane) {
+  if (lane < 9) {
+    const int x = tx + lane % 3 - 1, y = ty + lane / 3 - 1;
+    if (x < 0 || y < 0 || x >= v.tiles_x || y >= v.tiles_y) return;
+    occ_set_bits(v.bocc + (size_t)(y * v.tiles_x + x) * v.bw, max((zlo >> 3) - 1 - v.bz0, 0),
+                 min((zhi >> 3) + 1 - v.bz0, v.nbz - 1));
+  } else if (lane < 18) {
+    const int k = lane - 9;
+    const int x = (tx >> 2) + k % 3 - 1, y = (ty >> 2) + k / 3 - 1;
+    if (x < 0 || y < 0 || x >= v.stx || y >= v.sty) return;
+    occ_set_bits(v.socc + (size_t)(y * v.stx + x) * v.sw, max((zlo >> 5) - 1 - v.sz0, 0),
+                 min((zhi >> 5) + 1 - v.sz0, v.nsz - 1));
+  }
+}
+// Wave-wide [min lo, max hi] then occ_mark (all 64 lanes active).
+__device__ __forceinline__ void occ_mark_wave(const VolView &v, int tile, int lo, int hi, int lane) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    lo = min(lo, __shfl_xor(lo, off));
+    hi = max(hi, __shfl_xor(hi, off));
+  }
+  if (hi >= lo) occ_mark(v, tile % v.tiles_x, tile / v.tiles_x, lo, hi, lane);
+}
+
 // Level-indexed block decomposition for kernels that process all pyramid
 // levels in one launch (16x16 pixel tiles).
 struct LevelTiles {
@@ -1146,6 +1187,12 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
       v.weight[i] = 0;
       v.rgb[i] = 0u;
     }
+    if (chunk == 0) {  // the zeroed volume holds no negative tsdf
+      for (int i = lane; i < v.bw; i += 64) v.bocc[(size_t)tile * v.bw + i] = 0ull;
+      const int tx = tile % v.tiles_x, ty = tile / v.tiles_x;
+      if ((tx & 3) == 0 && (ty & 3) == 0)
+        for (int i = lane; i < v.sw; i += 64) v.socc[(size_t)((ty >> 2) * v.stx + (tx >> 2)) * v.sw + i] = 0u;
+    }
     return;
   }
   const DevPose P = s_pose;
@@ -1201,6 +1248,7 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
   const float thres_color = trunc / 2;
   // kCount: updated, coloured, visited, gathered voxels; wave batches
   unsigned cu = 0, cc = 0, cv = 0, cg = 0, cb = 0;
+  int nlo = INT_MAX, nhi = -1;  // global z range of the negative tsdf this lane wrote
   int z = 1;
 #pragma unroll 8
   for (; z < za; ++z) vc = add(vc, zs);
@@ -1326,6 +1374,10 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
           div_rn(fmaf(pre_t, (float)pre_w, ts), (float)(pre_w + 1), rtab[pre_w + 1]);
       int q = (int)(new_t * (float)kShortMax);
       q = max(-kShortMax, min(kShortMax, q));
+      if (q < 0) {
+        nlo = min(nlo, z + j);
+        nhi = max(nhi, z + j);
+      }
       // saturated voxels (w = 64 at a tsdf fixed point) keep their values:
       // skipping those stores changes nothing and saves write bandwidth
       if (q != t0[j]) mem.st_t(i, (int16_t)q);
@@ -1346,6 +1398,7 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
       }
     }
   }
+  if (!kCount) occ_mark_wave(v, tile, nlo, nhi, lane);  // raycast skip maps
 #ifdef KFX_INT_TRACE
   if (!kCount && counters && lane == 0) {  // debug: per-wave timeline
     unsigned long long *r = counters + 4 * ((size_t)(blockIdx.y * gridDim.x + blockIdx.x) * (KFX_INT_BLOCK / 64) + (threadIdx.x >> 6));
@@ -1374,6 +1427,7 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
 struct RayConsts {
   f3 vs, vs_inv, gd;
   float step;
+  float skip_cap;  // most samples one skip replays (accumulated rounding < 0.1 voxel)
 };
 
 __device__ __forceinline__ float voxel2tsdf(const VolView &v, const RayConsts &rc, f3 p) {
@@ -1441,6 +1495,7 @@ __device__ __forceinline__ size_t ray_index(const VolView &v, int x, int y, int 
 struct RayArgs {
   LevelGeom g[kMaxLevels];
   int levels;
+  unsigned long long *stats;  // k_raycast<.., kStats>: 6 counters
 };
 
 __device__ void resize_tile(const RayArgs &ra, int kind, int tx0, int ty0, int lx, int ly, f3 vout,
@@ -1455,12 +1510,41 @@ __device__ void resize_tile(const RayArgs &ra, int kind, int tx0, int ty0, int l
 // the reference's result; each sample has exactly one owner).  The event at
 // sample i reads samples i-1 and i and the trilinear normal at most 4 slices
 // from sample i, all inside the stored halo.  Resize runs after the combine.
-template <bool kIdx32, bool kSlab>
+// Samples a ray may replay from voxel position c while every sample stays in
+// the box that a clear dilated (super)brick run guarantees non-negative or
+// NaN: per axis [B*b - B, B*b + 2B - 1] (open at the volume's edge columns),
+// z [zl, zh]; each face with 0.2 voxel of margin (rint reaches a voxel only
+// within 0.5 of it, the accumulated rounding of <= 511 adds stays below 0.1).
+constexpr float kInf = __builtin_huge_valf();
+__device__ __forceinline__ float axis_limit(float c, float d, float id, float lo, float hi) {
+  return d > 0.f ? (hi + 0.2f - c) * id : (d < 0.f ? (c - lo + 0.2f) * id : kInf);
+}
+__device__ __forceinline__ float box_limit(int B, int bx, int by, int nbx, int nby, float zl, float zh,
+                                           float cx, float cy, float cz, f3 dv, f3 idv) {
+  const float xl = bx > 0 ? (float)(B * bx - B) : -kInf, xh = bx < nbx - 1 ? (float)(B * bx + 2 * B - 1) : kInf;
+  const float yl = by > 0 ? (float)(B * by - B) : -kInf, yh = by < nby - 1 ? (float)(B * by + 2 * B - 1) : kInf;
+  return fminf(fminf(axis_limit(cx, dv.x, idv.x, xl, xh), axis_limit(cy, dv.y, idv.y, yl, yh)),
+               axis_limit(cz, dv.z, idv.z, zl, zh));
+}
+
+#ifdef KFX_RAY_TRACE
+constexpr bool kTrace = true;
+#else
+constexpr bool kTrace = false;
+#endif
+template <bool kIdx32, bool kSlab, bool kStats = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KFX_RAY_OCC))) void k_raycast(VolView v, RayArgs ra, RayConsts rc,
                                                     FrameView cur, FrameView prev,
                                                     const DevState *__restrict__ st,
                                                     const DevPose *__restrict__ log, DevPose vpose,
                                                     const float *xpose, uint32_t *keys) {
+  // kStats: march statistics (rays, skip lookups, skipped samples, blocked
+  // lookups, sample batches, normal passes), no stores
+  unsigned st_rays = 0, st_lookups = 0, st_skipped = 0, st_blocked = 0, st_batches = 0, st_cand = 0;
+#ifdef KFX_RAY_TRACE
+  const unsigned long long t_start = wall_clock64();
+  unsigned long long t_march = 0, t_norm = 0, t_ndone = 0;
+#endif
   // cam2vol = volume_pose^-1 * pose, Rinv = R^T (tsdf_volume.cpp:59-61; D: transpose)
   __shared__ DevPose s_c2v;
   __shared__ float s_rinv[9];
@@ -1547,10 +1631,133 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KFX_RAY_OCC
     f3 cvert = {0.f, 0.f, 0.f}, r_nextp = nextp;
     float r_rl = 0.f, r_tprev = 0.f;
     uint32_t ckey = 0u, r_kbase = 0u;
+    // Empty-space skipping (exact): no event can happen at a sample whose
+    // nearest voxel holds no negative tsdf unless the sample before it is
+    // negative (every event needs a negative sample: tsdf_volume.cu:242-244).
+    // With the last sample non-negative or NaN (sprev >= 0), the dilated
+    // brick and super-brick map words of the current column (both loads in
+    // flight together) give runs of clear cells along z in the direction of
+    // travel; every voxel of the box such a run guarantees (box_limit) is
+    // non-negative, and voxels outside the volume (or the stored slab) are
+    // NaN.  The samples that stay inside the larger of the two boxes are only
+    // replayed (nextp += vstep, ray_len += step: the reference's exact adds)
+    // without loads; the last one is then loaded as the carried sample.
+    const f3 dv = mulc(vstep, rc.vs_inv);  // per-sample displacement in voxels
+    const f3 idv = {1.f / fabsf(dv.x), 1.f / fabsf(dv.y), 1.f / fabsf(dv.z)};
+    const float rstep = 1.f / rc.step;
+    const bool can_skip = !isnan(dv.x + dv.y + dv.z);
+    if (kStats || kTrace) st_rays += live ? 1u : 0u;
+#ifdef KFX_RAY_TRACE
+    t_march = wall_clock64();
+#endif
     while (__any(live || cand)) {
     while (__any(live)) {
+      if (can_skip && live && sprev >= 0) {
+        uint32_t nsk = 0;
+        for (;;) {
+          const float cx = nextp.x * rc.vs_inv.x, cy = nextp.y * rc.vs_inv.y, cz = nextp.z * rc.vs_inv.z;
+          const int ix = (int)floorf(cx), iy = (int)floorf(cy), iz = (int)floorf(cz);
+          const int bx = min(max(ix >> 3, 0), v.tiles_x - 1), by = min(max(iy >> 3, 0), v.tiles_y - 1);
+          const int lbz = min(max((iz >> 3) - v.bz0, 0), v.nbz - 1);
+          const int sx = min(max(ix >> 5, 0), v.stx - 1), sy = min(max(iy >> 5, 0), v.sty - 1);
+          const int lsz = min(max((iz >> 5) - v.sz0, 0), v.nsz - 1);
+          // both map words in flight together (one round trip per step)
+          const unsigned long long bwd = v.bocc[(size_t)(by * v.tiles_x + bx) * v.bw + (lbz >> 6)];
+          const uint32_t swd = v.socc[(size_t)(sy * v.stx + sx) * v.sw + (lsz >> 5)];
+          const int bb = lbz & 63, sb = lsz & 31;
+          float lim = 0.f;
+          if (!((bwd >> bb) & 1ull)) {  // brick clear: its 3x3 tile box, dilated z run
+            float zl = -kInf, zh = kInf;
+            if (dv.z > 0.f) {
+              const unsigned long long up = bwd >> bb;
+              const int top = lbz + (up ? __builtin_ctzll(up) : 64 - bb) - 1;
+              if (top < v.nbz - 1) zh = (float)(8 * (top + v.bz0) + 15);
+            } else {
+              const unsigned long long dn = bwd << (63 - bb);
+              const int bot = lbz - (dn ? __builtin_clzll(dn) : bb + 1) + 1;
+              if (bot > 0) zl = (float)(8 * (bot + v.bz0) - 8);
+            }
+            lim = box_limit(8, bx, by, v.tiles_x, v.tiles_y, zl, zh, cx, cy, cz, dv, idv);
+          }
+          if (!((swd >> sb) & 1u)) {  // super-brick clear: the same over 32^3 cells
+            float zl = -kInf, zh = kInf;
+            if (dv.z > 0.f) {
+              const uint32_t up = swd >> sb;
+              const int top = lsz + (up ? __builtin_ctz(up) : 32 - sb) - 1;
+              if (top < v.nsz - 1) zh = (float)(32 * (top + v.sz0) + 63);
+            } else {
+              const uint32_t dn = swd << (31 - sb);
+              const int bot = lsz - (dn ? __builtin_clz(dn) : sb + 1) + 1;
+              if (bot > 0) zl = (float)(32 * (bot + v.sz0) - 32);
+            }
+            lim = fmaxf(lim, box_limit(32, sx, sy, v.stx, v.sty, zl, zh, cx, cy, cz, dv, idv));
+          }
+          if (!(lim >= 1.f)) {
+            if (kStats) st_blocked += 1;
+            break;
+          }
+          const int n = (int)fminf(lim, rc.skip_cap);
+          if (kStats || kTrace) {
+            st_lookups += 1;
+            st_skipped += (unsigned)n;
+          }
+          // replay: packed adds {x, y} and {z, ray_len} (the per-element IEEE
+          // adds of the reference); the first nf samples provably stay below
+          // tfar (2 steps of margin over the accumulated rounding)
+          pf2 pxy = {nextp.x, nextp.y}, pzr = {nextp.z, ray_len};
+          const pf2 sxy = {vstep.x, vstep.y}, szr = {vstep.z, rc.step};
+#ifdef KFX_RAY_NOREPLAY  // timing experiment only (wrong values): jump instead of replay
+          const int nf = 0;
+          pxy = pxy + sxy * pf2{(float)(n - 1), (float)(n - 1)};
+          pzr = pzr + szr * pf2{(float)(n - 1), (float)(n - 1)};
+          if (true) {
+            if (!(pzr.y < tfar)) live = false;
+            pxy = pxy + sxy;
+            pzr = pzr + szr;
+            nextp = {pxy.x, pxy.y, pzr.x};
+            ray_len = pzr.y;
+            nsk += (uint32_t)n;
+            if (!live) break;
+            continue;
+          }
+#else
+          const int nf = min(n, max(0, (int)((tfar - ray_len) * rstep) - 2));
+#endif
+          int i = 0;
+          for (; i + 8 <= nf; i += 8) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+              pxy = pxy + sxy;
+              pzr = pzr + szr;
+            }
+          }
+          for (; i < nf; ++i) {
+            pxy = pxy + sxy;
+            pzr = pzr + szr;
+          }
+          for (; i < n; ++i) {
+            if (!(pzr.y < tfar)) {  // the loop ends inside the skipped samples: no event
+              live = false;
+              break;
+            }
+            pxy = pxy + sxy;
+            pzr = pzr + szr;
+          }
+          nextp = {pxy.x, pxy.y, pzr.x};
+          ray_len = pzr.y;
+          nsk += (uint32_t)n;
+          if (!live) break;
+        }
+        if (nsk != 0u && live) {
+          kbase += nsk;
+          tprev = voxel2tsdf(v, rc, nextp);
+          sprev = isnan(tprev) ? 0 : (tprev > 0.f ? 1 : (tprev < 0.f ? -1 : 0));
+        }
+      }
+      if (!__any(live)) break;
       int16_t raw[kR];
       unsigned pm = 0u, nm = 0u, am = 0u, ownm = 0u;
+      if (kStats || kTrace) st_batches += live ? 1u : 0u;
       float rl = ray_len;
       const f3 p0 = nextp;  // position before the batch's first sample
       // Interior batch: if the first and (estimated) last sample round into the
@@ -1662,14 +1869,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KFX_RAY_OCC
       ray_len = rl;
       kbase += kR;
     }
+    if (kStats) st_cand += cand ? 1u : 0u;
+#ifdef KFX_RAY_TRACE
+    if (__any(cand) && !t_norm) t_norm = wall_clock64();
+#endif
     if (cand) {  // the wave's normal pass
       cand = false;
+#ifdef KFX_RAY_NONORMAL  // timing experiment only (wrong values)
+      const f3 n = {cvert.x, 0.5f, 0.5f};
+#else
       const f3 n = compute_normal(v, rc, cvert);
+#endif
       if (!isnan(n.x * n.y * n.z)) {
-        // Rinv re-read from LDS here (volatile: not held in registers
-        // through the march)
+        // Rinv re-read from LDS here (volatile LDS reads: not held in
+        // registers through the march; a generic volatile pointer would
+        // become serialised flat loads)
         float ri[9];
-        const volatile float *vr = s_rinv;
+        const volatile __attribute__((address_space(3))) float *vr =
+            (const volatile __attribute__((address_space(3))) float *)s_rinv;
 #pragma unroll
         for (int q = 0; q < 9; ++q) ri[q] = vr[q];
         nout = rmul(ri, n);
@@ -1684,7 +1901,40 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KFX_RAY_OCC
         tprev = r_tprev;
       }
     }
+#ifdef KFX_RAY_TRACE
+    t_ndone = wall_clock64();
+#endif
     }
+  }
+#ifdef KFX_RAY_TRACE
+  if (!kStats && ra.stats) {  // debug: per-wave {start, end, xcc<<32|hw_id, lookups<<32|batches} of lane 0
+    unsigned long long *r = ra.stats + 8 * ((size_t)blockIdx.x * 4 + (threadIdx.x >> 6));
+    unsigned lk = st_lookups, bt = st_batches;
+    for (int off = 32; off > 0; off >>= 1) {
+      lk = max(lk, (unsigned)__shfl_xor((int)lk, off));
+      bt = max(bt, (unsigned)__shfl_xor((int)bt, off));
+    }
+    if (lane == 0) {
+      r[0] = t_start;
+      r[1] = wall_clock64();
+      r[2] = ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |
+             (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+      r[3] = ((unsigned long long)lk << 32) | bt;
+      r[4] = t_march;
+      r[5] = t_norm;
+      r[6] = t_ndone;
+    }
+  }
+#endif
+  if (kStats) {
+    const unsigned c[6] = {st_rays, st_lookups, st_skipped, st_blocked, st_batches, st_cand};
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      unsigned x = c[k];
+      for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
+      if (lane == 0) atomicAdd(&ra.stats[k], (unsigned long long)x);
+    }
+    return;
   }
   if (inimg) {
     st3(prev.v[0], o, vout);
@@ -2095,6 +2345,23 @@ __global__ __launch_bounds__(256) void k_checksum(VolView v, unsigned long long 
   }
 }
 
+// Occupancy maps of the whole stored volume (after an upload; the maps were
+// cleared): wave = one brick (column tile x 8 slices), lane = one column.
+__global__ __launch_bounds__(256) void k_occ_rebuild(VolView v) {
+  const int lane = threadIdx.x & 63;
+  const size_t w = (size_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (w >= (size_t)v.tiles_x * v.tiles_y * v.nbz) return;
+  const int tile = (int)(w / v.nbz), lb = (int)(w % v.nbz);
+  const int z0 = max((v.bz0 + lb) * 8, v.zb), z1 = min((v.bz0 + lb) * 8 + 8, v.zb + v.zn);
+  int lo = INT_MAX, hi = -1;
+  for (int z = z0; z < z1; ++z)
+    if (v.tsdf[(size_t)tile * v.tile_voxels() + (size_t)(z - v.zb) * 64 + lane] < 0) {
+      lo = min(lo, z);
+      hi = max(hi, z);
+    }
+  occ_mark_wave(v, tile, lo, hi, lane);
+}
+
 __global__ void k_export_soa(VolView v, int z0, int nz, int16_t *t, int16_t *w, uint32_t *c) {
   const size_t n = v.slice * (size_t)nz;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
@@ -2169,7 +2436,7 @@ static int g_int_trace_waves = 0;
 extern "C" int kfx_debug_integrate_trace(unsigned long long *out, int cap) {
   const int n = std::min(cap, kfx::g_int_trace_waves);
   if (hipDeviceSynchronize() != hipSuccess) return -1;
-  if (hipMemcpy(out, kfx::g_int_trace, sizeof(unsigned long long) * 4 * n, hipMemcpyDeviceToHost) != hipSuccess)
+  if (hipMemcpy(out, kfx::g_int_trace, sizeof(unsigned long long) * 8 * n, hipMemcpyDeviceToHost) != hipSuccess)
     return -1;
   return n;
 }
@@ -2307,21 +2574,61 @@ void launch_integrate(hipStream_t s, VolView v, LevelGeom g0, const float2 *dl0,
                        vpose, xpose, counters);
 }
 
+#ifdef KFX_RAY_TRACE
+static unsigned long long *g_ray_trace = nullptr;
+static int g_ray_trace_waves = 0;
+}  // namespace kfx
+// debug build only: the last raycast launch's per-wave records
+extern "C" int kfx_debug_raycast_trace(unsigned long long *out, int cap) {
+  const int n = std::min(cap, kfx::g_ray_trace_waves);
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpy(out, kfx::g_ray_trace, sizeof(unsigned long long) * 8 * n, hipMemcpyDeviceToHost) != hipSuccess)
+    return -1;
+  return n;
+}
+namespace kfx {
+#endif
 void launch_raycast(hipStream_t s, VolView v, int levels, const LevelGeom *g, FrameView cur,
                     FrameView prev, const DevState *st, const DevPose *log, DevPose vpose,
-                    const float *xpose, uint32_t *keys) {
+                    const float *xpose, uint32_t *keys, unsigned long long *stats) {
+  const bool want_stats = stats != nullptr;
+#ifdef KFX_RAY_TRACE
+  if (!stats) {
+    if (!g_ray_trace) (void)hipMalloc(&g_ray_trace, sizeof(unsigned long long) * 8 * (1 << 16));
+    g_ray_trace_waves = (int)(((g[0].w + 15) / 16) * ((g[0].h + 15) / 16) * 4);
+    stats = g_ray_trace;
+  }
+#endif
   RayConsts rc;
   rc.vs = {v.vs[0], v.vs[1], v.vs[2]};
   rc.vs_inv = {1.f / v.vs[0], 1.f / v.vs[1], 1.f / v.vs[2]};
   rc.gd = {v.vs[0] * 0.5f, v.vs[1] * 0.5f, v.vs[2] * 0.5f};
   rc.step = v.vs[0];
+  // half an ulp of a position inside the volume is <= max_dim * 2^-23 voxels
+  rc.skip_cap = std::min(511.f, std::floor(0.1f * 8388608.f / (float)std::max(v.X, std::max(v.Y, v.Z))));
   RayArgs ra{};
   ra.levels = levels;
+  ra.stats = stats;
   for (int l = 0; l < levels; ++l) ra.g[l] = g[l];
   dim3 grd(((g[0].w + 15) / 16) * ((g[0].h + 15) / 16));
   // 32-bit tsdf byte offsets (24-bit operands of the tile * zn products)
   const bool idx32 = v.local_voxels() < (1ull << 31) && (size_t)v.tiles_x * v.tiles_y < (1ull << 24) &&
                      v.zn < (1 << 24);
+  if (want_stats) {
+    if (keys && idx32)
+      hipLaunchKernelGGL((k_raycast<true, true, true>), grd, dim3(256), 0, s, v, ra, rc, cur, prev, st, log,
+                         vpose, xpose, keys);
+    else if (keys)
+      hipLaunchKernelGGL((k_raycast<false, true, true>), grd, dim3(256), 0, s, v, ra, rc, cur, prev, st, log,
+                         vpose, xpose, keys);
+    else if (idx32)
+      hipLaunchKernelGGL((k_raycast<true, false, true>), grd, dim3(256), 0, s, v, ra, rc, cur, prev, st, log,
+                         vpose, xpose, keys);
+    else
+      hipLaunchKernelGGL((k_raycast<false, false, true>), grd, dim3(256), 0, s, v, ra, rc, cur, prev, st, log,
+                         vpose, xpose, keys);
+    return;
+  }
   if (keys) {
     if (idx32)
       hipLaunchKernelGGL((k_raycast<true, true>), grd, dim3(256), 0, s, v, ra, rc, cur, prev, st, log,
@@ -2438,6 +2745,13 @@ void launch_checksum(hipStream_t s, VolView v, unsigned long long *out) {
 void launch_export_soa(hipStream_t s, VolView v, int z0, int nz, int16_t *t, int16_t *w,
                        uint32_t *c) {
   hipLaunchKernelGGL(k_export_soa, slab_grid(v, nz), dim3(256), 0, s, v, z0, nz, t, w, c);
+}
+
+void launch_occ_rebuild(hipStream_t s, VolView v) {
+  (void)hipMemsetAsync(v.bocc, 0, v.bocc_bytes(), s);
+  (void)hipMemsetAsync(v.socc, 0, v.socc_bytes(), s);
+  const size_t waves = (size_t)v.tiles_x * v.tiles_y * v.nbz;
+  hipLaunchKernelGGL(k_occ_rebuild, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, v);
 }
 
 }  // namespace kfx

@@ -33,7 +33,7 @@ EXPORTS = [
     "kfx_write_poses_txt", "kfx_get_frame_maps", "kfx_set_frame_maps", "kfx_download_tsdf",
     "kfx_upload_tsdf", "kfx_download_volume_soa", "kfx_stage_preprocess", "kfx_stage_icp_accumulate",
     "kfx_stage_icp", "kfx_stage_integrate", "kfx_stage_raycast", "kfx_set_profiling", "kfx_get_stage_ms",
-    "kfx_integrate_counts", "kfx_integrate_stats", "kfx_create_slab", "kfx_slab_info", "kfx_comm_get_unique_id", "kfx_comm_init",
+    "kfx_integrate_counts", "kfx_integrate_stats", "kfx_raycast_stats", "kfx_create_slab", "kfx_slab_info", "kfx_comm_get_unique_id", "kfx_comm_init",
     "kfx_pipeline_group", "kfx_render", "kfx_volume_checksum", "kfx_extract_points", "kfx_write_ply", "kfx_save_pointcloud",
     "kfx_extract_mesh", "kfx_write_ply_mesh",
     "kfx_dataset_open", "kfx_dataset_info", "kfx_dataset_read", "kfx_dataset_close", "kfx_png_info",
@@ -99,6 +99,7 @@ def lib():
         "kfx_get_stage_ms": ([vp, P(f)], i),
         "kfx_integrate_counts": ([vp, P(C.c_int64), P(C.c_int64)], i),
         "kfx_integrate_stats": ([vp, P(C.c_int64)], i),
+        "kfx_raycast_stats": ([vp, P(C.c_int64)], i),
         "kfx_create_slab": ([P(Intrinsics), P(Params), i, i, i, P(vp)], i),
         "kfx_slab_info": ([vp, P(i), P(i), P(i), P(i)], i),
         "kfx_comm_get_unique_id": ([P(C.c_uint8)], i),
@@ -365,6 +366,13 @@ class KinectFusion:
         a = (C.c_int64 * 8)()
         _check(lib().kfx_integrate_stats(self._h, a), "kfx_integrate_stats")
         return dict(zip(["updated", "colored", "visited", "gathered", "wave_batches"], a[:5]))
+
+    def raycast_stats(self) -> dict:
+        """Work of the last frame's raycast (re-run, nothing written)."""
+        a = (C.c_int64 * 8)()
+        _check(lib().kfx_raycast_stats(self._h, a), "kfx_raycast_stats")
+        return dict(zip(["rays", "skip_lookups", "skipped_samples", "blocked_lookups", "batches",
+                         "normal_candidates"], a[:6]))
 
     def volume_checksum(self) -> tuple:
         """(hash sum mod 2^64, voxels with weight > 0) over the owned slices."""
