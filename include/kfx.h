@@ -200,6 +200,13 @@ int kfx_integrate_stats(kfx_ctx *ctx, int64_t out[8]);
  * samples skipped by them, lookups that found an occupied brick, 14-sample
  * batches marched (per ray), hit candidates whose normal was computed, 0, 0}. */
 int kfx_raycast_stats(kfx_ctx *ctx, int64_t out[8]);
+/* Voxel records of n selected (x, y) columns over this context's owned slices
+ * [own0, own1) (test seam for volumes too large to download whole): cols =
+ * n int32 (x, y) pairs; each output holds n * (own1 - own0) entries, column
+ * after column, z ascending (rgb: u8 c0, c1, c2, 0 per voxel).  Any output
+ * may be null. */
+int kfx_download_columns(kfx_ctx *ctx, const int32_t *cols, int n, int16_t *tsdf, int16_t *weight,
+                         uint32_t *rgb);
 
 /* ---- point cloud ------------------------------------------ */
 /* TSDFVolume::fetchPointCloud buffer size (tsdf_volume.cpp:67) */

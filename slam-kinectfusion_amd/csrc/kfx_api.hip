@@ -1035,6 +1035,35 @@ int kfx_upload_tsdf(kfx_ctx *c, const void *src) {
   return KFX_OK;
 }
 
+int kfx_download_columns(kfx_ctx *c, const int32_t *cols, int n, int16_t *t, int16_t *w, uint32_t *rgb) {
+  int r = check_ctx(c);
+  if (r) return r;
+  if (n < 0 || (n > 0 && !cols)) return set_err(KFX_ERR_ARG, "bad columns");
+  for (int k = 0; k < n; ++k)
+    if (cols[2 * k] < 0 || cols[2 * k] >= c->vol.X || cols[2 * k + 1] < 0 || cols[2 * k + 1] >= c->vol.Y)
+      return set_err(KFX_ERR_ARG, "column outside the volume");
+  if (n == 0) return KFX_OK;
+  const size_t cnt = (size_t)n * (c->vol.own1 - c->vol.own0);
+  char *tmp = nullptr;
+  HIPCHK(hipMalloc(&tmp, (size_t)n * 8 + cnt * 8));
+  int32_t *dcols = (int32_t *)tmp;
+  int16_t *dt = (int16_t *)(tmp + (size_t)n * 8);
+  int16_t *dw = dt + cnt;
+  uint32_t *dc = (uint32_t *)(dw + cnt);
+  hipError_t e = hipMemcpyAsync(dcols, cols, (size_t)n * 8, hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) {
+    launch_gather_columns(c->stream, c->vol, dcols, n, dt, dw, dc);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess && t) e = hipMemcpyAsync(t, dt, cnt * 2, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess && w) e = hipMemcpyAsync(w, dw, cnt * 2, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess && rgb) e = hipMemcpyAsync(rgb, dc, cnt * 4, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  (void)hipFree(tmp);
+  if (e != hipSuccess) return set_err(KFX_ERR_HIP, std::string("download_columns: ") + hipGetErrorString(e));
+  return KFX_OK;
+}
+
 int kfx_download_volume_soa(kfx_ctx *c, int16_t *t, int16_t *w, uint8_t *rgba) {
   int r = check_ctx(c);
   if (r) return r;

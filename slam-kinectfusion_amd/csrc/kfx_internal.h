@@ -192,5 +192,8 @@ void launch_export_soa(hipStream_t s, VolView v, int z0, int nz, int16_t *t, int
 // clear the occupancy maps and re-mark every brick holding a negative tsdf
 // (after a volume upload)
 void launch_occ_rebuild(hipStream_t s, VolView v);
+// owned-slice records of n (x, y) columns (device cols), column-major outputs
+void launch_gather_columns(hipStream_t s, VolView v, const int32_t *cols, int n, int16_t *t, int16_t *w,
+                           uint32_t *c);
 
 }  // namespace kfx

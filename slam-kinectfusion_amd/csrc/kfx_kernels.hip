@@ -2362,6 +2362,18 @@ __global__ __launch_bounds__(256) void k_occ_rebuild(VolView v) {
   occ_mark_wave(v, tile, lo, hi, lane);
 }
 
+__global__ void k_gather_columns(VolView v, const int32_t *cols, int n, int16_t *t, int16_t *w, uint32_t *c) {
+  const int nz = v.own1 - v.own0;
+  const size_t total = (size_t)n * nz;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int k = (int)(i / nz), z = v.own0 + (int)(i % nz);
+    const size_t s = vox_index(v, cols[2 * k], cols[2 * k + 1], z);
+    if (t) t[i] = v.tsdf[s];
+    if (w) w[i] = v.weight[s];
+    if (c) c[i] = v.rgb[s];
+  }
+}
+
 __global__ void k_export_soa(VolView v, int z0, int nz, int16_t *t, int16_t *w, uint32_t *c) {
   const size_t n = v.slice * (size_t)nz;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
@@ -2745,6 +2757,13 @@ void launch_checksum(hipStream_t s, VolView v, unsigned long long *out) {
 void launch_export_soa(hipStream_t s, VolView v, int z0, int nz, int16_t *t, int16_t *w,
                        uint32_t *c) {
   hipLaunchKernelGGL(k_export_soa, slab_grid(v, nz), dim3(256), 0, s, v, z0, nz, t, w, c);
+}
+
+void launch_gather_columns(hipStream_t s, VolView v, const int32_t *cols, int n, int16_t *t, int16_t *w,
+                           uint32_t *c) {
+  const size_t total = (size_t)n * (v.own1 - v.own0);
+  const unsigned b = (unsigned)std::min<size_t>(8192, (total + 255) / 256);
+  hipLaunchKernelGGL(k_gather_columns, dim3(std::max(1u, b)), dim3(256), 0, s, v, cols, n, t, w, c);
 }
 
 void launch_occ_rebuild(hipStream_t s, VolView v) {

@@ -33,7 +33,7 @@ EXPORTS = [
     "kfx_write_poses_txt", "kfx_get_frame_maps", "kfx_set_frame_maps", "kfx_download_tsdf",
     "kfx_upload_tsdf", "kfx_download_volume_soa", "kfx_stage_preprocess", "kfx_stage_icp_accumulate",
     "kfx_stage_icp", "kfx_stage_integrate", "kfx_stage_raycast", "kfx_set_profiling", "kfx_get_stage_ms",
-    "kfx_integrate_counts", "kfx_integrate_stats", "kfx_raycast_stats", "kfx_create_slab", "kfx_slab_info", "kfx_comm_get_unique_id", "kfx_comm_init",
+    "kfx_integrate_counts", "kfx_integrate_stats", "kfx_raycast_stats", "kfx_download_columns", "kfx_create_slab", "kfx_slab_info", "kfx_comm_get_unique_id", "kfx_comm_init",
     "kfx_pipeline_group", "kfx_render", "kfx_volume_checksum", "kfx_extract_points", "kfx_write_ply", "kfx_save_pointcloud",
     "kfx_extract_mesh", "kfx_write_ply_mesh",
     "kfx_dataset_open", "kfx_dataset_info", "kfx_dataset_read", "kfx_dataset_close", "kfx_png_info",
@@ -100,6 +100,7 @@ def lib():
         "kfx_integrate_counts": ([vp, P(C.c_int64), P(C.c_int64)], i),
         "kfx_integrate_stats": ([vp, P(C.c_int64)], i),
         "kfx_raycast_stats": ([vp, P(C.c_int64)], i),
+        "kfx_download_columns": ([vp, P(C.c_int32), i, P(C.c_int16), P(C.c_int16), P(C.c_uint32)], i),
         "kfx_create_slab": ([P(Intrinsics), P(Params), i, i, i, P(vp)], i),
         "kfx_slab_info": ([vp, P(i), P(i), P(i), P(i)], i),
         "kfx_comm_get_unique_id": ([P(C.c_uint8)], i),
@@ -454,6 +455,19 @@ class KinectFusion:
         c = np.zeros(4 * self.nvox, np.uint8)
         _check(lib().kfx_download_volume_soa(self._h, i16ptr(t), i16ptr(w), u8ptr(c)), "kfx_download_volume_soa")
         return t, w, c
+
+    def download_columns(self, cols):
+        """(tsdf, weight, rgb u8x4) of (x, y) columns over the owned slices, shape (n, nz)."""
+        cols = np.ascontiguousarray(cols, np.int32).reshape(-1, 2)
+        n = cols.shape[0]
+        _, _, o0, o1 = self.slab_info()
+        t = np.zeros((n, o1 - o0), np.int16)
+        w = np.zeros((n, o1 - o0), np.int16)
+        c = np.zeros((n, o1 - o0), np.uint32)
+        _check(lib().kfx_download_columns(self._h, cols.ctypes.data_as(C.POINTER(C.c_int32)), n, i16ptr(t),
+                                          i16ptr(w), c.ctypes.data_as(C.POINTER(C.c_uint32))),
+               "kfx_download_columns")
+        return t, w, c.view(np.uint8).reshape(n, o1 - o0, 4)
 
     # ---- stage seams -----------------------------------------------------
     def stage_preprocess(self, color, depth_mm):
