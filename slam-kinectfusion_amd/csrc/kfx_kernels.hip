@@ -1222,26 +1222,41 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
     const double zfar = ((double)dmax + (double)v.trunc) * 1.02 + 0.01;
     clip_lin(zfar - az, -sz, lo, hi);
   }
-  int za = 1, zb = 0;  // this lane's chunk of its column interval (empty: none)
+  // this lane's candidate interval [zl, zh] (empty: zl > zh)
+  int zl = INT_MAX, zh = INT_MIN;
   if (hi >= lo) {
-    const int zlo = max((int)lo0, (int)floor(lo) - 2);
-    const int zhi = min((int)hi0, (int)ceil(hi) + 2);
-    if (zhi >= zlo) {
-      const int len = zhi - zlo + 1;
-#if KFX_INT_CHUNKR == 100
-      za = zlo + (int)((long long)len * chunk / nchunk);
-      zb = zlo + (int)((long long)len * (chunk + 1) / nchunk) - 1;
-#else
-      // chunk c gets weight r^c: the chunks dispatched last (highest
-      // blockIdx.y) are the shortest, so the kernel's tail waves are short
-      const float r = (float)KFX_INT_CHUNKR * 0.01f;
-      const float den = 1.f - __powf(r, (float)nchunk);
-      za = zlo + (int)((float)len * ((1.f - __powf(r, (float)chunk)) / den));
-      zb = chunk + 1 == nchunk ? zhi : zlo + (int)((float)len * ((1.f - __powf(r, (float)(chunk + 1))) / den)) - 1;
-#endif
-    }
+    zl = max((int)lo0, (int)floor(lo) - 2);
+    zh = min((int)hi0, (int)ceil(hi) + 2);
+    if (zh < zl) zl = INT_MAX, zh = INT_MIN;
   }
-  const bool live = zb >= za;
+  // The wave takes a chunk of the UNION of its lanes' intervals, so all 64
+  // lanes step the same z and each voxel load / store of the wave is one
+  // 128-B line (per-lane intervals put the lanes on different slices: one
+  // line per lane); a lane only updates voxels inside its own interval.
+  int wl = zl, wh = zh;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    wl = min(wl, __shfl_xor(wl, off));
+    wh = max(wh, __shfl_xor(wh, off));
+  }
+  if (wh < wl) return;  // wave-uniform
+  int za, zb;
+  {
+    const int len = wh - wl + 1;
+#if KFX_INT_CHUNKR == 100
+    za = wl + (int)((long long)len * chunk / nchunk);
+    zb = wl + (int)((long long)len * (chunk + 1) / nchunk) - 1;
+#else
+    // chunk c gets weight r^c: the chunks dispatched last (highest
+    // blockIdx.y) are the shortest, so the kernel's tail waves are short
+    const float r = (float)KFX_INT_CHUNKR * 0.01f;
+    const float den = 1.f - __powf(r, (float)nchunk);
+    za = wl + (int)((float)len * ((1.f - __powf(r, (float)chunk)) / den));
+    zb = chunk + 1 == nchunk ? wh : wl + (int)((float)len * ((1.f - __powf(r, (float)(chunk + 1))) / den)) - 1;
+#endif
+  }
+  const int la = max(za, zl), lb = min(zb, zh);  // this lane's voxels of the chunk
+  const bool live = lb >= la;
   if (__all(!live)) return;
 
   const float trunc = v.trunc;
@@ -1294,11 +1309,11 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
           // compare per axis is the float range test [0, w) of the rounded
           // value; 24-bit multiply (w, h < 2^24)
           const int iu = (int)rintf(uu[k]), iv = (int)rintf(vv[k]);
-          ok[j + k] = (z + j + k <= zb) & (pz[k] > 0) & ((unsigned)iu < (unsigned)g.w) & ((unsigned)iv < (unsigned)g.h);
+          ok[j + k] = (z + j + k >= la) & (z + j + k <= lb) & (pz[k] > 0) & ((unsigned)iu < (unsigned)g.w) & ((unsigned)iv < (unsigned)g.h);
           pix[j + k] = ok[j + k] ? __umul24((unsigned)iv, 8u * (unsigned)g.w) + ((unsigned)iu << 3) : kOob;
 #else
           const float uf = rintf(uu[k]), vf = rintf(vv[k]);
-          ok[j + k] = (z + j + k <= zb) & (pz[k] > 0) & (uf >= 0.f) & (uf < fw) & (vf >= 0.f) & (vf < fh);
+          ok[j + k] = (z + j + k >= la) & (z + j + k <= lb) & (pz[k] > 0) & (uf >= 0.f) & (uf < fw) & (vf >= 0.f) & (vf < fh);
           pix[j + k] = ok[j + k] ? ((unsigned)(int)vf * (unsigned)g.w + (unsigned)(int)uf) * 8u : kOob;
 #endif
         }
@@ -1308,14 +1323,18 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
       for (int j = 0; j < kB; ++j) {
         const float uf = rintf((p[j].x / p[j].z) * g.fx + g.cx);
         const float vf = rintf((p[j].y / p[j].z) * g.fy + g.cy);
-        ok[j] = (z + j <= zb) & (p[j].z > 0) & (uf >= 0.f) & (uf < fw) & (vf >= 0.f) & (vf < fh);
+        ok[j] = (z + j >= la) & (z + j <= lb) & (p[j].z > 0) & (uf >= 0.f) & (uf < fw) & (vf >= 0.f) & (vf < fh);
         pix[j] = ok[j] ? ((unsigned)(int)vf * (unsigned)g.w + (unsigned)(int)uf) * 8u : kOob;
       }
     }
     float2 d[kB];
 #pragma unroll
     for (int j = 0; j < kB; ++j)
+#if KFX_INT_EXP == 1  // timing experiment only (wrong values): contiguous gather addresses
+      d[j] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rdl, pix[j] == kOob ? kOob : 8u * (unsigned)lane + 4096u * (unsigned)j, 0, 0));
+#else
       d[j] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rdl, pix[j], 0, 0));
+#endif
     // sdf and the depth test (tsdf_volume.cu:67-71)
     if (fast) {
 #pragma unroll
@@ -1335,7 +1354,7 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
       ++cb;
 #pragma unroll
       for (int j = 0; j < kB; ++j) {
-        cv += (z + j <= zb);
+        cv += (z + j >= la) & (z + j <= lb);
         cg += (pix[j] != kOob);
       }
 #pragma unroll
@@ -1355,8 +1374,13 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
     for (int j = 0; j < kB; ++j) {
       vi[j] = iz + (Idx)j * slice;
       const Idx i = ok[j] ? vi[j] : Mem::kNone;
+#if KFX_INT_EXP == 2  // timing experiment only (wrong values): no voxel loads
+      t0[j] = 0;
+      w0[j] = (int16_t)(i == Mem::kNone ? 0 : 0);
+#else
       t0[j] = mem.ld_t(i);
       w0[j] = mem.ld_w(i);
+#endif
     }
     iz += (Idx)kB * slice;
 #pragma unroll
@@ -1380,8 +1404,10 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
       }
       // saturated voxels (w = 64 at a tsdf fixed point) keep their values:
       // skipping those stores changes nothing and saves write bandwidth
+#if KFX_INT_EXP != 3  // 3: timing experiment only (wrong values): no tsdf/weight stores
       if (q != t0[j]) mem.st_t(i, (int16_t)q);
       if (new_w != pre_w) mem.st_w(i, (int16_t)new_w);
+#endif
       if (sdf[j] <= thres_color && sdf[j] >= -thres_color) {  // colour band (rare)
         const uint32_t c0 = mem.ld_c(i);
         const uint8_t *px = bgr + 3 * (size_t)(pix[j] >> 3);
