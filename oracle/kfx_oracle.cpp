@@ -334,6 +334,37 @@ void kfo_pose_identity(kfx_pose *out) {
   out->R[0] = out->R[4] = out->R[8] = 1.f;
 }
 
+// D: cos / sin of the Rodrigues angle (cv::Affine3f(rvec, t) uses std::cos /
+// std::sin).  For theta < 0.5 (every ICP increment in practice) their Taylor
+// polynomials in theta^2, Horner form with separately rounded double ops
+// (truncation < 1e-19 relative; within an ulp or two of the libm values, then
+// rounded to float): the same operations as the kernel's det_sincos, so GPU
+// and oracle agree bit for bit; larger angles use libm on both sides.
+void kfo_sincos(double theta, double *s, double *c) {
+  if (!(theta < 0.5)) {
+    *s = std::sin(theta);
+    *c = std::cos(theta);
+    return;
+  }
+  const double x2 = theta * theta;
+  double ps = -1.0 / 1307674368000.0;
+  ps = ps * x2 + 1.0 / 6227020800.0;
+  ps = ps * x2 + -1.0 / 39916800.0;
+  ps = ps * x2 + 1.0 / 362880.0;
+  ps = ps * x2 + -1.0 / 5040.0;
+  ps = ps * x2 + 1.0 / 120.0;
+  ps = ps * x2 + -1.0 / 6.0;
+  *s = theta + theta * (x2 * ps);
+  double pc = -1.0 / 87178291200.0;
+  pc = pc * x2 + 1.0 / 479001600.0;
+  pc = pc * x2 + -1.0 / 3628800.0;
+  pc = pc * x2 + 1.0 / 40320.0;
+  pc = pc * x2 + -1.0 / 720.0;
+  pc = pc * x2 + 1.0 / 24.0;
+  pc = pc * x2 + -0.5;
+  *c = 1.0 + x2 * pc;
+}
+
 // icp_registration.cpp:33-42: A/b unpack (rigid_icp.cu:156-165), det check
 // (cv::determinant, LU), solve (D: LU with partial pivoting and pivot
 // reciprocals instead of SVD),
@@ -395,7 +426,9 @@ int kfo_icp_update(const int64_t sums[27], kfx_pose *pose, double x_out[6]) {
   if (theta < 2.220446049250313e-16) {
     for (int i = 0; i < 9; ++i) inc.R[i] = (i % 4 == 0) ? 1.f : 0.f;
   } else {
-    const double c = std::cos(theta), sn = std::sin(theta), c1 = 1.0 - c;
+    double c, sn;
+    kfo_sincos(theta, &sn, &c);
+    const double c1 = 1.0 - c;
     const double it = 1.0 / theta;
     const float r[3] = {(float)(rv[0] * it), (float)(rv[1] * it), (float)(rv[2] * it)};
     const float rrt[9] = {r[0] * r[0], r[0] * r[1], r[0] * r[2], r[0] * r[1], r[1] * r[1],

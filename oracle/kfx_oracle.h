@@ -63,6 +63,8 @@ void kfo_icp_accumulate(const float *cur_v, const float *cur_n,
                         float dist_thres, float angle_thres, int64_t sums[27]);
 /* det check + solve + Rodrigues + pose = pose * Tinc
  * (icp_registration.cpp:33-42).  Returns 0 ok, 1 tracking failure. */
+/* D: deterministic cos/sin of the Rodrigues angle (theta < 0.5: polynomial, else libm) */
+void kfo_sincos(double theta, double *s, double *c);
 int kfo_icp_update(const int64_t sums[27], kfx_pose *pose, double x_out[6]);
 /* ICPRegistration::rigidTransform (icp_registration.cpp:16-46). */
 int kfo_icp_track(float **cur_v, float **cur_n, float **pre_v, float **pre_n,

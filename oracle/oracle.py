@@ -47,6 +47,7 @@ def lib():
         L.kfo_preprocess.argtypes = [P(f), i, i, i, P(Intrinsics), P(Params), P(P(f)), P(P(f)), P(P(f))]
         L.kfo_icp_accumulate.argtypes = [P(f), P(f), P(f), P(f), i, i, P(Intrinsics), P(Pose), f, f,
                                          P(C.c_int64)]
+        L.kfo_sincos.argtypes = [C.c_double, P(C.c_double), P(C.c_double)]
         L.kfo_icp_update.argtypes = [P(C.c_int64), P(Pose), P(C.c_double)]
         L.kfo_icp_update.restype = i
         L.kfo_pose_mul.argtypes = [P(Pose), P(Pose), P(Pose)]
@@ -175,6 +176,13 @@ def icp_update(sums: np.ndarray, pose: Pose):
     x = (C.c_double * 6)()
     st = lib().kfo_icp_update(i64ptr(sums), C.byref(p), x)
     return st, p, np.array(x[:])
+
+
+def sincos(theta: float):
+    """kfo_sincos: the deterministic (sin, cos) of the Rodrigues step."""
+    a, b = C.c_double(), C.c_double()
+    lib().kfo_sincos(theta, C.byref(a), C.byref(b))
+    return a.value, b.value
 
 
 def pose_mul(a: Pose, b: Pose) -> Pose:

@@ -107,6 +107,7 @@ struct kfx_ctx {
   bool overlap = true;
   hipStream_t pstream = nullptr;
   hipEvent_t ev_prep = nullptr, ev_free[2]{};
+  hipEvent_t ev_icp = nullptr;  // after the last overlapped frame's ICP (the next preprocess starts there)
 
   // sampled kernel timing (kfx_set_kernel_timing): every `timing_every`-th
   // pipelined frame records its stage events into the next unused set
@@ -169,6 +170,9 @@ int dalloc(kfx_ctx *c, void **p, size_t bytes) {
   return KFX_OK;
 }
 
+#ifndef KFX_PREP_AFTER_ICP
+#define KFX_PREP_AFTER_ICP 1  // overlapped frames: next preprocess waits for this frame's ICP
+#endif
 #ifndef KFX_VOL_PAD
 #define KFX_VOL_PAD 4096  // weight offset past the 2 MiB-rounded tsdf (bytes)
 #endif
@@ -281,6 +285,7 @@ void enqueue_track(kfx_ctx *c, FrameInput in, hipEvent_t *ev, bool begin) {
     }
   }
   if (ev) (void)hipEventRecord(ev[2], s);
+  if (begin) (void)hipEventRecord(c->ev_icp, s);  // overlapped frames: the next preprocess waits here
   launch_integrate(s, c->vol, c->g[0], c->dl0, in.bgr, c->st, c->pose_log,
                    to_dev(c->p.volu_pose), nullptr, nullptr);
   if (ev) (void)hipEventRecord(ev[3], s);
@@ -300,6 +305,11 @@ int enqueue_frame_overlap(kfx_ctx *c, FrameInput in, hipEvent_t *ev) {
   set_par(c, p);
   hipStream_t b = c->pstream;
   HIPCHK(hipStreamWaitEvent(b, c->ev_free[p], 0));  // the frame before last is done with set p
+#if KFX_PREP_AFTER_ICP
+  // start behind the previous frame's ICP: the latency-bound persistent ICP
+  // then runs alone and the preprocess shares the GPU with integrate/raycast
+  HIPCHK(hipStreamWaitEvent(b, c->ev_icp, 0));
+#endif
   const float *raw[kMaxLevels];
   for (int l = 0; l < kMaxLevels; ++l) raw[l] = c->raw[l];
   raw[0] = in.d32;
@@ -644,7 +654,7 @@ static int create_impl(const kfx_intrinsics *intr, const kfx_params *params, int
   if (hipStreamCreateWithFlags(&c->pstream, hipStreamNonBlocking) != hipSuccess)
     return fail(set_err(KFX_ERR_HIP, "hipStreamCreate failed"));
   // cross-stream ordering on one device: a device-scope release suffices
-  for (hipEvent_t *e : {&c->ev_prep, &c->ev_free[0], &c->ev_free[1]})
+  for (hipEvent_t *e : {&c->ev_prep, &c->ev_free[0], &c->ev_free[1], &c->ev_icp})
     if (hipEventCreateWithFlags(e, hipEventDisableTiming | hipEventReleaseToDevice) != hipSuccess)
       return fail(set_err(KFX_ERR_HIP, "hipEventCreate failed"));
 
@@ -714,7 +724,7 @@ int kfx_destroy(kfx_ctx *c) {
   for (void *a : c->allocs) (void)hipFree(a);
   for (auto &e : c->ev)
     if (e) (void)hipEventDestroy(e);
-  for (hipEvent_t e : {c->ev_prep, c->ev_free[0], c->ev_free[1]})
+  for (hipEvent_t e : {c->ev_prep, c->ev_free[0], c->ev_free[1], c->ev_icp})
     if (e) (void)hipEventDestroy(e);
   for (hipEvent_t e : c->tsets) (void)hipEventDestroy(e);
   if (c->pstream) (void)hipStreamDestroy(c->pstream);

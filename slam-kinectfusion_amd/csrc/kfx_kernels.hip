@@ -24,9 +24,6 @@
 #ifndef KFX_RAY_KR
 #define KFX_RAY_KR 14  // raycast: samples per batch (loads in flight per lane)
 #endif
-#ifndef KFX_SINCOS
-#define KFX_SINCOS 1
-#endif
 #ifndef KFX_INT_OCC
 #define KFX_INT_OCC 8  // integrate: waves per SIMD the register budget is sized for
 #endif
@@ -450,7 +447,12 @@ __global__ __launch_bounds__(256) void k_preprocess_maps(BilatArgs a) {
 #define KFX_ICP_PIX 4
 #endif
 constexpr int kIcpPix = KFX_ICP_PIX;
-constexpr int kIcpBlockPix = 256 * kIcpPix;
+#ifndef KFX_ICP_THREADS
+#define KFX_ICP_THREADS 256  // ICP: threads per block
+#endif
+constexpr int kIcpThreads = KFX_ICP_THREADS;
+constexpr int kIcpWaves = kIcpThreads / 64;
+constexpr int kIcpBlockPix = kIcpThreads * kIcpPix;
 constexpr unsigned long long kIcpWatchdogTicks = 20000000ull;  // >= 0.2 s of s_memrealtime
 __device__ int icp_update(const long long *sums, DevPose &pose, double *xo);
 
@@ -535,7 +537,7 @@ __device__ __forceinline__ void icp_load_cur(const LevelGeom &g, int xe, int npi
                                              f3 (&v0)[kIcpPix], bool (&ok)[kIcpPix]) {
 #pragma unroll
   for (int q = 0; q < kIcpPix; ++q) {
-    const int i = grp * 256 * ppl + q * 256 + threadIdx.x;
+    const int i = grp * kIcpThreads * ppl + q * kIcpThreads + threadIdx.x;
     ok[q] = q < ppl && i < npix;
     const size_t idx = ok[q] ? (size_t)(i / xe) * g.w + (i % xe) : 0;
     n0[q] = ld3(cn, idx);
@@ -543,7 +545,7 @@ __device__ __forceinline__ void icp_load_cur(const LevelGeom &g, int xe, int npi
   }
 }
 
-// Block reduction of the 256 lanes' 27 sums.  Within a wave, a reduce-scatter
+// Block reduction of the block's lanes' 27 sums.  Within a wave, a reduce-scatter
 // butterfly in registers: at each step a lane keeps the half of its values
 // selected by one lane bit and adds its partner's copy of that half, so after
 // 5 steps lane L holds value (L >> 1) summed over 32 lanes, and a last
@@ -554,7 +556,7 @@ __device__ __forceinline__ void icp_load_cur(const LevelGeom &g, int xe, int npi
 // 2^53: every order of fp64 adds is exact.  Returns, in threads 0..26, the
 // block's sum k as int64.
 struct IcpRed {
-  double red2[kIcpShards * 27];  // >= 4 * 27; also stages the shard reads
+  double red2[(kIcpShards > kIcpWaves ? kIcpShards : kIcpWaves) * 27];  // waves' sums; also stages the shard reads
 };
 __device__ __forceinline__ unsigned lo32(double v) { return (unsigned)__double_as_longlong(v); }
 __device__ __forceinline__ unsigned hi32(double v) {
@@ -618,7 +620,10 @@ __device__ __forceinline__ long long icp_block_reduce(IcpRed &r, const double (&
   long long v = 0;
   if (threadIdx.x < 27) {
     const int k = threadIdx.x;
-    v = (long long)(r.red2[k] + r.red2[27 + k] + r.red2[54 + k] + r.red2[81 + k]);
+    double a = r.red2[k];
+#pragma unroll
+    for (int q = 1; q < kIcpWaves; ++q) a += r.red2[27 * q + k];
+    v = (long long)a;
   }
   __syncthreads();  // red2 is reused by the caller
   return v;
@@ -626,7 +631,7 @@ __device__ __forceinline__ long long icp_block_reduce(IcpRed &r, const double (&
 
 // One ICP iteration per launch (stage API seam and the fallback when the
 // persistent kernel's grid cannot be co-resident).
-__global__ __launch_bounds__(256) void k_icp_acc(LevelGeom g, int xe, int npix,
+__global__ __launch_bounds__(kIcpThreads) void k_icp_acc(LevelGeom g, int xe, int npix,
                                                  const float *__restrict__ cv,
                                                  const float *__restrict__ cn,
                                                  const float *__restrict__ pv,
@@ -707,7 +712,7 @@ __global__ __launch_bounds__(256) void k_icp_acc(LevelGeom g, int xe, int npix,
 // begin: the frame's frame_begin is folded in (overlapped frames): every block
 // derives the begun state itself and block 0's thread 0, the only writer of
 // these fields during the kernel, stores it first
-__global__ __launch_bounds__(256, 2) void k_icp_track(IcpPlan pl, DevState *__restrict__ st,
+__global__ __launch_bounds__(kIcpThreads, 2) void k_icp_track(IcpPlan pl, DevState *__restrict__ st,
                                                    IcpSync *__restrict__ sy, int begin) {
   DevPose P;
   if (begin) {
@@ -845,7 +850,7 @@ __global__ __launch_bounds__(256, 2) void k_icp_track(IcpPlan pl, DevState *__re
   __syncthreads();
   if (sfail) {  // this block drew the last exit ticket
     const int n = slot * kIcpShards * 27;
-    for (int i = threadIdx.x; i < n; i += 256)
+    for (int i = threadIdx.x; i < n; i += kIcpThreads)
       __hip_atomic_store(&sy->sums[i], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (threadIdx.x == 0) {
       __hip_atomic_store(&sy->arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -873,6 +878,33 @@ __device__ __forceinline__ double bcast(double v, int src) {
 // bit-identical.  (The earlier partial-pivot LU spent most of its ~3.4k
 // cycles on data-dependent row moves.)  sums: 27 int64 (any memory, read by
 // all lanes).
+// D: cos / sin of the Rodrigues angle as the oracle's kfo_sincos (theta < 0.5:
+// Taylor polynomials in theta^2, separately rounded double ops; else ocml) —
+// bit-identical to the oracle and far shorter than ocml's sincos.
+__device__ __forceinline__ void det_sincos(double theta, double *s, double *c) {
+  if (!(theta < 0.5)) {  // wave-uniform
+    sincos(theta, s, c);
+    return;
+  }
+  const double x2 = theta * theta;
+  double ps = -1.0 / 1307674368000.0;
+  ps = ps * x2 + 1.0 / 6227020800.0;
+  ps = ps * x2 + -1.0 / 39916800.0;
+  ps = ps * x2 + 1.0 / 362880.0;
+  ps = ps * x2 + -1.0 / 5040.0;
+  ps = ps * x2 + 1.0 / 120.0;
+  ps = ps * x2 + -1.0 / 6.0;
+  *s = theta + theta * (x2 * ps);
+  double pc = -1.0 / 87178291200.0;
+  pc = pc * x2 + 1.0 / 479001600.0;
+  pc = pc * x2 + -1.0 / 3628800.0;
+  pc = pc * x2 + 1.0 / 40320.0;
+  pc = pc * x2 + -1.0 / 720.0;
+  pc = pc * x2 + 1.0 / 24.0;
+  pc = pc * x2 + -0.5;
+  *c = 1.0 + x2 * pc;
+}
+
 __device__ int icp_update(const long long *sums, DevPose &pose, double *xo) {
   double A[6][7];  // column 6 = b
   {
@@ -942,15 +974,7 @@ __device__ int icp_update(const long long *sums, DevPose &pose, double *xo) {
     for (int q = 0; q < 9; ++q) inc.R[q] = (q % 4 == 0) ? 1.f : 0.f;
   } else {
     double sn, c;
-#if KFX_SINCOS == 2  // timing experiment only (wrong values)
-    c = 1.0 - 0.5 * theta * theta;
-    sn = theta;
-#elif KFX_SINCOS
-    sincos(theta, &sn, &c);  // one shared range reduction
-#else
-    c = cos(theta);
-    sn = sin(theta);
-#endif
+    det_sincos(theta, &sn, &c);
     const double c1 = 1.0 - c;
     const double it = 1.0 / theta;
     const float r[3] = {(float)(rv[0] * it), (float)(rv[1] * it), (float)(rv[2] * it)};
@@ -1330,7 +1354,9 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
     float2 d[kB];
 #pragma unroll
     for (int j = 0; j < kB; ++j)
-#if KFX_INT_EXP == 1  // timing experiment only (wrong values): contiguous gather addresses
+#if KFX_INT_EXP == 4  // timing experiment only (wrong values): no depth gathers
+      d[j] = make_float2(pix[j] == kOob ? 0.f : 2.0f, 1.0f);
+#elif KFX_INT_EXP == 1  // timing experiment only (wrong values): contiguous gather addresses
       d[j] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rdl, pix[j] == kOob ? kOob : 8u * (unsigned)lane + 4096u * (unsigned)j, 0, 0));
 #else
       d[j] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rdl, pix[j], 0, 0));
@@ -1390,12 +1416,12 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
       // the identity — skip it (same stores skipped as below)
       if (!ok[j] || (w0[j] == kMaxWeight && t0[j] == v.tsat && sdf[j] >= trunc)) continue;
       const Idx i = vi[j];
-      const float ts = fminf(1.f, div_rn(sdf[j], trunc, v.inv_trunc));
       const int pre_w = w0[j];
+      const float ts = fminf(1.f, div_rn(sdf[j], trunc, v.inv_trunc));
       const float pre_t = (float)t0[j] * kDivShortMax;
       const int new_w = min(pre_w + 1, kMaxWeight);
-      const float new_t =
-          div_rn(fmaf(pre_t, (float)pre_w, ts), (float)(pre_w + 1), rtab[pre_w + 1]);
+      const float new_t = div_rn(fmaf(pre_t, (float)pre_w, ts), (float)(pre_w + 1),
+                                 (unsigned)pre_w <= (unsigned)kMaxWeight ? rtab[pre_w + 1] : 1.f / (float)(pre_w + 1));
       int q = (int)(new_t * (float)kShortMax);
       q = max(-kShortMax, min(kShortMax, q));
       if (q < 0) {
@@ -1412,7 +1438,7 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
         const uint32_t c0 = mem.ld_c(i);
         const uint8_t *px = bgr + 3 * (size_t)(pix[j] >> 3);
         const float c = (float)(new_w + 1);
-        const float rc = rtab[new_w + 1];
+        const float rc = (unsigned)new_w <= (unsigned)kMaxWeight ? rtab[new_w + 1] : 1.f / c;
         uint32_t out = 0u;
 #pragma unroll
         for (int ch = 0; ch < 3; ++ch) {
@@ -2542,8 +2568,8 @@ IcpPlan make_icp_plan(int levels, const LevelGeom *g, const int *iters, FrameVie
     pl.npix[l] = icp_npix(g[l], &pl.xe[l]);
     // pixels per lane: the fewest that keep the level within one block per
     // CU (256), so coarse levels spread over more waves (shorter lane phase)
-    pl.ppl[l] = std::max(1, std::min(kIcpPix, (pl.npix[l] + 256 * 256 - 1) / (256 * 256)));
-    pl.groups[l] = std::max(1, (pl.npix[l] + 256 * pl.ppl[l] - 1) / (256 * pl.ppl[l]));
+    pl.ppl[l] = std::max(1, std::min(kIcpPix, (pl.npix[l] + 256 * kIcpThreads - 1) / (256 * kIcpThreads)));
+    pl.groups[l] = std::max(1, (pl.npix[l] + kIcpThreads * pl.ppl[l] - 1) / (kIcpThreads * pl.ppl[l]));
     pl.iters[l] = iters[l];
     pl.cv[l] = cur.v[l];
     pl.cn[l] = cur.n[l];
@@ -2559,7 +2585,7 @@ IcpPlan make_icp_plan(int levels, const LevelGeom *g, const int *iters, FrameVie
 bool icp_persistent_ok(const IcpPlan &pl, int device) {
   if (pl.slots > kIcpMaxSlots) return false;
   int per_cu = 0, cus = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_icp_track, 256, 0) != hipSuccess)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_icp_track, kIcpThreads, 0) != hipSuccess)
     return false;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
     return false;
@@ -2567,7 +2593,7 @@ bool icp_persistent_ok(const IcpPlan &pl, int device) {
 }
 
 void launch_icp_track(hipStream_t s, const IcpPlan &pl, DevState *st, IcpSync *sync, int begin) {
-  hipLaunchKernelGGL(k_icp_track, dim3(pl.nblocks), dim3(256), 0, s, pl, st, sync, begin);
+  hipLaunchKernelGGL(k_icp_track, dim3(pl.nblocks), dim3(kIcpThreads), 0, s, pl, st, sync, begin);
 }
 
 void launch_icp(hipStream_t s, const LevelGeom &g, const float *cv, const float *cn,
@@ -2575,7 +2601,7 @@ void launch_icp(hipStream_t s, const LevelGeom &g, const float *cv, const float 
                 unsigned long long *shards, unsigned *ticket, int force, int update) {
   int xe;
   const int n = icp_npix(g, &xe);
-  hipLaunchKernelGGL(k_icp_acc, dim3(icp_blocks(g)), dim3(256), 0, s, g, xe, n, cv, cn, pv, pn,
+  hipLaunchKernelGGL(k_icp_acc, dim3(icp_blocks(g)), dim3(kIcpThreads), 0, s, g, xe, n, cv, cn, pv, pn,
                      dist_thr, angle_thr, st, shards, ticket, force, update);
 }
 

@@ -407,3 +407,21 @@ def test_render_kat(oracle_lib):
                 continue
             assert list(ph[y, x]) == _render_ref(v[y, x], n[y, x], eye), (y, x)
             assert list(nm[y, x]) == [int(np.float32(abs(c)) * np.float32(255)) for c in n[y, x]]
+
+
+def test_rodrigues_sincos_within_an_ulp_of_libm(oracle_lib):
+    """D: the Rodrigues cos/sin are Taylor polynomials for
+    theta < 0.5 (kfo_sincos, the kernel's det_sincos): within 1 ulp of libm in
+    double, and the float factors the pose update uses (float(c), float(1-c),
+    float(s) times unit-range values) round to libm's except at rounding ties."""
+    rng = np.random.default_rng(3)
+    th = np.concatenate([rng.uniform(0, 0.5, 20000), 10.0 ** rng.uniform(-12, -0.31, 20000), [1e-15, 0.4999999]])
+    worst, fdiff = 0.0, 0
+    for t in th:
+        s, c = oracle_lib.sincos(float(t))
+        worst = max(worst, abs(s - math.sin(t)) / math.ulp(math.sin(t)), abs(c - math.cos(t)) / math.ulp(math.cos(t)))
+        fdiff += np.float32(s) != np.float32(math.sin(t))
+        fdiff += np.float32(1.0 - c) != np.float32(1.0 - math.cos(t))
+    assert worst <= 1.0
+    assert fdiff <= 2
+    assert oracle_lib.sincos(0.7) == (math.sin(0.7), math.cos(0.7))  # libm above the polynomial range
