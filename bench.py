@@ -56,6 +56,11 @@ def parse():
     ap.add_argument("--unique", type=int, default=48, help="distinct frames rendered (played ping-pong)")
     ap.add_argument("--profile-frames", type=int, default=20)
     ap.add_argument("--cpu-frames", type=int, default=8, help="oracle frames timed for cpu_baseline (0 = skip)")
+    ap.add_argument("--c1-frames", type=int, default=100,
+                    help="oracle frames of the C1 record (128^3, same frames; 0 = skip)")
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r02_integrate_pmc.json"),
+                    help="integrate PMC traffic record; attached only when it was measured on this command's "
+                         "workload and step counts")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--sample-every", type=int, default=8,
                     help="time kernels on every k-th timed frame with HIP events (0 = off)")
@@ -77,24 +82,59 @@ def intrinsics(w, h):
     return synth.Intrinsics(w, h, 525.0 * s, 525.0 * s, (w - 1) / 2.0, (h - 1) / 2.0)
 
 
-def cpu_baseline(intr, params, bgr, dep, n):
+class pinned_to_one_core:
+    """Run the serial CPU baseline on one host core (taskset -c <first allowed
+    core> semantics for this process), restoring the affinity afterwards."""
+
+    def __enter__(self):
+        self.prev = os.sched_getaffinity(0)
+        self.core = min(self.prev)
+        os.sched_setaffinity(0, {self.core})
+        return self
+
+    def __exit__(self, *exc):
+        os.sched_setaffinity(0, self.prev)
+
+
+def cpu_baseline(intr, params, bgr, dep, order, n):
     """Serial oracle (TEST INFRASTRUCTURE, used here only as the reported CPU
-    baseline) on a bounded sample: frame 0 bootstraps untimed, frames 1..n timed."""
+    baseline) on a bounded sample, pinned to one core: the first frame of
+    `order` bootstraps untimed, the next n are timed."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     from kfx.abi import Intrinsics
     pipe = oracle.Pipeline(Intrinsics.from_any(intr), params)
-    pipe.process(bgr[0], dep[0].astype(np.float32))
-    t0 = time.perf_counter()
-    for k in range(1, n + 1):
-        pipe.process(bgr[k], dep[k].astype(np.float32))
-    dt = time.perf_counter() - t0
+    with pinned_to_one_core() as pin:
+        pipe.process(bgr[order[0]], dep[order[0]].astype(np.float32))
+        t0 = time.perf_counter()
+        for k in order[1:n + 1]:
+            assert pipe.process(bgr[k], dep[k].astype(np.float32)) == 0
+        dt = time.perf_counter() - t0
     return {"value": round(n / dt, 4), "unit": "frames/s", "cores": 1, "kind": "port",
             "ms_per_frame": round(1000.0 * dt / n, 1),
-            "sample": f"frames 1..{n} of the same synthetic sequence at the same config "
+            "sample": f"{n} frames after a bootstrap frame of the same synthetic sequence "
                       f"({intr.width}x{intr.height}, {params.volu_dims[0]}^3), full pipeline "
-                      f"(preprocess+ICP+integrate+raycast), single thread, oracle/kfx_oracle.cpp -O2",
-            "cpu": _cpu_model()}
+                      f"(preprocess+ICP+integrate+raycast), single thread pinned to core {pin.core}, "
+                      f"oracle/kfx_oracle.cpp -O2",
+            "host_cpus": os.cpu_count(), "cpu": _cpu_model()}
+
+
+def raycast_roofline(work, ms, W, H, ms_source):
+    """B_ray = 2 N_uniq + 24 W H, N_uniq = the distinct voxels
+    the reference raycast (no skipping) reads, counted on the device on the
+    last frame's state (kfx_raycast_stats, pinned against the oracle's count).
+    The empty-space skipping kernel reads far fewer: `kernel_tsdf_reads`
+    estimates its 2-B sample loads (14 per marched batch + the carried sample
+    after each skip run + 48 normal corners per hit candidate)."""
+    if not work or not work.get("ref_uniq_voxels") or not ms == ms:
+        return None
+    b = 2 * work["ref_uniq_voxels"] + 24 * W * H
+    achieved = b / (ms * 1e-3) / 1e9
+    return {"kernel": "k_raycast", "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+            "algorithmic_bytes_per_launch": int(b), "avg_launch_ms": round(ms, 4), "launch_ms_source": ms_source,
+            "ref_uniq_voxels": work["ref_uniq_voxels"], "ref_tsdf_reads": work["ref_reads"],
+            "kernel_tsdf_reads": int(14 * work["batches"] + work["blocked_lookups"] + 48 * work["normal_candidates"])}
 
 
 def _cpu_model():
@@ -148,14 +188,18 @@ class Dist:
 
 
 def timed_frames(kf, order, lo, hi, D):
-    """W/K contract: barrier + device sync on both sides, max over ranks."""
+    """W/K contract: barrier + device sync on both sides, max over ranks; a
+    frame dropped by a tracking failure fails the run."""
+    import kfx
     kf.synchronize()
     D.barrier()
     t0 = time.perf_counter()
     for i in range(lo, hi):
         kf.pipeline_staged(order[i])
-    kf.synchronize()
+    st = kf.synchronize()
     elapsed = time.perf_counter() - t0
+    if st != kfx.KFX_OK:
+        raise SystemExit("bench: a timed frame lost tracking (KFX_TRACKING_LOST)")
     elapsed = D.max(elapsed)
     D.barrier()
     return elapsed
@@ -228,6 +272,8 @@ def main():
     ktime = kf.kernel_timing() if a.sample_every > 0 else None
     kf.set_kernel_timing(0)
     tracked = kf.pose_record.shape[0] - n_before  # frames that appended a pose
+    if tracked != a.steps:  # a dropped frame (tracking reset) invalidates the measurement
+        raise SystemExit(f"bench: {a.steps - tracked} of {a.steps} timed frames were not tracked")
 
     # per-stage device ms + integrate roofline on further frames (profiled, eager)
     kf.set_profiling(True)
@@ -247,6 +293,8 @@ def main():
     ray_work = kf.raycast_stats() if a.profile_frames else None
     kf.synchronize()
     kf.close()
+    ray_ms = float(ktime["raycast"]) if ktime and ktime["samples"] > 0 else (
+        float(statistics.median(stages["raycast"])) if stages["raycast"] else float("nan"))
     stage_med = {k: round(statistics.median(v), 4) for k, v in stages.items()} if a.profile_frames else {}
     avg_bytes = float(np.mean(int_bytes)) if int_bytes else 0.0
     # the integrate launch duration of the roofline: the HIP-event samples of
@@ -256,17 +304,27 @@ def main():
     else:
         avg_ms, ms_source = (float(np.mean(int_ms)) if int_ms else float("nan")), "profiled frames"
     achieved = avg_bytes / (avg_ms * 1e-3) / 1e9 if avg_ms == avg_ms else 0.0
-    traffic = None
-    pmc_path = os.path.join(ROOT, "profiles", "integrate_pmc.json")
-    if os.path.exists(pmc_path) and not slab_main and (a.dims, W, H) == (512, 640, 480):
-        try:
-            traffic = json.load(open(pmc_path)).get("hbm_bytes_per_launch")
-        except (OSError, ValueError):
-            traffic = None
+    # HBM traffic of the integrate launch from a rocprofv3 FETCH_SIZE/WRITE_SIZE
+    # record (tools/prof.sh), attached only when that record was measured on
+    # this workload with the same step counts (the same saturation regime)
+    traffic, traffic_src = None, "none: no PMC record of this workload and step count"
+    try:
+        rec = json.load(open(a.traffic))
+        if (not slab_main and rec.get("workload") == [a.dims, W, H] and rec.get("steps") == a.steps
+                and rec.get("warmup") == a.warmup):
+            traffic = rec.get("hbm_bytes_per_launch")
+            traffic_src = f"{os.path.relpath(a.traffic, ROOT)}: {rec.get('command')} ({rec.get('regime')})"
+    except (OSError, ValueError):
+        pass
 
-    cpu = None
+    cpu = c1 = None
     if rank == 0 and world == 1 and a.cpu_frames > 0:
-        cpu = cpu_baseline(intr, params, bgr, dep, min(a.cpu_frames, a.unique - 1))
+        cpu = cpu_baseline(intr, params, bgr, dep, synth.ping_pong(a.unique, a.cpu_frames + 1), a.cpu_frames)
+    if rank == 0 and world == 1 and a.c1_frames > 0 and (W, H) == (640, 480):
+        # BASELINE C1: 128^3 TSDF (16 mm) on the same 640x480 frames, serial oracle
+        c1 = cpu_baseline(intr, default_params(dims=128, range_m=a.range), bgr, dep,
+                          synth.ping_pong(a.unique, a.c1_frames + 1), a.c1_frames)
+        c1["config"] = "C1: 128^3 TSDF @ 16 mm, 640x480 synthetic frames (the bundled dataset is absent)"
 
     frames = a.steps if slab_main else a.steps * world
     value = frames / elapsed
@@ -307,11 +365,14 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
+            "traffic_source": traffic_src,
             "algorithmic_bytes_per_launch": int(avg_bytes),
             "avg_launch_ms": round(avg_ms, 4),
             "launch_ms_source": ms_source,
         },
+        "roofline_raycast": raycast_roofline(ray_work, ray_ms, W, H, ms_source),
         "cpu_baseline": cpu,
+        "c1_record": c1,
     }
 
     if mode == "replicas" and a.zslab:

@@ -102,7 +102,11 @@ int kfx_pipeline_u16(kfx_ctx *ctx, const uint8_t *bgr, const uint16_t *depth_mm)
 
 /* Device-resident input: frames uploaded once with kfx_stage_frames are
  * processed without PCIe traffic and without a host sync (tracking state lives
- * on the device).  kfx_synchronize waits for queued frames. */
+ * on the device).  kfx_synchronize waits for queued frames
+ * and reports them: KFX_TRACKING_LOST if any frame completed since the last
+ * status check (kfx_pipeline, kfx_synchronize) was dropped by a tracking
+ * failure (reset() applied, kinectfusion.cpp:97-101), KFX_ERR_HIP if the ICP
+ * barrier watchdog fired, else KFX_OK. */
 int kfx_stage_frames(kfx_ctx *ctx, int n_frames, const uint8_t *bgr,
                      const float *depth_mm);
 int kfx_pipeline_staged(kfx_ctx *ctx, int frame_index);
@@ -198,7 +202,10 @@ int kfx_integrate_stats(kfx_ctx *ctx, int64_t out[8]);
 /* Work statistics of the last processed frame's raycast (re-run on the same
  * state, nothing written): out = {rays marched, empty-space skip lookups,
  * samples skipped by them, lookups that found an occupied brick, 14-sample
- * batches marched (per ray), hit candidates whose normal was computed, 0, 0}. */
+ * batches marched (per ray), hit candidates whose normal was computed,
+ * N_uniq = distinct voxels the reference raycast (tsdf_volume.cu:210-260, no
+ * skipping) reads — nearest samples plus the trilinear corners of the normals
+ * (0 for slab contexts), and the number of those reads}. */
 int kfx_raycast_stats(kfx_ctx *ctx, int64_t out[8]);
 /* Voxel records of n selected (x, y) columns over this context's owned slices
  * [own0, own1) (test seam for volumes too large to download whole): cols =

@@ -535,7 +535,16 @@ struct RayCtx {
   int64_t slice;
   V3 vs, vs_inv, gd;
   int zb, zn;  // slices that may be read: [zb, zb+zn) (the whole volume unless slab)
+  uint8_t *touch = nullptr;  // kfo_raycast_touched: 1 per voxel whose tsdf was read
+  int64_t *reads = nullptr;  // and the number of tsdf reads
 };
+inline float tsdf_at(const RayCtx &c, int64_t i) {
+  if (c.touch) {
+    c.touch[i] = 1;
+    ++*c.reads;
+  }
+  return (float)c.tsdf[i] * kDivShortMax;
+}
 // raycasthelper::voxel2tsdf (tsdf_volume.cu:178-191): nearest voxel, valid 1..dim-2
 inline float voxel2tsdf(const RayCtx &c, V3 p) {
   const int x = f2i_rn(p.x * c.vs_inv.x);
@@ -543,7 +552,7 @@ inline float voxel2tsdf(const RayCtx &c, V3 p) {
   const int z = f2i_rn(p.z * c.vs_inv.z);
   if (x >= c.X - 1 || y >= c.Y - 1 || z >= c.Z - 1 || x < 1 || y < 1 || z < 1) return NAN;
   if (z < c.zb || z >= c.zb + c.zn) return NAN;  // slab: not stored
-  return (float)c.tsdf[(int64_t)x + (int64_t)y * c.X + (int64_t)z * c.slice] * kDivShortMax;
+  return tsdf_at(c, (int64_t)x + (int64_t)y * c.X + (int64_t)z * c.slice);
 }
 // interpolate (tsdf_volume.cu:137-161), terms accumulated in listed order
 inline float interp(const RayCtx &c, V3 cf) {
@@ -552,9 +561,7 @@ inline float interp(const RayCtx &c, V3 cf) {
   if (gz < c.zb || gz + 1 >= c.zb + c.zn) return NAN;  // slab: not stored
   const float a = cf.x - (float)gx, b = cf.y - (float)gy, cc = cf.z - (float)gz;
   auto T = [&](int dx, int dy, int dz) {
-    return (float)c.tsdf[(int64_t)(gx + dx) + (int64_t)(gy + dy) * c.X +
-                         (int64_t)(gz + dz) * c.slice] *
-           kDivShortMax;
+    return tsdf_at(c, (int64_t)(gx + dx) + (int64_t)(gy + dy) * c.X + (int64_t)(gz + dz) * c.slice);
   };
   float s = 0.f;
   s += T(0, 0, 0) * (1 - a) * (1 - b) * (1 - cc);
@@ -591,8 +598,11 @@ inline V3 compute_normal(const RayCtx &c, V3 p) {
 static void raycast_impl(const int16_t *tsdf, const int dims[3], const float vs[3],
                          const float range[3], const kfx_intrinsics *in, const kfx_pose *pose,
                          const float Rinv[9], float *vmap, float *nmap, const int32_t *pix,
-                         int64_t npix, int zb, int zn, int own0, int own1, uint32_t *keys) {
+                         int64_t npix, int zb, int zn, int own0, int own1, uint32_t *keys,
+                         uint8_t *touch = nullptr, int64_t *reads = nullptr) {
   RayCtx c;
+  c.touch = touch;
+  c.reads = reads;
   c.tsdf = tsdf;
   c.X = dims[0];
   c.Y = dims[1];
@@ -674,6 +684,24 @@ void kfo_raycast(const int16_t *tsdf, const int dims[3], const float vs[3],
                  int64_t npix) {
   raycast_impl(tsdf, dims, vs, range, in, pose, Rinv, vmap, nmap, pix, npix, 0, dims[2], 0,
                dims[2], nullptr);
+}
+
+// SURVEY.md §8d raycast roofline input: N_uniq = the distinct voxels whose
+// tsdf the reference raycast reads (nearest samples + trilinear corners of the
+// normals), and the total number of those reads.
+void kfo_raycast_touched(const int16_t *tsdf, const int dims[3], const float vs[3],
+                         const float range[3], const kfx_intrinsics *in, const kfx_pose *pose,
+                         const float Rinv[9], int64_t *n_uniq, int64_t *n_reads) {
+  const int64_t n = (int64_t)dims[0] * dims[1] * dims[2];
+  std::vector<uint8_t> touch((size_t)n, 0);
+  std::vector<float> vmap((size_t)in->width * in->height * 3), nmap(vmap.size());
+  int64_t reads = 0;
+  raycast_impl(tsdf, dims, vs, range, in, pose, Rinv, vmap.data(), nmap.data(), nullptr, 0, 0, dims[2], 0,
+               dims[2], nullptr, touch.data(), &reads);
+  int64_t u = 0;
+  for (uint8_t t : touch) u += t;
+  *n_uniq = u;
+  *n_reads = reads;
 }
 
 void kfo_raycast_slab(const int16_t *tsdf, const int dims[3], const float vs[3],

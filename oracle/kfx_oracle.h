@@ -97,6 +97,11 @@ void kfo_raycast(const int16_t *tsdf, const int dims[3], const float voxel_size[
 /* Z-slab restatement of the raycast: tsdf readable only in
  * slices [zb, zb+zn); events only at samples whose nearest voxel z is in
  * [own0, own1); keys[] = loop index of the deciding sample (UINT32_MAX none). */
+/* distinct voxels read by the reference raycast (samples + normal corners) and
+ * the number of reads (SURVEY.md §8d N_uniq) */
+void kfo_raycast_touched(const int16_t *tsdf, const int dims[3], const float vs[3],
+                         const float range[3], const kfx_intrinsics *in, const kfx_pose *pose,
+                         const float Rinv[9], int64_t *n_uniq, int64_t *n_reads);
 void kfo_raycast_slab(const int16_t *tsdf, const int dims[3], const float vs[3],
                       const float range[3], const kfx_intrinsics *in, const kfx_pose *pose,
                       const float Rinv[9], int zb, int zn, int own0, int own1, float *vmap,

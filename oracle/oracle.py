@@ -47,6 +47,8 @@ def lib():
         L.kfo_preprocess.argtypes = [P(f), i, i, i, P(Intrinsics), P(Params), P(P(f)), P(P(f)), P(P(f))]
         L.kfo_icp_accumulate.argtypes = [P(f), P(f), P(f), P(f), i, i, P(Intrinsics), P(Pose), f, f,
                                          P(C.c_int64)]
+        L.kfo_raycast_touched.argtypes = [P(C.c_int16), P(i), P(f), P(f), P(Intrinsics), P(Pose), P(f),
+                                          P(C.c_int64), P(C.c_int64)]
         L.kfo_sincos.argtypes = [C.c_double, P(C.c_double), P(C.c_double)]
         L.kfo_icp_update.argtypes = [P(C.c_int64), P(Pose), P(C.c_double)]
         L.kfo_icp_update.restype = i
@@ -240,6 +242,15 @@ def raycast(vol: Volume, intr: Intrinsics, cam2vol: Pose, Rinv: np.ndarray, pix:
                       fptr(vol.range), C.byref(intr), C.byref(cam2vol), fptr(Rinv), fptr(vmap), fptr(nmap),
                       pp, npix)
     return vmap, nmap
+
+
+def raycast_touched(vol: Volume, intr: Intrinsics, cam2vol: Pose, Rinv: np.ndarray):
+    """(N_uniq, reads) of the reference raycast over `vol`."""
+    Rinv = _f32(Rinv).reshape(9)
+    u, r = C.c_int64(), C.c_int64()
+    lib().kfo_raycast_touched(i16ptr(vol.tsdf), vol.dims.ctypes.data_as(C.POINTER(C.c_int)), fptr(vol.voxel_size),
+                              fptr(vol.range), C.byref(intr), C.byref(cam2vol), fptr(Rinv), C.byref(u), C.byref(r))
+    return u.value, r.value
 
 
 def raycast_slab(tsdf: np.ndarray, vol: Volume, intr: Intrinsics, cam2vol: Pose, Rinv: np.ndarray,

@@ -142,6 +142,7 @@ struct kfx_ctx {
   float stage_ms[5]{};
   int pending = 0;      // frames enqueued since the last host sync
   int known_poses = 1;  // n_poses at the last sync
+  int known_fails = 0;  // DevState::fails at the last status check
 
   // Z-slab sharding: this context owns slab `rank` of `world`
   bool slab = false;
@@ -444,16 +445,25 @@ int run_frame(kfx_ctx *c, FrameInput in, hipGraphExec_t *graph, bool overlap = f
   return KFX_OK;
 }
 
+// Status of the frames completed since the last check: a fired ICP watchdog
+// (cleared here; that frame was dropped) is an error, a tracking failure of
+// any of them is KFX_TRACKING_LOST.
+int check_status(kfx_ctx *c, const DevState &s) {
+  const bool lost = s.fails != c->known_fails;
+  c->known_fails = s.fails;
+  if (s.icp_stalled) {
+    HIPCHK(hipMemsetAsync(c->icp_sync, 0, sizeof(IcpSync), c->stream));
+    const int r = write_field(c, offsetof(DevState, icp_stalled), 0);
+    return r ? r : set_err(KFX_ERR_HIP, "ICP grid barrier watchdog fired (grid not co-resident)");
+  }
+  return lost ? KFX_TRACKING_LOST : KFX_OK;
+}
+
 int finish_frame(kfx_ctx *c) {
   DevState s;
   int r = read_state(c, &s);
   if (r) return r;
-  if (s.icp_stalled) {
-    HIPCHK(hipMemsetAsync(c->icp_sync, 0, sizeof(IcpSync), c->stream));
-    r = write_field(c, offsetof(DevState, icp_stalled), 0);
-    return r ? r : set_err(KFX_ERR_HIP, "ICP grid barrier watchdog fired (grid not co-resident)");
-  }
-  return s.last_fail ? KFX_TRACKING_LOST : KFX_OK;
+  return check_status(c, s);
 }
 
 // Slab `rank` of `world` owns global slices [Z*rank/world, Z*(rank+1)/world)
@@ -540,6 +550,7 @@ int do_reset(kfx_ctx *c) {
   set_par(c, 0);
   c->pending = 0;
   c->known_poses = 1;
+  c->known_fails = 0;
   return KFX_OK;
 }
 
@@ -807,9 +818,10 @@ int kfx_pipeline_staged(kfx_ctx *c, int idx) {
 int kfx_synchronize(kfx_ctx *c) {
   int r = check_ctx(c);
   if (r) return r;
-  HIPCHK(hipStreamSynchronize(c->stream));
   HIPCHK(hipStreamSynchronize(c->pstream));
-  return KFX_OK;
+  DevState s;
+  if ((r = read_state(c, &s))) return r;  // also waits for the frame stream
+  return check_status(c, s);
 }
 
 int kfx_set_frame_overlap(kfx_ctx *c, int enabled) {
@@ -1236,6 +1248,19 @@ int kfx_raycast_stats(kfx_ctx *c, int64_t out[8]) {
   HIPCHK(hipMemcpyAsync(h, c->counters, sizeof(h), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   for (int i = 0; i < 8; ++i) out[i] = i < 6 ? (int64_t)h[i] : 0;
+  if (!c->slab) {  // the reference raycast's N_uniq and reads (single volume)
+    uint32_t *bits = nullptr;
+    HIPCHK(hipMalloc(&bits, (c->vol.local_voxels() + 31) / 32 * 4));
+    launch_raycast_touch(c->stream, c->vol, c->g[0], c->st, c->pose_log, to_dev(c->p.volu_pose), nullptr, bits,
+                         c->counters + 8);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemcpyAsync(h, c->counters + 8, 16, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    (void)hipFree(bits);
+    if (e != hipSuccess) return set_err(KFX_ERR_HIP, std::string("raycast_touch: ") + hipGetErrorString(e));
+    out[6] = (int64_t)h[0];
+    out[7] = (int64_t)h[1];
+  }
   return KFX_OK;
 }
 

@@ -32,6 +32,7 @@ struct DevState {
   long long sums[27];   // last ICP sums (test seam)
   double x[6];          // last ICP increment
   int icp_stalled;      // persistent ICP barrier watchdog fired (reported as KFX_ERR_HIP)
+  int fails;            // frames dropped by a tracking failure (reset) so far
 };
 
 struct LevelGeom {
@@ -155,6 +156,10 @@ void launch_integrate(hipStream_t s, VolView v, LevelGeom g0, const float2 *dl0,
 void launch_raycast(hipStream_t s, VolView v, int levels, const LevelGeom *g, FrameView cur,
                     FrameView prev, const DevState *st, const DevPose *log, DevPose vpose,
                     const float *xpose, uint32_t *keys, unsigned long long *stats = nullptr);
+// the reference raycast's distinct voxels read (out[0]) and reads (out[1]),
+// count-only (bits: one bit per stored voxel, workspace)
+void launch_raycast_touch(hipStream_t s, VolView v, LevelGeom g0, const DevState *st, const DevPose *log,
+                          DevPose vpose, const float *xpose, uint32_t *bits, unsigned long long *out);
 // resizePointsNormals of levels >= 1 from the level-0 model maps
 void launch_resize(hipStream_t s, int levels, const LevelGeom *g, FrameView cur, FrameView prev,
                    const DevState *st, const float *xpose);

@@ -1009,6 +1009,7 @@ __device__ void frame_bookkeeping(DevState *st, DevPose *log, int kind, const De
     st->n_poses = 1;
     log[0] = pose_identity();
     st->last_fail = 1;
+    st->fails += 1;
     return;
   }
   if (kind == 1) {
@@ -1997,6 +1998,109 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KFX_RAY_OCC
   resize_tile(ra, kind, tx0, ty0, lx, ly, vout, nout, cur, prev);
 }
 
+// SURVEY.md §8d raycast roofline input (count-only, off the frame path): the
+// reference raycast (tsdf_volume.cu:210-260) marched naively, one thread per
+// pixel, marking in `bits` (one bit per stored voxel) every voxel whose tsdf it
+// reads (nearest samples and the trilinear corners of hit normals) and adding
+// the reads to reads[0].  N_uniq = popcount(bits) (k_popcount).
+__device__ __forceinline__ float touch_read(const VolView &v, uint32_t *bits, unsigned &nr, size_t i) {
+  const uint32_t m = 1u << (i & 31);
+  if (!(bits[i >> 5] & m)) atomicOr(&bits[i >> 5], m);
+  ++nr;
+  return (float)v.tsdf[i] * kDivShortMax;
+}
+__device__ float touch_interp(const VolView &v, uint32_t *bits, unsigned &nr, f3 cf) {
+  const int gx = f2i_rd(cf.x), gy = f2i_rd(cf.y), gz = f2i_rd(cf.z);
+  if (gx < 0 || gx >= v.X - 1 || gy < 0 || gy >= v.Y - 1 || gz < 0 || gz >= v.Z - 1) return NAN;
+  const float a = cf.x - (float)gx, b = cf.y - (float)gy, c = cf.z - (float)gz;
+  float s = 0.f;
+  s += touch_read(v, bits, nr, vox_index(v, gx, gy, gz)) * (1 - a) * (1 - b) * (1 - c);
+  s += touch_read(v, bits, nr, vox_index(v, gx, gy, gz + 1)) * (1 - a) * (1 - b) * c;
+  s += touch_read(v, bits, nr, vox_index(v, gx, gy + 1, gz)) * (1 - a) * b * (1 - c);
+  s += touch_read(v, bits, nr, vox_index(v, gx, gy + 1, gz + 1)) * (1 - a) * b * c;
+  s += touch_read(v, bits, nr, vox_index(v, gx + 1, gy, gz)) * a * (1 - b) * (1 - c);
+  s += touch_read(v, bits, nr, vox_index(v, gx + 1, gy, gz + 1)) * a * (1 - b) * c;
+  s += touch_read(v, bits, nr, vox_index(v, gx + 1, gy + 1, gz)) * a * b * (1 - c);
+  s += touch_read(v, bits, nr, vox_index(v, gx + 1, gy + 1, gz + 1)) * a * b * c;
+  return s;
+}
+__global__ __launch_bounds__(256) void k_raycast_touch(VolView v, LevelGeom g, RayConsts rc,
+                                                       const DevState *__restrict__ st,
+                                                       const DevPose *__restrict__ log, DevPose vpose,
+                                                       const float *xpose, uint32_t *bits,
+                                                       unsigned long long *reads) {
+  __shared__ DevPose s_c2v;
+  __shared__ int s_kind;
+  if (threadIdx.x == 0) {
+    if (xpose) {
+      s_kind = 1;
+      for (int i = 0; i < 9; ++i) s_c2v.R[i] = xpose[i];
+      for (int i = 0; i < 3; ++i) s_c2v.t[i] = xpose[9 + i];
+    } else {
+      s_kind = frame_kind(st);
+      if (s_kind == 1) s_c2v = pose_mul(pose_inv(vpose), frame_pose(st, log, 1));
+    }
+  }
+  __syncthreads();
+  unsigned nr = 0;
+  const int pi = blockIdx.x * 256 + threadIdx.x;
+  if (s_kind == 1 && pi < g.w * g.h) {
+    const int x = pi % g.w, y = pi / g.w;
+    const DevPose P = s_c2v;
+    const f3 org = {P.t[0], P.t[1], P.t[2]};
+    const f3 pp = {(1.f * ((float)x - g.cx)) / g.fx, (1.f * ((float)y - g.cy)) / g.fy, 1.f};
+    const f3 dir = normalized(rmul(P.R, pp));
+    const f3 invR = {1.f / dir.x, 1.f / dir.y, 1.f / dir.z};
+    const f3 tbot = mulc(invR, sub({0.f, 0.f, 0.f}, org));
+    const f3 ttop = mulc(invR, sub({v.range[0], v.range[1], v.range[2]}, org));
+    const f3 tmin = {fminf(ttop.x, tbot.x), fminf(ttop.y, tbot.y), fminf(ttop.z, tbot.z)};
+    const f3 tmax = {fmaxf(ttop.x, tbot.x), fmaxf(ttop.y, tbot.y), fmaxf(ttop.z, tbot.z)};
+    const float tnear = fmaxf(fmaxf(tmin.x, tmin.y), fmaxf(tmin.x, tmin.z));
+    const float tfar = fminf(fminf(tmax.x, tmax.y), fminf(tmax.x, tmax.z));
+    float ray_len = fmaxf(tnear, 0.f);
+    if (ray_len < tfar) {
+      const f3 vstep = mulc(dir, rc.vs);
+      ray_len += rc.step;
+      f3 nextp = add(org, scl(dir, ray_len));
+      auto sample = [&](f3 p) -> float {
+        const int ix = f2i_rn(p.x * rc.vs_inv.x), iy = f2i_rn(p.y * rc.vs_inv.y), iz = f2i_rn(p.z * rc.vs_inv.z);
+        if (ix >= v.X - 1 || iy >= v.Y - 1 || iz >= v.Z - 1 || ix < 1 || iy < 1 || iz < 1) return NAN;
+        return touch_read(v, bits, nr, vox_index(v, ix, iy, iz));
+      };
+      float tn = sample(nextp);
+      for (; ray_len < tfar; ray_len += rc.step) {
+        nextp = add(nextp, vstep);
+        const float tc = tn;
+        tn = sample(nextp);
+        if (isnan(tn)) continue;
+        if (tc < 0.f && tn > 0.f) break;
+        if (tc > 0.f && tn < 0.f) {
+          const float Ts = ray_len - (v.vs[0] * tc) / (tc - tn);
+          const f3 p = add(org, scl(dir, Ts));
+          f3 n;
+          n.x = (touch_interp(v, bits, nr, mulc({p.x + rc.gd.x, p.y, p.z}, rc.vs_inv)) -
+                 touch_interp(v, bits, nr, mulc({p.x - rc.gd.x, p.y, p.z}, rc.vs_inv))) / rc.gd.x;
+          n.y = (touch_interp(v, bits, nr, mulc({p.x, p.y + rc.gd.y, p.z}, rc.vs_inv)) -
+                 touch_interp(v, bits, nr, mulc({p.x, p.y - rc.gd.y, p.z}, rc.vs_inv))) / rc.gd.y;
+          n.z = (touch_interp(v, bits, nr, mulc({p.x, p.y, p.z + rc.gd.z}, rc.vs_inv)) -
+                 touch_interp(v, bits, nr, mulc({p.x, p.y, p.z - rc.gd.z}, rc.vs_inv))) / rc.gd.z;
+          n = normalized(n);
+          if (!isnan(n.x * n.y * n.z)) break;
+        }
+      }
+    }
+  }
+  unsigned long long t = nr;
+  for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off);
+  if ((threadIdx.x & 63) == 0 && t) atomicAdd(reads, t);
+}
+__global__ __launch_bounds__(256) void k_popcount(const uint32_t *bits, size_t n, unsigned long long *out) {
+  unsigned long long c = 0;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) c += __popc(bits[i]);
+  for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(out, c);
+}
+
 // kernel_resizePointsNormals (image_process.cu:95-125) for levels >= 1: the
 // block's 16x16 level-0 tile (this thread's values vout/nout at (lx, ly)) maps
 // onto 8x8 / 4x4 / 2x2 tiles of levels 1 / 2 / 3, computed from the level
@@ -2707,6 +2811,22 @@ void launch_raycast(hipStream_t s, VolView v, int levels, const LevelGeom *g, Fr
     hipLaunchKernelGGL((k_raycast<false, false>), grd, dim3(256), 0, s, v, ra, rc, cur, prev, st,
                        log, vpose, xpose, keys);
   }
+}
+
+void launch_raycast_touch(hipStream_t s, VolView v, LevelGeom g0, const DevState *st, const DevPose *log,
+                          DevPose vpose, const float *xpose, uint32_t *bits, unsigned long long *out) {
+  RayConsts rc;
+  rc.vs = {v.vs[0], v.vs[1], v.vs[2]};
+  rc.vs_inv = {1.f / v.vs[0], 1.f / v.vs[1], 1.f / v.vs[2]};
+  rc.gd = {v.vs[0] * 0.5f, v.vs[1] * 0.5f, v.vs[2] * 0.5f};
+  rc.step = v.vs[0];
+  rc.skip_cap = 0.f;
+  const size_t words = (v.local_voxels() + 31) / 32;
+  (void)hipMemsetAsync(bits, 0, words * 4, s);
+  (void)hipMemsetAsync(out, 0, 16, s);
+  hipLaunchKernelGGL(k_raycast_touch, dim3((g0.w * g0.h + 255) / 256), dim3(256), 0, s, v, g0, rc, st, log, vpose,
+                     xpose, bits, out + 1);
+  hipLaunchKernelGGL(k_popcount, dim3(2048), dim3(256), 0, s, bits, words, out);
 }
 
 void launch_resize(hipStream_t s, int levels, const LevelGeom *g, FrameView cur, FrameView prev,

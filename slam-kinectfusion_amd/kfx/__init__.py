@@ -315,8 +315,10 @@ class KinectFusion:
     def pipeline_staged(self, idx: int):
         _check(lib().kfx_pipeline_staged(self._h, int(idx)), "kfx_pipeline_staged")
 
-    def synchronize(self):
-        _check(lib().kfx_synchronize(self._h), "kfx_synchronize")
+    def synchronize(self) -> int:
+        """Wait for queued frames; KFX_OK, or KFX_TRACKING_LOST if one of the
+        frames completed since the last status check was dropped (reset)."""
+        return _check(lib().kfx_synchronize(self._h), "kfx_synchronize", ok=(KFX_OK, KFX_TRACKING_LOST))
 
     def set_graph_mode(self, on: bool):
         _check(lib().kfx_set_graph_mode(self._h, int(on)), "kfx_set_graph_mode")
@@ -373,7 +375,7 @@ class KinectFusion:
         a = (C.c_int64 * 8)()
         _check(lib().kfx_raycast_stats(self._h, a), "kfx_raycast_stats")
         return dict(zip(["rays", "skip_lookups", "skipped_samples", "blocked_lookups", "batches",
-                         "normal_candidates"], a[:6]))
+                         "normal_candidates", "ref_uniq_voxels", "ref_reads"], a[:8]))
 
     def volume_checksum(self) -> tuple:
         """(hash sum mod 2^64, voxels with weight > 0) over the owned slices."""

@@ -304,6 +304,31 @@ def test_tracking_failure_resets_like_reference(seq_qvga):
     kf.close()
 
 
+def test_staged_tracking_failure_reported_by_synchronize(seq_qvga):
+    """Staged (device-input, overlapped) frames return without a host sync; the
+    drop of a frame by a tracking failure is reported by kfx_synchronize
+    (ADVICE r1), once, and the state equals the host-frame path's."""
+    bgr, dep, gt = seq_qvga
+    intr = synth.Intrinsics.qvga()
+    frames = dep[:4].astype(np.float32).copy()
+    frames[2] = 0.0  # no depth: ICP det check fails -> reset(), frame dropped
+    kf, p = make(intr, dims=64)
+    kf.stage_frames(bgr[:4], frames)
+    assert kf.synchronize() == KFX_OK
+    for k in range(4):
+        kf.pipeline_staged(k)
+    assert kf.synchronize() == KFX_TRACKING_LOST
+    assert kf.synchronize() == KFX_OK  # reported once
+    assert kf.frame_count == 2 and kf.pose_record.shape == (1, 4, 4)
+    ref, _ = make(intr, dims=64)
+    st = [ref.pipeline(bgr[k], frames[k]) for k in range(4)]
+    assert st == [KFX_OK, KFX_OK, KFX_TRACKING_LOST, KFX_OK]
+    for a, b in zip(kf.volume_soa(), ref.volume_soa()):
+        assert np.array_equal(a, b)
+    kf.close()
+    ref.close()
+
+
 def test_tsdf_record_export_roundtrip(seq_qvga):
     bgr, dep, gt = seq_qvga
     intr = synth.Intrinsics.qvga()

@@ -245,3 +245,30 @@ def test_c4_1024_eight_slabs_match_single_volume():
     for m in members:
         m.close()
     single.close()
+
+
+def test_raycast_uniq_count_matches_oracle():
+    """SURVEY.md §8d raycast roofline input: N_uniq (distinct voxels the
+    reference raycast reads: nearest samples + normal corners) and the read
+    count from the device's count-only pass equal the oracle's, and the
+    empty-space skipping raycast touches a small fraction of them."""
+    intr = synth.Intrinsics.qvga()
+    I = Intrinsics.from_any(intr)
+    bgr, dep, gt = synth.sequence(6, intr, noise=True, dropout=0.005)
+    p = default_params(dims=128, range_m=L_VOL)
+    kf = KinectFusion(I, p)
+    pipe = O.Pipeline(I, p)
+    for k in range(6):
+        d = dep[k].astype(np.float32)
+        assert kf.pipeline(bgr[k], d) == KFX_OK
+        assert pipe.process(bgr[k], d) == 0
+    st = kf.raycast_stats()
+    vol = O.Volume((128,) * 3, (L_VOL,) * 3)
+    vol.tsdf[:] = pipe.volume()[0]
+    cam2vol = O.pose_mul(O.pose_inv(p.volu_pose), Pose.from_matrix(pipe.poses()[-1]))
+    Rinv = cam2vol.matrix()[:3, :3].T.copy()
+    nu, nr = O.raycast_touched(vol, I, cam2vol, Rinv)
+    assert (st["ref_uniq_voxels"], st["ref_reads"]) == (nu, nr)
+    assert nu > 10000 and nr > nu
+    assert st["rays"] > 0.5 * intr.width * intr.height
+    kf.close()

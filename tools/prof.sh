@@ -10,7 +10,7 @@ set -o pipefail
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 cd /tmp && export TMPDIR=/tmp
 ARGS="$*"   # the stats pass runs bench.py with these (default: its defaults)
-PMC_ARGS="--cpu-frames 0"  # the bench defaults: same frames as the stats pass
+PMC_ARGS="$ARGS --cpu-frames 0 --c1-frames 0"  # same frames and step counts as the stats pass
 OUT="$ROOT/gpurun_out/prof"
 mkdir -p "$OUT"
 run() {  # name, timeout, rocprof args...
@@ -24,11 +24,13 @@ run() {  # name, timeout, rocprof args...
 }
 run stats 300 --kernel-trace --stats --output-format csv -d "$OUT/stats" -o run -- python3 "$ROOT/bench.py" $ARGS
 grep "^{\"metric\"" "$OUT/stats.log" | tail -1 > "$OUT/stats_bench.json"
-python3 "$ROOT/tools/prof_summary.py" "$OUT/stats/run_kernel_trace.csv" 20 300 "$OUT/kernel_summary.json" > /dev/null
+W=$(python3 -c "import sys;a=sys.argv[1:];print(a[a.index('--warmup')+1] if '--warmup' in a else 20)" $ARGS)
+S=$(python3 -c "import sys;a=sys.argv[1:];print(a[a.index('--steps')+1] if '--steps' in a else 300)" $ARGS)
+python3 "$ROOT/tools/prof_summary.py" "$OUT/stats/run_kernel_trace.csv" $W $S "$OUT/kernel_summary.json" > /dev/null
 if [ -x "$ROOT/tools/build/pmc_calib" ]; then
   run calib_fetch 90 --pmc FETCH_SIZE --output-format csv -d "$OUT/calib/FETCH_SIZE" -- "$ROOT/tools/build/pmc_calib"
   run calib_write 90 --pmc WRITE_SIZE --output-format csv -d "$OUT/calib/WRITE_SIZE" -- "$ROOT/tools/build/pmc_calib"
 fi
 run pmc_fetch 240 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc/FETCH_SIZE" -- python3 "$ROOT/bench.py" $PMC_ARGS
 run pmc_write 240 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc/WRITE_SIZE" -- python3 "$ROOT/bench.py" $PMC_ARGS
-python3 "$ROOT/tools/traffic.py" "$OUT"
+PROF_ARGS="$ARGS" python3 "$ROOT/tools/traffic.py" "$OUT" --commit

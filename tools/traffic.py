@@ -69,17 +69,34 @@ def main():
     for k, r in out["kernels"].items():
         if k.startswith("k_"):
             print(f"{k:40s} n={r['dispatches']:5d} hbm/launch={r.get('hbm_bytes_per_launch', float('nan')) / 1e6:10.2f} MB")
-    if commit:
+    if commit:  # profiles/r02_integrate_pmc.json: what bench.py attaches as roofline.traffic
         integ = [r for k, r in out["kernels"].items()
                  if k.startswith("k_integrate<false") and "hbm_bytes_per_launch" in r]
         if integ:
+            import shlex
+            args = shlex.split(os.environ.get("PROF_ARGS", ""))
+
+            def arg(name, default):
+                return int(args[args.index(name) + 1]) if name in args else default
+            steps, warmup, dims = arg("--steps", 300), arg("--warmup", 20), arg("--dims", 512)
             r = max(integ, key=lambda r: r["dispatches"])
+            ray = [rr for k, rr in out["kernels"].items() if k.startswith("k_raycast<true, false, false>")]
             prof = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles")
             json.dump({"kernel": "k_integrate", "hbm_bytes_per_launch": int(r["hbm_bytes_per_launch"]),
                        "read_bytes": int(r["read_bytes"]), "write_bytes": int(r["write_bytes"]),
                        "dispatches": r["dispatches"], "factor_units_per_byte": fac,
+                       "raycast_hbm_bytes_per_launch": int(ray[0]["hbm_bytes_per_launch"]) if ray and
+                       "hbm_bytes_per_launch" in ray[0] else None,
+                       "workload": [dims, 640, 480], "steps": steps, "warmup": warmup,
+                       "command": "python3 bench.py " + " ".join(args),
+                       "regime": ("mean over every dispatch of the run: %d warm-up + %d timed + 20 profiled "
+                                  "frames%s" % (warmup, steps, " (unsaturated transient: < 64 frames)"
+                                                if warmup + steps + 20 < 64 else "")),
                        "source": "tools/prof.sh FETCH_SIZE/WRITE_SIZE passes, 2-byte stream calibration"},
-                      open(os.path.join(prof, "integrate_pmc.json"), "w"), indent=1)
+                      open(os.path.join(prof, "r02_integrate_pmc.json"), "w"), indent=1)
+            # a copy beside the counters (profiles/ does not come back from the GPU box)
+            json.dump(json.load(open(os.path.join(prof, "r02_integrate_pmc.json"))),
+                      open(os.path.join(root, "r02_integrate_pmc.json"), "w"), indent=1)
 
 
 if __name__ == "__main__":
