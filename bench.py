@@ -56,6 +56,8 @@ def parse():
     ap.add_argument("--unique", type=int, default=48, help="distinct frames rendered (played ping-pong)")
     ap.add_argument("--profile-frames", type=int, default=20)
     ap.add_argument("--cpu-frames", type=int, default=8, help="oracle frames timed for cpu_baseline (0 = skip)")
+    ap.add_argument("--host-frames", type=int, default=200,
+                    help="frames fed from host memory through kfx_pipeline_async for host_input (0 = skip)")
     ap.add_argument("--c1-frames", type=int, default=100,
                     help="oracle frames of the C1 record (128^3, same frames; 0 = skip)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r02_integrate_pmc.json"),
@@ -275,6 +277,28 @@ def main():
     if tracked != a.steps:  # a dropped frame (tracking reset) invalidates the measurement
         raise SystemExit(f"bench: {a.steps - tracked} of {a.steps} timed frames were not tracked")
 
+    # host-input throughput (not `value`): the same frames from host memory
+    # through kfx_pipeline_async (pinned ring, H2D overlapped with the previous
+    # frame), PCIe included, f32 depth as the reference's pipeline() takes it
+    host_in = None
+    if a.host_frames > 0:
+        hb = [np.ascontiguousarray(bgr[i]) for i in range(a.unique)]
+        hd = [np.ascontiguousarray(dep[i].astype(np.float32)) for i in range(a.unique)]
+        ho = synth.ping_pong(a.unique, a.host_frames)
+        kf.synchronize()
+        D.barrier()
+        t0 = time.perf_counter()
+        for i in ho:
+            kf.pipeline_async(hb[i], hd[i])
+        st_h = kf.synchronize()
+        dt_h = D.max(time.perf_counter() - t0)
+        host_in = {"value": round(len(ho) * (world if not slab_main else 1) / dt_h, 3), "unit": "frames/s",
+                   "ms_per_step": round(1000.0 * dt_h / len(ho), 4), "frames": len(ho),
+                   "status": "ok" if st_h == kfx.KFX_OK else "tracking lost",
+                   "bytes_per_frame_h2d": W * H * 7,
+                   "path": "kfx_pipeline_async: host frame -> pinned 4-slot ring -> H2D on a copy stream "
+                           "overlapped with the previous frame; f32 depth mm + BGR8"}
+
     # per-stage device ms + integrate roofline on further frames (profiled, eager)
     kf.set_profiling(True)
     stages = {k: [] for k in ("preprocess", "icp", "integrate", "raycast", "total")}
@@ -371,6 +395,7 @@ def main():
             "launch_ms_source": ms_source,
         },
         "roofline_raycast": raycast_roofline(ray_work, ray_ms, W, H, ms_source),
+        "host_input": host_in,
         "cpu_baseline": cpu,
         "c1_record": c1,
     }

@@ -111,6 +111,14 @@ int kfx_stage_frames(kfx_ctx *ctx, int n_frames, const uint8_t *bgr,
                      const float *depth_mm);
 int kfx_pipeline_staged(kfx_ctx *ctx, int frame_index);
 int kfx_synchronize(kfx_ctx *ctx);
+/* Pipelined host input (kinectfusion::pipeline, kinectfusion.cpp:48-52, without
+ * the per-frame host sync): the frame is copied into a pinned 4-slot ring and
+ * uploaded on a copy stream while earlier frames run, then queued like a
+ * staged frame; the call returns without waiting for the GPU (it blocks only
+ * when the ring slot's previous upload is still in flight).  The caller's
+ * buffers are free on return.  Tracking status: kfx_synchronize. */
+int kfx_pipeline_async(kfx_ctx *ctx, const uint8_t *bgr, const float *depth_mm);
+int kfx_pipeline_async_u16(kfx_ctx *ctx, const uint8_t *bgr, const uint16_t *depth_mm);
 /* Use a captured hipGraph for the per-frame launch sequence (default on). */
 int kfx_set_graph_mode(kfx_ctx *ctx, int enabled);
 /* Overlap each staged frame's preprocess with the previous frame's tracking on

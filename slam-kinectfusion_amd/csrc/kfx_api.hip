@@ -151,6 +151,15 @@ struct kfx_ctx {
   uint8_t *mc_tab = nullptr;      // marching-cubes table (uploaded on first use)
   uint32_t *key_local = nullptr;  // per-pixel sample index of this slab's decisive event
   uint32_t *key_min = nullptr;    // all-reduce MIN of key_local over the slabs
+  // kfx_pipeline_async: host frames copied into a pinned ring slot, uploaded on
+  // the copy stream while earlier frames run (slot reuse ordered by events)
+  static constexpr int kRing = 4;
+  uint8_t *ring_host = nullptr, *ring_dev = nullptr;
+  size_t ring_slot = 0;  // bytes per slot: f32 depth + BGR8
+  hipEvent_t ring_h2d[kRing]{}, ring_done[kRing]{};
+  bool ring_used[kRing]{};
+  int ring_next = 0;
+  hipStream_t cstream = nullptr;
   ncclComm_t comm = nullptr;      // RCCL communicator over the slab ranks (one process per GPU)
 };
 
@@ -199,11 +208,15 @@ void destroy_graphs(kfx_ctx *c) {
     }
 }
 
-// Frame input: depth (f32 mm, or u16 mm) and BGR8 colour, in device memory.
+// Frame input: depth (f32 mm, or u16 mm) and BGR8 colour, in device memory;
+// ready (optional): the input is in place once this event completes (async
+// host input); done (optional): recorded after the frame's last kernel.
 struct FrameInput {
   const float *d32;
   const uint16_t *d16;
   const uint8_t *bgr;
+  hipEvent_t ready = nullptr;
+  hipEvent_t done = nullptr;
 };
 
 // The per-frame launch sequence (kinectfusion.cpp:78-127 with the frame-1 and
@@ -306,6 +319,7 @@ int enqueue_frame_overlap(kfx_ctx *c, FrameInput in, hipEvent_t *ev) {
   set_par(c, p);
   hipStream_t b = c->pstream;
   HIPCHK(hipStreamWaitEvent(b, c->ev_free[p], 0));  // the frame before last is done with set p
+  if (in.ready) HIPCHK(hipStreamWaitEvent(b, in.ready, 0));  // host input uploaded
 #if KFX_PREP_AFTER_ICP
   // start behind the previous frame's ICP: the latency-bound persistent ICP
   // then runs alone and the preprocess shares the GPU with integrate/raycast
@@ -333,6 +347,7 @@ int enqueue_frame_overlap(kfx_ctx *c, FrameInput in, hipEvent_t *ev) {
   if (c->slab) r = enqueue_combine(c);
   if (ev) HIPCHK(hipEventRecord(ev[4], c->stream));
   HIPCHK(hipEventRecord(c->ev_free[p], c->stream));
+  if (in.done) HIPCHK(hipEventRecord(in.done, c->stream));
   return r;
 }
 
@@ -424,6 +439,7 @@ int run_frame(kfx_ctx *c, FrameInput in, hipGraphExec_t *graph, bool overlap = f
     return KFX_OK;
   }
   set_par(c, 0);  // single-stream frames (and their graphs) use set 0
+  if (in.ready) HIPCHK(hipStreamWaitEvent(c->stream, in.ready, 0));
   if (c->profiling) {
     if ((r = enqueue_frame(c, in, c->ev))) return r;
     HIPCHK(hipGetLastError());
@@ -441,6 +457,7 @@ int run_frame(kfx_ctx *c, FrameInput in, hipGraphExec_t *graph, bool overlap = f
       HIPCHK(hipGetLastError());
     }
   }
+  if (in.done) HIPCHK(hipEventRecord(in.done, c->stream));
   c->pending += 1;
   return KFX_OK;
 }
@@ -730,7 +747,13 @@ int kfx_destroy(kfx_ctx *c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->pstream) (void)hipStreamSynchronize(c->pstream);
+  if (c->cstream) (void)hipStreamSynchronize(c->cstream);
   destroy_graphs(c);
+  if (c->ring_host) (void)hipHostFree(c->ring_host);
+  for (int k = 0; k < kfx_ctx::kRing; ++k)
+    for (hipEvent_t e : {c->ring_h2d[k], c->ring_done[k]})
+      if (e) (void)hipEventDestroy(e);
+  if (c->cstream) (void)hipStreamDestroy(c->cstream);
   if (c->comm) (void)ncclCommDestroy(c->comm);
   for (void *a : c->allocs) (void)hipFree(a);
   for (auto &e : c->ev)
@@ -747,6 +770,8 @@ int kfx_destroy(kfx_ctx *c) {
 int kfx_reset(kfx_ctx *c) {
   int r = check_ctx(c);
   if (r) return r;
+  if (c->cstream) HIPCHK(hipStreamSynchronize(c->cstream));
+  HIPCHK(hipStreamSynchronize(c->pstream));
   HIPCHK(hipStreamSynchronize(c->stream));
   return do_reset(c);
 }
@@ -771,6 +796,48 @@ int kfx_pipeline_u16(kfx_ctx *c, const uint8_t *bgr, const uint16_t *depth_mm) {
   HIPCHK(hipMemcpyAsync(c->bgr, bgr, np * 3, hipMemcpyHostToDevice, c->stream));
   if ((r = run_frame(c, {c->raw[0], c->raw0_u16, c->bgr}, &c->graph[1]))) return r;
   return finish_frame(c);
+}
+
+static int pipeline_async(kfx_ctx *c, const uint8_t *bgr, const void *depth, bool u16) {
+  int r = check_ctx(c);
+  if (r) return r;
+  if (!bgr || !depth) return set_err(KFX_ERR_ARG, "null image");
+  const size_t np = (size_t)c->intr.width * c->intr.height;
+  if (!c->ring_host) {  // first use: pinned + device rings, copy stream, events
+    c->ring_slot = (np * 4 + np * 3 + 255) & ~(size_t)255;
+    HIPCHK(hipHostMalloc((void **)&c->ring_host, c->ring_slot * kfx_ctx::kRing, hipHostMallocDefault));
+    if ((r = dalloc(c, (void **)&c->ring_dev, c->ring_slot * kfx_ctx::kRing))) return r;
+    HIPCHK(hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
+    for (int k = 0; k < kfx_ctx::kRing; ++k) {
+      HIPCHK(hipEventCreateWithFlags(&c->ring_h2d[k], hipEventDisableTiming));
+      HIPCHK(hipEventCreateWithFlags(&c->ring_done[k], hipEventDisableTiming));
+    }
+  }
+  const int k = c->ring_next;
+  c->ring_next = (k + 1) % kfx_ctx::kRing;
+  uint8_t *hs = c->ring_host + c->ring_slot * k, *ds = c->ring_dev + c->ring_slot * k;
+  if (c->ring_used[k]) HIPCHK(hipEventSynchronize(c->ring_h2d[k]));  // the slot's last upload is done
+  const size_t dbytes = np * (u16 ? 2 : 4);
+  std::memcpy(hs, depth, dbytes);
+  std::memcpy(hs + np * 4, bgr, np * 3);
+  // the device slot is free once the frame that read it has finished
+  if (c->ring_used[k]) HIPCHK(hipStreamWaitEvent(c->cstream, c->ring_done[k], 0));
+  HIPCHK(hipMemcpyAsync(ds, hs, dbytes, hipMemcpyHostToDevice, c->cstream));
+  HIPCHK(hipMemcpyAsync(ds + np * 4, hs + np * 4, np * 3, hipMemcpyHostToDevice, c->cstream));
+  HIPCHK(hipEventRecord(c->ring_h2d[k], c->cstream));
+  c->ring_used[k] = true;
+  FrameInput in{u16 ? c->raw[0] : (const float *)ds, u16 ? (const uint16_t *)ds : nullptr, ds + np * 4};
+  in.ready = c->ring_h2d[k];
+  in.done = c->ring_done[k];
+  return run_frame(c, in, nullptr, true);
+}
+
+int kfx_pipeline_async(kfx_ctx *c, const uint8_t *bgr, const float *depth_mm) {
+  return pipeline_async(c, bgr, depth_mm, false);
+}
+
+int kfx_pipeline_async_u16(kfx_ctx *c, const uint8_t *bgr, const uint16_t *depth_mm) {
+  return pipeline_async(c, bgr, depth_mm, true);
 }
 
 int kfx_stage_frames(kfx_ctx *c, int n, const uint8_t *bgr, const float *depth_mm) {
@@ -819,6 +886,7 @@ int kfx_synchronize(kfx_ctx *c) {
   int r = check_ctx(c);
   if (r) return r;
   HIPCHK(hipStreamSynchronize(c->pstream));
+  if (c->cstream) HIPCHK(hipStreamSynchronize(c->cstream));
   DevState s;
   if ((r = read_state(c, &s))) return r;  // also waits for the frame stream
   return check_status(c, s);

@@ -33,7 +33,7 @@ EXPORTS = [
     "kfx_write_poses_txt", "kfx_get_frame_maps", "kfx_set_frame_maps", "kfx_download_tsdf",
     "kfx_upload_tsdf", "kfx_download_volume_soa", "kfx_stage_preprocess", "kfx_stage_icp_accumulate",
     "kfx_stage_icp", "kfx_stage_integrate", "kfx_stage_raycast", "kfx_set_profiling", "kfx_get_stage_ms",
-    "kfx_integrate_counts", "kfx_integrate_stats", "kfx_raycast_stats", "kfx_download_columns", "kfx_create_slab", "kfx_slab_info", "kfx_comm_get_unique_id", "kfx_comm_init",
+    "kfx_integrate_counts", "kfx_integrate_stats", "kfx_raycast_stats", "kfx_download_columns", "kfx_pipeline_async", "kfx_pipeline_async_u16", "kfx_create_slab", "kfx_slab_info", "kfx_comm_get_unique_id", "kfx_comm_init",
     "kfx_pipeline_group", "kfx_render", "kfx_volume_checksum", "kfx_extract_points", "kfx_write_ply", "kfx_save_pointcloud",
     "kfx_extract_mesh", "kfx_write_ply_mesh",
     "kfx_dataset_open", "kfx_dataset_info", "kfx_dataset_read", "kfx_dataset_close", "kfx_png_info",
@@ -100,6 +100,8 @@ def lib():
         "kfx_integrate_counts": ([vp, P(C.c_int64), P(C.c_int64)], i),
         "kfx_integrate_stats": ([vp, P(C.c_int64)], i),
         "kfx_raycast_stats": ([vp, P(C.c_int64)], i),
+        "kfx_pipeline_async": ([vp, P(C.c_uint8), P(f)], i),
+        "kfx_pipeline_async_u16": ([vp, P(C.c_uint8), P(C.c_uint16)], i),
         "kfx_download_columns": ([vp, P(C.c_int32), i, P(C.c_int16), P(C.c_int16), P(C.c_uint32)], i),
         "kfx_create_slab": ([P(Intrinsics), P(Params), i, i, i, P(vp)], i),
         "kfx_slab_info": ([vp, P(i), P(i), P(i), P(i)], i),
@@ -314,6 +316,18 @@ class KinectFusion:
 
     def pipeline_staged(self, idx: int):
         _check(lib().kfx_pipeline_staged(self._h, int(idx)), "kfx_pipeline_staged")
+
+    def pipeline_async(self, color, depth_mm):
+        """Queue a host frame (f32 or u16 depth, mm) without waiting for the GPU
+        (kfx_pipeline_async); tracking status comes with synchronize()."""
+        color = np.ascontiguousarray(color, np.uint8)
+        if np.asarray(depth_mm).dtype == np.uint16:
+            d = np.ascontiguousarray(depth_mm, np.uint16)
+            _check(lib().kfx_pipeline_async_u16(self._h, u8ptr(color), d.ctypes.data_as(C.POINTER(C.c_uint16))),
+                   "kfx_pipeline_async_u16")
+        else:
+            d = np.ascontiguousarray(depth_mm, np.float32)
+            _check(lib().kfx_pipeline_async(self._h, u8ptr(color), fptr(d)), "kfx_pipeline_async")
 
     def synchronize(self) -> int:
         """Wait for queued frames; KFX_OK, or KFX_TRACKING_LOST if one of the

@@ -329,6 +329,32 @@ def test_staged_tracking_failure_reported_by_synchronize(seq_qvga):
     ref.close()
 
 
+@pytest.mark.parametrize("u16", [False, True])
+def test_async_host_input_matches_staged(u16, seq_qvga):
+    """kfx_pipeline_async (pinned ring + H2D on a copy stream, no per-frame host
+    sync; more frames than ring slots, a dropped frame among them) gives the
+    staged path's poses and volume bit for bit, and reports the drop once."""
+    bgr, dep, gt = seq_qvga
+    intr = synth.Intrinsics.qvga()
+    frames = dep.astype(np.uint16 if u16 else np.float32).copy()
+    frames[6] = 0  # tracking failure: reset(), frame dropped
+    kf, p = make(intr, dims=64)
+    for k in range(len(frames)):
+        kf.pipeline_async(bgr[k], frames[k])
+    assert kf.synchronize() == KFX_TRACKING_LOST
+    assert kf.synchronize() == KFX_OK
+    ref, _ = make(intr, dims=64)
+    ref.stage_frames(bgr, frames.astype(np.float32))
+    for k in range(len(frames)):
+        ref.pipeline_staged(k)
+    assert ref.synchronize() == KFX_TRACKING_LOST
+    assert np.array_equal(kf.pose_record, ref.pose_record) and kf.frame_count == ref.frame_count
+    for a, b in zip(kf.volume_soa(), ref.volume_soa()):
+        assert np.array_equal(a, b)
+    kf.close()
+    ref.close()
+
+
 def test_tsdf_record_export_roundtrip(seq_qvga):
     bgr, dep, gt = seq_qvga
     intr = synth.Intrinsics.qvga()
