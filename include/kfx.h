@@ -220,6 +220,15 @@ int kfx_raycast_stats(kfx_ctx *ctx, int64_t out[8]);
  * n int32 (x, y) pairs; each output holds n * (own1 - own0) entries, column
  * after column, z ascending (rgb: u8 c0, c1, c2, 0 per voxel).  Any output
  * may be null. */
+/* Host side of the Z-slab raycast combine (the same code the
+ * device combine runs, exposed for multi-process tests without a GPU): after
+ * the all-reduce MIN of the keys, clear the payload {Ts, nout} planes (4 x n
+ * u32) of the pixels this slab lost; after the all-reduce MAX of the payload
+ * bits, rebuild the level-0 vmap/nmap (n float3 each) of a tracked frame at
+ * cam2vol / Rinv (tsdf_volume.cu:246-255). */
+int kfx_slab_mask_payload(const uint32_t *key_local, const uint32_t *key_min, uint32_t *payload, int64_t n);
+int kfx_slab_expand(const uint32_t *payload, const kfx_intrinsics *intr, const kfx_pose *cam2vol,
+                    const float Rinv[9], float *vmap, float *nmap);
 int kfx_download_columns(kfx_ctx *ctx, const int32_t *cols, int n, int16_t *tsdf, int16_t *weight,
                          uint32_t *rgb);
 

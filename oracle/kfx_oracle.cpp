@@ -599,7 +599,7 @@ static void raycast_impl(const int16_t *tsdf, const int dims[3], const float vs[
                          const float range[3], const kfx_intrinsics *in, const kfx_pose *pose,
                          const float Rinv[9], float *vmap, float *nmap, const int32_t *pix,
                          int64_t npix, int zb, int zn, int own0, int own1, uint32_t *keys,
-                         uint8_t *touch = nullptr, int64_t *reads = nullptr) {
+                         uint8_t *touch = nullptr, int64_t *reads = nullptr, float *ts_out = nullptr) {
   RayCtx c;
   c.touch = touch;
   c.reads = reads;
@@ -629,6 +629,7 @@ static void raycast_impl(const int16_t *tsdf, const int dims[3], const float vs[
     st3(vmap, o, {0.f, 0.f, 0.f});
     st3(nmap, o, {0.f, 0.f, 0.f});
     if (keys) keys[o] = UINT32_MAX;
+    if (ts_out) ts_out[o] = 0.f;
     const V3 pp = {(1.f * ((float)x - in->cx)) / in->fx, (1.f * ((float)y - in->cy)) / in->fy,
                    1.f};
     const V3 dir = normalized(rmul(pose->R, pp));
@@ -671,6 +672,7 @@ static void raycast_impl(const int16_t *tsdf, const int dims[3], const float vs[
           st3(nmap, o, rmul(Rinv, n));
           st3(vmap, o, rmul(Rinv, sub(vertex, org)));
           if (keys) keys[o] = k;
+          if (ts_out) ts_out[o] = Ts;
           break;
         }
       }
@@ -707,9 +709,9 @@ void kfo_raycast_touched(const int16_t *tsdf, const int dims[3], const float vs[
 void kfo_raycast_slab(const int16_t *tsdf, const int dims[3], const float vs[3],
                       const float range[3], const kfx_intrinsics *in, const kfx_pose *pose,
                       const float Rinv[9], int zb, int zn, int own0, int own1, float *vmap,
-                      float *nmap, uint32_t *keys) {
+                      float *nmap, uint32_t *keys, float *ts) {
   raycast_impl(tsdf, dims, vs, range, in, pose, Rinv, vmap, nmap, nullptr, 0, zb, zn, own0, own1,
-               keys);
+               keys, nullptr, nullptr, ts);
 }
 
 // FullScan6 (tsdf_volume.cu:307-481) in the canonical order of the GPU

@@ -105,7 +105,7 @@ void kfo_raycast_touched(const int16_t *tsdf, const int dims[3], const float vs[
 void kfo_raycast_slab(const int16_t *tsdf, const int dims[3], const float vs[3],
                       const float range[3], const kfx_intrinsics *in, const kfx_pose *pose,
                       const float Rinv[9], int zb, int zn, int own0, int own1, float *vmap,
-                      float *nmap, uint32_t *keys);
+                      float *nmap, uint32_t *keys, float *ts /* Ts of the hit per pixel (0: none), nullable */);
 
 /* FullScan6 point extraction (tsdf_volume.cu:307-481), canonical order; x-fastest
  * volume; z in [zlo, zhi); writes min(cap, total) points, returns total. */

@@ -60,7 +60,7 @@ def lib():
         L.kfo_raycast.argtypes = [P(C.c_int16), P(i), P(f), P(f), P(Intrinsics), P(Pose), P(f), P(f), P(f),
                                   P(C.c_int32), C.c_int64]
         L.kfo_raycast_slab.argtypes = [P(C.c_int16), P(i), P(f), P(f), P(Intrinsics), P(Pose), P(f), i, i, i, i,
-                                       P(f), P(f), P(C.c_uint32)]
+                                       P(f), P(f), P(C.c_uint32), P(f)]
         L.kfo_extract_points.argtypes = [P(C.c_int16), P(C.c_int16), P(i), P(f), P(Pose), i, i, P(f),
                                          C.c_int64]
         L.kfo_extract_points.restype = C.c_int64
@@ -256,16 +256,18 @@ def raycast_touched(vol: Volume, intr: Intrinsics, cam2vol: Pose, Rinv: np.ndarr
 def raycast_slab(tsdf: np.ndarray, vol: Volume, intr: Intrinsics, cam2vol: Pose, Rinv: np.ndarray,
                  zb: int, zn: int, own0: int, own1: int):
     """Per-slab raycast of the Z-slab decomposition: only slices
-    [zb, zb+zn) of `tsdf` (full-size array) are read.  Returns (keys u32, vmap, nmap)."""
+    [zb, zb+zn) of `tsdf` (full-size array) are read.  Returns (keys u32, vmap,
+    nmap, Ts of the hit per pixel (0: none))."""
     vmap = np.zeros((intr.height, intr.width, 3), np.float32)
     nmap = np.zeros_like(vmap)
     keys = np.zeros((intr.height, intr.width), np.uint32)
+    ts = np.zeros((intr.height, intr.width), np.float32)
     Rinv = _f32(Rinv).reshape(9)
     tsdf = np.ascontiguousarray(tsdf, np.int16)
     lib().kfo_raycast_slab(i16ptr(tsdf), vol.dims.ctypes.data_as(C.POINTER(C.c_int)), fptr(vol.voxel_size),
                            fptr(vol.range), C.byref(intr), C.byref(cam2vol), fptr(Rinv), zb, zn, own0, own1,
-                           fptr(vmap), fptr(nmap), keys.ctypes.data_as(C.POINTER(C.c_uint32)))
-    return keys, vmap, nmap
+                           fptr(vmap), fptr(nmap), keys.ctypes.data_as(C.POINTER(C.c_uint32)), fptr(ts))
+    return keys, vmap, nmap, ts
 
 
 def slab_bounds(Z: int, rank: int, world: int, halo: int = 4):

@@ -245,17 +245,20 @@ int enqueue_frame(kfx_ctx *c, FrameInput in, hipEvent_t *ev) {
   } while (0)
 
 // Cross-slab raycast combine: all-reduce MIN of the per-pixel
-// event keys, each slab clears the pixels it lost, all-reduce MAX of the map
-// bits (level-0 vmap and nmap are one contiguous buffer), then the pyramid.
+// event keys, each slab clears the payload {Ts, nout} of the pixels it lost,
+// all-reduce MAX of the payload bits (16 B per pixel instead of the 24 B of
+// vmap|nmap), every rank rebuilds the level-0 maps from it, then the pyramid.
 int enqueue_combine(kfx_ctx *c) {
   hipStream_t s = c->stream;
   const size_t np = (size_t)c->g[0].w * c->g[0].h;
+  uint32_t *pay = c->key_local + np;  // [Ts | nx | ny | nz] planes after the keys
   if (c->world > 1 || c->comm) {
     if (!c->comm) return set_err(KFX_ERR_STATE, "slab context without a communicator (kfx_comm_init, or kfx_pipeline_group)");
     NCCLCHK(ncclAllReduce(c->key_local, c->key_min, np, ncclUint32, ncclMin, c->comm, s));
-    launch_slab_mask(s, c->key_local, c->key_min, c->prev.v[0], c->prev.n[0], (int)np);
-    NCCLCHK(ncclAllReduce(c->prev.v[0], c->prev.v[0], 6 * np, ncclUint32, ncclMax, c->comm, s));
+    launch_slab_mask(s, c->key_local, c->key_min, (int)np);
+    NCCLCHK(ncclAllReduce(pay, pay, 4 * np, ncclUint32, ncclMax, c->comm, s));
   }
+  launch_slab_expand(s, c->g[0], pay, c->cur, c->prev, c->st, c->pose_log, to_dev(c->p.volu_pose));
   launch_resize(s, c->L, c->g, c->cur, c->prev, c->st, nullptr);
   return KFX_OK;
 }
@@ -700,7 +703,7 @@ static int create_impl(const kfx_intrinsics *intr, const kfx_params *params, int
   }
   const size_t np0 = (size_t)intr->width * intr->height;
   if (slab) {
-    if ((r = dalloc(c, (void **)&c->key_local, np0 * 4))) return fail(r);
+    if ((r = dalloc(c, (void **)&c->key_local, np0 * 4 * 5))) return fail(r);  // keys + payload
     if ((r = dalloc(c, (void **)&c->key_min, np0 * 4))) return fail(r);
   }
   if ((r = dalloc(c, (void **)&c->raw0_u16, np0 * 2))) return fail(r);
@@ -1151,6 +1154,25 @@ int kfx_download_columns(kfx_ctx *c, const int32_t *cols, int n, int16_t *t, int
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   (void)hipFree(tmp);
   if (e != hipSuccess) return set_err(KFX_ERR_HIP, std::string("download_columns: ") + hipGetErrorString(e));
+  return KFX_OK;
+}
+
+int kfx_slab_mask_payload(const uint32_t *key_local, const uint32_t *key_min, uint32_t *payload, int64_t n) {
+  if (!key_local || !key_min || !payload || n < 0) return set_err(KFX_ERR_ARG, "null argument");
+  for (int64_t i = 0; i < n; ++i) slab_mask_px(key_local, key_min, payload, (size_t)n, (size_t)i);
+  return KFX_OK;
+}
+
+int kfx_slab_expand(const uint32_t *payload, const kfx_intrinsics *intr, const kfx_pose *cam2vol,
+                    const float Rinv[9], float *vmap, float *nmap) {
+  if (!payload || !intr || !cam2vol || !Rinv || !vmap || !nmap) return set_err(KFX_ERR_ARG, "null argument");
+  const LevelGeom g = level_geom(*intr, 0);
+  const size_t n = (size_t)g.w * g.h;
+  for (size_t i = 0; i < n; ++i) {
+    float d[3];
+    ray_dir(cam2vol->R, g, (int)(i % g.w), (int)(i / g.w), d);
+    slab_expand_px(payload, n, i, cam2vol->t, d, Rinv, vmap + 3 * i, nmap + 3 * i);
+  }
   return KFX_OK;
 }
 
@@ -1667,7 +1689,7 @@ int kfx_pipeline_group(kfx_ctx **cs, int n, const uint8_t *bgr, const float *dep
   for (int k = 0; k < n; ++k) {
     kin[k] = cs[k]->key_local;
     kout[k] = cs[k]->key_min;
-    pay[k] = reinterpret_cast<uint32_t *>(cs[k]->prev.v[0]);
+    pay[k] = cs[k]->key_local + np;
   }
   kfx_ctx *c0 = cs[0];
   if ((r = check_ctx(c0))) return r;
@@ -1676,17 +1698,18 @@ int kfx_pipeline_group(kfx_ctx **cs, int n, const uint8_t *bgr, const float *dep
   HIPCHK(hipStreamSynchronize(c0->stream));
   for (int k = 0; k < n; ++k) {
     if ((r = check_ctx(cs[k]))) return r;
-    launch_slab_mask(cs[k]->stream, cs[k]->key_local, cs[k]->key_min, cs[k]->prev.v[0],
-                     cs[k]->prev.n[0], (int)np);
+    launch_slab_mask(cs[k]->stream, cs[k]->key_local, cs[k]->key_min, (int)np);
     HIPCHK(hipStreamSynchronize(cs[k]->stream));
   }
   if ((r = check_ctx(c0))) return r;
-  launch_group_reduce(c0->stream, pay, n, pay, n, 6 * np, true);
+  launch_group_reduce(c0->stream, pay, n, pay, n, 4 * np, true);
   HIPCHK(hipStreamSynchronize(c0->stream));
   int status = KFX_OK;
   for (int k = 0; k < n; ++k) {
     kfx_ctx *c = cs[k];
     if ((r = check_ctx(c))) return r;
+    launch_slab_expand(c->stream, c->g[0], c->key_local + np, c->cur, c->prev, c->st, c->pose_log,
+                       to_dev(c->p.volu_pose));
     launch_resize(c->stream, c->L, c->g, c->cur, c->prev, c->st, nullptr);
     HIPCHK(hipGetLastError());
     c->pending += 1;

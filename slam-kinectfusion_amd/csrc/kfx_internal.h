@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 #include <stddef.h>
 #include <stdint.h>
+#include <math.h>
 
 namespace kfx {
 
@@ -113,6 +114,54 @@ struct VolView {
   __host__ __device__ size_t tile_voxels() const { return (size_t)zn * 64; }
 };
 
+// ---- slab raycast combine, shared by the kernels and the host entry points
+// (kfx_slab_mask_payload / kfx_slab_expand) so a CPU test drives the same code.
+// A slab ships per pixel only {Ts, nout} of its winning hit (the payload,
+// 4 u32 planes); every rank rebuilds the vertex from Ts and the ray with the
+// raycast's own float ops.
+// raycasthelper (tsdf_volume.cu:217-220): dir = normalize(R * reproj(x, y, 1))
+__host__ __device__ inline void ray_dir(const float *R, const LevelGeom &g, int x, int y, float d[3]) {
+  const float p0 = (1.f * ((float)x - g.cx)) / g.fx, p1 = (1.f * ((float)y - g.cy)) / g.fy, p2 = 1.f;
+  const float v0 = R[0] * p0 + R[1] * p1 + R[2] * p2;
+  const float v1 = R[3] * p0 + R[4] * p1 + R[5] * p2;
+  const float v2 = R[6] * p0 + R[7] * p1 + R[8] * p2;
+  const float t = sqrtf(v0 * v0 + v1 * v1 + v2 * v2);
+  d[0] = v0 / t;
+  d[1] = v1 / t;
+  d[2] = v2 / t;
+}
+// tsdf_volume.cu:247-255: vertex = org + dir * Ts, vmap = Rinv * (vertex - org)
+__host__ __device__ inline void hit_vertex(const float org[3], const float dir[3], float Ts, const float *Rinv,
+                                           float out[3]) {
+  const float w0 = (org[0] + dir[0] * Ts) - org[0];
+  const float w1 = (org[1] + dir[1] * Ts) - org[1];
+  const float w2 = (org[2] + dir[2] * Ts) - org[2];
+  out[0] = Rinv[0] * w0 + Rinv[1] * w1 + Rinv[2] * w2;
+  out[1] = Rinv[3] * w0 + Rinv[4] * w1 + Rinv[5] * w2;
+  out[2] = Rinv[6] * w0 + Rinv[7] * w1 + Rinv[8] * w2;
+}
+// The losers' payload is cleared after the MIN of the keys, so the MAX of the
+// u32 bits leaves the winner's (0 is the smallest u32; a hit's normal is
+// nonzero, so a zero normal means no surface).
+__host__ __device__ inline void slab_mask_px(const uint32_t *key_local, const uint32_t *key_min, uint32_t *pay,
+                                             size_t n, size_t i) {
+  if (key_local[i] != key_min[i])
+    for (int q = 0; q < 4; ++q) pay[q * n + i] = 0u;
+}
+__host__ __device__ inline void slab_expand_px(const uint32_t *pay, size_t n, size_t i, const float org[3],
+                                               const float dir[3], const float *Rinv, float v[3], float nm[3]) {
+  for (int q = 0; q < 3; ++q) {
+    union { uint32_t u; float f; } b;
+    b.u = pay[(1 + q) * n + i];
+    nm[q] = b.f;
+  }
+  v[0] = v[1] = v[2] = 0.f;
+  if ((pay[n + i] | pay[2 * n + i] | pay[3 * n + i]) == 0u) return;
+  union { uint32_t u; float f; } ts;
+  ts.u = pay[i];
+  hit_vertex(org, dir, ts.f, Rinv, v);
+}
+
 struct FrameView {
   float *d[kMaxLevels];
   float *v[kMaxLevels];
@@ -169,8 +218,11 @@ void launch_checksum(hipStream_t s, VolView v, unsigned long long *out);
 // renderPhong (type 0) / renderNormals (type 1) of the level-0 maps into w*h uchar3
 void launch_render(hipStream_t s, const float *vmap, const float *nmap, int n, const DevState *st,
                    const DevPose *log, int type, uint8_t *out);
-void launch_slab_mask(hipStream_t s, const uint32_t *key_local, const uint32_t *key_min,
-                      float *vmap, float *nmap, int n);
+// keys = [key | Ts | nx | ny | nz] planes of the slab raycast (launch_raycast's keys)
+void launch_slab_mask(hipStream_t s, const uint32_t *keys, const uint32_t *key_min, int n);
+// level-0 model maps from the combined payload (and the frame kind)
+void launch_slab_expand(hipStream_t s, LevelGeom g0, const uint32_t *pay, FrameView cur, FrameView prev,
+                        const DevState *st, const DevPose *log, DevPose vpose);
 constexpr int kMaxGroup = 16;
 // element-wise MIN/MAX of n_in u32 buffers (any device-accessible pointers),
 // result stored to each of the n_out buffers

@@ -1632,6 +1632,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KFX_RAY_OCC
   const int kind = s_kind;
   f3 vout = {0.f, 0.f, 0.f}, nout = {0.f, 0.f, 0.f};
   uint32_t key = kind == 0 ? 0u : UINT_MAX;  // kSlab: sample index of the decisive event
+  float hts = 0.f;                             // kSlab: Ts of the hit written to the maps
   if (kind == 0 && inimg) {  // frame 1: the measured maps become the model maps
     vout = ld3(cur.v[0], o);
     nout = ld3(cur.n[0], o);
@@ -1639,8 +1640,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KFX_RAY_OCC
   if (kind == 1) {  // block-uniform
     const DevPose P = s_c2v;
     const f3 org = {P.t[0], P.t[1], P.t[2]};
-    const f3 pp = {(1.f * ((float)x - g.cx)) / g.fx, (1.f * ((float)y - g.cy)) / g.fy, 1.f};
-    const f3 dir = normalized(rmul(P.R, pp));
+    float da[3];
+    ray_dir(P.R, g, x, y, da);
+    const f3 dir = {da[0], da[1], da[2]};
     const f3 invR = {1.f / dir.x, 1.f / dir.y, 1.f / dir.z};
     const f3 tbot = mulc(invR, sub({0.f, 0.f, 0.f}, org));
     const f3 ttop = mulc(invR, sub({v.range[0], v.range[1], v.range[2]}, org));
@@ -1682,6 +1684,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KFX_RAY_OCC
     // order, same result.
     bool cand = false;
     f3 cvert = {0.f, 0.f, 0.f}, r_nextp = nextp;
+    float cts = 0.f;  // the candidate's Ts (slab payload)
     float r_rl = 0.f, r_tprev = 0.f;
     uint32_t ckey = 0u, r_kbase = 0u;
     // Empty-space skipping (exact): no event can happen at a sample whose
@@ -1895,6 +1898,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KFX_RAY_OCC
             }
             const float Ts = rj - (v.vs[0] * tc) / (tc - tn);  // A3 (R)
             cvert = add(org, scl(dir, Ts));
+            cts = Ts;
             cand = true;
             ckey = kbase + (uint32_t)j0;
             // resume state: sample j0 was processed, the next is j0 + 1
@@ -1945,6 +1949,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KFX_RAY_OCC
         nout = rmul(ri, n);
         vout = rmul(ri, sub(cvert, org));
         key = ckey;
+        hts = cts;
       } else {  // NaN normal: keep marching after the candidate (tsdf_volume.cu:251)
         live = true;
         nextp = r_nextp;
@@ -1990,9 +1995,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KFX_RAY_OCC
     return;
   }
   if (inimg) {
-    st3(prev.v[0], o, vout);
-    st3(prev.n[0], o, nout);
-    if (kSlab) keys[o] = key;
+    if (kSlab) {  // key + payload {Ts, nout} (kfx_internal.h slab combine)
+      const size_t np = (size_t)g.w * g.h;
+      keys[o] = key;
+      keys[np + o] = __float_as_uint(hts);
+      keys[2 * np + o] = __float_as_uint(nout.x);
+      keys[3 * np + o] = __float_as_uint(nout.y);
+      keys[4 * np + o] = __float_as_uint(nout.z);
+    } else {
+      st3(prev.v[0], o, vout);
+      st3(prev.n[0], o, nout);
+    }
   }
   if (kSlab) return;  // resize runs after the cross-slab combine (k_resize)
   resize_tile(ra, kind, tx0, ty0, lx, ly, vout, nout, cur, prev);
@@ -2176,15 +2189,45 @@ __global__ __launch_bounds__(256) void k_resize(RayArgs ra, FrameView cur, Frame
 }
 
 // Cross-slab combine, step 2 (after the all-reduce MIN of the keys): a rank
-// that does not hold the earliest event of a pixel clears its maps there, so
-// the all-reduce MAX of the map bits (step 3) leaves exactly the winner's bits
-// (0 is the smallest u32; -0.f and NaN payloads survive bit for bit).
-__global__ void k_slab_mask(const uint32_t *__restrict__ key_local,
-                            const uint32_t *__restrict__ key_min, float *vmap, float *nmap, int n) {
+// that does not hold the earliest event of a pixel clears its payload there,
+// so the all-reduce MAX of the payload bits (step 3) leaves exactly the
+// winner's (kfx_internal.h slab_mask_px).
+__global__ void k_slab_mask(const uint32_t *__restrict__ keys, const uint32_t *__restrict__ key_min, int n) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n || key_local[i] == key_min[i]) return;
-  st3(vmap, i, {0.f, 0.f, 0.f});
-  st3(nmap, i, {0.f, 0.f, 0.f});
+  if (i < n) slab_mask_px(keys, key_min, const_cast<uint32_t *>(keys) + n, (size_t)n, (size_t)i);
+}
+// Step 4: the level-0 model maps from the combined payload (frame kind as in
+// k_raycast: frame 1 copies the measured maps, a reset frame writes zeros).
+__global__ __launch_bounds__(256) void k_slab_expand(LevelGeom g, const uint32_t *__restrict__ pay, FrameView cur,
+                                                     FrameView prev, const DevState *__restrict__ st,
+                                                     const DevPose *__restrict__ log, DevPose vpose) {
+  __shared__ DevPose s_c2v;
+  __shared__ float s_rinv[9];
+  __shared__ int s_kind;
+  if (threadIdx.x == 0) {
+    s_kind = frame_kind(st);
+    if (s_kind == 1) {
+      s_c2v = pose_mul(pose_inv(vpose), frame_pose(st, log, 1));
+      for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) s_rinv[3 * i + j] = s_c2v.R[3 * j + i];
+    }
+  }
+  __syncthreads();
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= g.w * g.h) return;
+  f3 v = {0.f, 0.f, 0.f}, nm = {0.f, 0.f, 0.f};
+  if (s_kind == 0) {
+    v = ld3(cur.v[0], i);
+    nm = ld3(cur.n[0], i);
+  } else if (s_kind == 1) {
+    float d[3], a[3], b[3];
+    ray_dir(s_c2v.R, g, i % g.w, i / g.w, d);
+    slab_expand_px(pay, (size_t)g.w * g.h, (size_t)i, s_c2v.t, d, s_rinv, a, b);
+    v = {a[0], a[1], a[2]};
+    nm = {b[0], b[1], b[2]};
+  }
+  st3(prev.v[0], i, v);
+  st3(prev.n[0], i, nm);
 }
 
 // In-process group combine (several slab contexts in one process): element-wise
@@ -2843,10 +2886,13 @@ void launch_render(hipStream_t s, const float *vmap, const float *nmap, int n, c
   hipLaunchKernelGGL(k_render, dim3((n + 255) / 256), dim3(256), 0, s, vmap, nmap, n, st, log, type, out);
 }
 
-void launch_slab_mask(hipStream_t s, const uint32_t *key_local, const uint32_t *key_min,
-                      float *vmap, float *nmap, int n) {
-  hipLaunchKernelGGL(k_slab_mask, dim3((n + 255) / 256), dim3(256), 0, s, key_local, key_min, vmap,
-                     nmap, n);
+void launch_slab_mask(hipStream_t s, const uint32_t *keys, const uint32_t *key_min, int n) {
+  hipLaunchKernelGGL(k_slab_mask, dim3((n + 255) / 256), dim3(256), 0, s, keys, key_min, n);
+}
+void launch_slab_expand(hipStream_t s, LevelGeom g0, const uint32_t *pay, FrameView cur, FrameView prev,
+                        const DevState *st, const DevPose *log, DevPose vpose) {
+  hipLaunchKernelGGL(k_slab_expand, dim3((g0.w * g0.h + 255) / 256), dim3(256), 0, s, g0, pay, cur, prev, st,
+                     log, vpose);
 }
 
 void launch_group_reduce(hipStream_t s, uint32_t *const *in, int n_in, uint32_t *const *out,

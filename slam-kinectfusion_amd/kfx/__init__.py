@@ -33,7 +33,7 @@ EXPORTS = [
     "kfx_write_poses_txt", "kfx_get_frame_maps", "kfx_set_frame_maps", "kfx_download_tsdf",
     "kfx_upload_tsdf", "kfx_download_volume_soa", "kfx_stage_preprocess", "kfx_stage_icp_accumulate",
     "kfx_stage_icp", "kfx_stage_integrate", "kfx_stage_raycast", "kfx_set_profiling", "kfx_get_stage_ms",
-    "kfx_integrate_counts", "kfx_integrate_stats", "kfx_raycast_stats", "kfx_download_columns", "kfx_pipeline_async", "kfx_pipeline_async_u16", "kfx_create_slab", "kfx_slab_info", "kfx_comm_get_unique_id", "kfx_comm_init",
+    "kfx_integrate_counts", "kfx_integrate_stats", "kfx_raycast_stats", "kfx_download_columns", "kfx_pipeline_async", "kfx_pipeline_async_u16", "kfx_slab_mask_payload", "kfx_slab_expand", "kfx_create_slab", "kfx_slab_info", "kfx_comm_get_unique_id", "kfx_comm_init",
     "kfx_pipeline_group", "kfx_render", "kfx_volume_checksum", "kfx_extract_points", "kfx_write_ply", "kfx_save_pointcloud",
     "kfx_extract_mesh", "kfx_write_ply_mesh",
     "kfx_dataset_open", "kfx_dataset_info", "kfx_dataset_read", "kfx_dataset_close", "kfx_png_info",
@@ -101,6 +101,8 @@ def lib():
         "kfx_integrate_stats": ([vp, P(C.c_int64)], i),
         "kfx_raycast_stats": ([vp, P(C.c_int64)], i),
         "kfx_pipeline_async": ([vp, P(C.c_uint8), P(f)], i),
+        "kfx_slab_mask_payload": ([P(C.c_uint32), P(C.c_uint32), P(C.c_uint32), C.c_int64], i),
+        "kfx_slab_expand": ([P(C.c_uint32), P(Intrinsics), P(Pose), P(f), P(f), P(f)], i),
         "kfx_pipeline_async_u16": ([vp, P(C.c_uint8), P(C.c_uint16)], i),
         "kfx_download_columns": ([vp, P(C.c_int32), i, P(C.c_int16), P(C.c_int16), P(C.c_uint32)], i),
         "kfx_create_slab": ([P(Intrinsics), P(Params), i, i, i, P(vp)], i),
@@ -136,6 +138,30 @@ def _check(rc: int, what: str, ok=(KFX_OK,)) -> int:
     if rc not in ok:
         raise KfxError(f"{what} failed ({rc}): {lib().kfx_last_error().decode(errors='replace')}")
     return rc
+
+
+def slab_mask_payload(key_local: np.ndarray, key_min: np.ndarray, payload: np.ndarray) -> np.ndarray:
+    """Host side of the slab combine (kfx_slab_mask_payload): payload (4, n)
+    u32 with the pixels this slab lost cleared (returns a copy)."""
+    u32p = C.POINTER(C.c_uint32)
+    kl = np.ascontiguousarray(key_local, np.uint32).ravel()
+    km = np.ascontiguousarray(key_min, np.uint32).ravel()
+    pay = np.ascontiguousarray(payload, np.uint32).copy()
+    _check(lib().kfx_slab_mask_payload(kl.ctypes.data_as(u32p), km.ctypes.data_as(u32p), pay.ctypes.data_as(u32p),
+                                       kl.size), "kfx_slab_mask_payload")
+    return pay
+
+
+def slab_expand(payload: np.ndarray, intr, cam2vol: Pose, Rinv: np.ndarray):
+    """Host side of the slab combine (kfx_slab_expand): level-0 (vmap, nmap)."""
+    pay = np.ascontiguousarray(payload, np.uint32)
+    I = Intrinsics.from_any(intr)
+    vmap = np.zeros((I.height, I.width, 3), np.float32)
+    nmap = np.zeros_like(vmap)
+    R = np.ascontiguousarray(Rinv, np.float32).reshape(9)
+    _check(lib().kfx_slab_expand(pay.ctypes.data_as(C.POINTER(C.c_uint32)), C.byref(I), C.byref(cam2vol), fptr(R),
+                                 fptr(vmap), fptr(nmap)), "kfx_slab_expand")
+    return vmap, nmap
 
 
 def write_ply(path: str, xyz: np.ndarray):

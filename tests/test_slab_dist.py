@@ -5,8 +5,11 @@ Each slab reads only its stored slices (the rest of its array is filled with
 garbage, so a read outside the halo would show), ends rays only at owned
 samples and reports the deciding sample's index; the combine is the GPU path's:
 all-reduce MIN of the keys, clear the pixels a slab lost, all-reduce MAX of
-the map bits.  The multi-process variant runs that combine over
-torch.distributed (gloo, world_size 2) like bench.py's ranks do over RCCL.
+the payload bits {Ts, nout}, rebuild the maps from the payload.  The
+multi-process variant runs that combine over torch.distributed (gloo,
+world_size 2) like bench.py's ranks do over RCCL, with libkfx's own host
+build of the combine steps (kfx_slab_mask_payload, kfx_slab_expand: the code
+the device combine runs, callable without a GPU).
 """
 import os
 import socket
@@ -15,7 +18,7 @@ import numpy as np
 import pytest
 
 import oracle as O
-from kfx import synth
+from kfx import slab_expand, slab_mask_payload, synth
 from kfx.abi import Intrinsics, Pose, default_params
 
 L_VOL = 2.048
@@ -47,15 +50,22 @@ def _slab_view(vol, rank, world, seed):
     return t, (zb, zn, o0, o1)
 
 
-def _combine(parts):
-    keys = np.min(np.stack([k for k, _, _ in parts]), axis=0)
-    out_v = np.zeros_like(parts[0][1]).view(np.uint32)
-    out_n = np.zeros_like(parts[0][2]).view(np.uint32)
-    for k, v, n in parts:
-        lost = (k != keys)[..., None]
-        out_v = np.maximum(out_v, np.where(lost, 0, v.view(np.uint32)))
-        out_n = np.maximum(out_n, np.where(lost, 0, n.view(np.uint32)))
-    return keys, out_v.view(np.float32), out_n.view(np.float32)
+def _payload(ts, nmap):
+    """A slab's combine payload: the [Ts | nx | ny | nz] u32 planes."""
+    n = ts.size
+    pay = np.zeros((4, n), np.uint32)
+    pay[0] = ts.ravel().view(np.uint32)
+    pay[1:] = nmap.reshape(n, 3).T.view(np.uint32)
+    return pay
+
+
+def _combine(parts, I, cam2vol, Rinv):
+    keys = np.min(np.stack([p[0] for p in parts]), axis=0)
+    pay = np.zeros((4, keys.size), np.uint32)
+    for k, v, n, ts in parts:
+        pay = np.maximum(pay, slab_mask_payload(k, keys, _payload(ts, n)))
+    v, n = slab_expand(pay, I, cam2vol, Rinv)
+    return keys, v, n
 
 
 @pytest.fixture(scope="module")
@@ -66,12 +76,16 @@ def scene():
 def test_single_slab_equals_raycast(scene):
     I, vol, poses = scene
     cam2vol, Rinv = poses[0]
-    k, v, n = O.raycast_slab(vol.tsdf, vol, I, cam2vol, Rinv, 0, DIMS, 0, DIMS)
+    k, v, n, ts = O.raycast_slab(vol.tsdf, vol, I, cam2vol, Rinv, 0, DIMS, 0, DIMS)
     rv, rn = O.raycast(vol, I, cam2vol, Rinv)
     assert np.array_equal(v.view(np.uint32), rv.view(np.uint32))
     assert np.array_equal(n.view(np.uint32), rn.view(np.uint32))
     hit = rv[..., 2] != 0
     assert hit.mean() > 0.5 and (k[hit] != np.uint32(0xFFFFFFFF)).all()
+    # the payload path rebuilds the same maps (libkfx host combine)
+    ev, en = slab_expand(_payload(ts, n), I, cam2vol, Rinv)
+    assert np.array_equal(ev.view(np.uint32), rv.view(np.uint32))
+    assert np.array_equal(en.view(np.uint32), rn.view(np.uint32))
 
 
 @pytest.mark.parametrize("world", [2, 3, 4, 8])
@@ -82,12 +96,12 @@ def test_slab_decomposition_serial(world, scene):
         for r in range(world):
             t, b = _slab_view(vol, r, world, seed=r)
             parts.append(O.raycast_slab(t, vol, I, cam2vol, Rinv, *b))
-        keys, v, n = _combine(parts)
+        keys, v, n = _combine(parts, I, cam2vol, Rinv)
         rv, rn = O.raycast(vol, I, cam2vol, Rinv)
         assert np.array_equal(v.view(np.uint32), rv.view(np.uint32)), (v != rv).sum()
         assert np.array_equal(n.view(np.uint32), rn.view(np.uint32))
         # the decisive events really are spread over several slabs
-        winners = [((k == keys) & (keys != 0xFFFFFFFF)).sum() for k, _, _ in parts]
+        winners = [((p[0] == keys) & (keys != 0xFFFFFFFF)).sum() for p in parts]
         assert sum(1 for w in winners if w > 0) >= 2
 
 
@@ -107,17 +121,16 @@ def _rank_main(rank, world, port, out_dir):
     ok = True
     for cam2vol, Rinv in poses:
         t, b = _slab_view(vol, rank, world, seed=100 + rank)
-        k, v, n = O.raycast_slab(t, vol, I, cam2vol, Rinv, *b)
+        k, v, n, ts = O.raycast_slab(t, vol, I, cam2vol, Rinv, *b)
         keys = torch.from_numpy(k.astype(np.int64))
         dist.all_reduce(keys, op=dist.ReduceOp.MIN)
-        lost = (k.astype(np.int64) != keys.numpy())[..., None]
-        vb = torch.from_numpy(np.where(lost, 0, v.view(np.uint32)).astype(np.int64))
-        nb = torch.from_numpy(np.where(lost, 0, n.view(np.uint32)).astype(np.int64))
-        dist.all_reduce(vb, op=dist.ReduceOp.MAX)
-        dist.all_reduce(nb, op=dist.ReduceOp.MAX)
+        pay = slab_mask_payload(k, keys.numpy().astype(np.uint32), _payload(ts, n))  # libkfx host combine
+        pb = torch.from_numpy(pay.astype(np.int64))
+        dist.all_reduce(pb, op=dist.ReduceOp.MAX)
+        gv, gn = slab_expand(pb.numpy().astype(np.uint32), I, cam2vol, Rinv)  # libkfx host combine
         rv, rn = O.raycast(vol, I, cam2vol, Rinv)
-        ok &= np.array_equal(vb.numpy().astype(np.uint32), rv.view(np.uint32))
-        ok &= np.array_equal(nb.numpy().astype(np.uint32), rn.view(np.uint32))
+        ok &= np.array_equal(gv.view(np.uint32), rv.view(np.uint32))
+        ok &= np.array_equal(gn.view(np.uint32), rn.view(np.uint32))
     dist.destroy_process_group()
     with open(os.path.join(out_dir, f"rank{rank}"), "w") as f:
         f.write("ok" if ok else "mismatch")
