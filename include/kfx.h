@@ -138,6 +138,12 @@ int kfx_get_kernel_timing(kfx_ctx *ctx, float out_ms[3], int *n_samples);
  * iteration).  Returns 1 if the persistent kernel is usable on this context, 0
  * if not, <0 on error.  Results are identical either way. */
 int kfx_set_icp_persistent(kfx_ctx *ctx, int enabled);
+/* Slab contexts (SURVEY.md §8e alternative): instead of every rank running
+ * the whole ICP (default), rank r accumulates the 27 products over its band
+ * of each level's rows and the exact int64 partials are all-reduced (SUM)
+ * per iteration (19 collectives per frame), then every rank solves the same
+ * system — poses identical to the replicated mode. */
+int kfx_set_icp_allreduce(kfx_ctx *ctx, int enabled);
 /* Profiling seam: per ICP iteration of the last persistent-ICP frame, five
  * s_memrealtime stamps (100 MHz): block 0 start, block 0 arrived, block 0
  * released from the barrier, block 0 solved, last block arrived.  Returns the

@@ -125,6 +125,7 @@ struct kfx_ctx {
   IcpPlan icp_plan{};
   bool icp_persistent = false;  // plan fits and its grid is co-resident
   bool icp_persistent_enabled = true;
+  bool icp_sharded = false;  // slab ranks: ICP partials all-reduced (kfx_set_icp_allreduce)
   unsigned long long *counters = nullptr;
   float *xpose = nullptr;  // explicit stage poses (21 floats: pose R,t + Rinv)
   std::vector<void *> allocs;
@@ -225,14 +226,15 @@ struct FrameInput {
 // [4] after raycast (+ slab combine); [0..1] are absent for overlapped frames.
 // Slab contexts stop after their local raycast (enqueue_local) and then
 // combine the slabs' raycast results (enqueue_combine).
+void enqueue_pre(kfx_ctx *c, FrameInput in, hipEvent_t *ev);
 void enqueue_local(kfx_ctx *c, FrameInput in, hipEvent_t *ev);
-void enqueue_track(kfx_ctx *c, FrameInput in, hipEvent_t *ev, bool begin);
+int enqueue_track(kfx_ctx *c, FrameInput in, hipEvent_t *ev, bool begin);
 int enqueue_combine(kfx_ctx *c);
 
 int enqueue_frame(kfx_ctx *c, FrameInput in, hipEvent_t *ev) {
-  enqueue_local(c, in, ev);
-  int r = KFX_OK;
-  if (c->slab) r = enqueue_combine(c);
+  enqueue_pre(c, in, ev);
+  int r = enqueue_track(c, in, ev, false);
+  if (!r && c->slab) r = enqueue_combine(c);
   if (ev) (void)hipEventRecord(ev[4], c->stream);
   return r;
 }
@@ -263,10 +265,10 @@ int enqueue_combine(kfx_ctx *c) {
   return KFX_OK;
 }
 
-void enqueue_local(kfx_ctx *c, FrameInput in, hipEvent_t *ev) {
+// imageProcess (kinectfusion.cpp:48-76) into the current set
+void enqueue_pre(kfx_ctx *c, FrameInput in, hipEvent_t *ev) {
   hipStream_t s = c->stream;
   if (ev) (void)hipEventRecord(ev[0], s);
-  // imageProcess (kinectfusion.cpp:48-76)
   const float *raw[kMaxLevels];
   for (int l = 0; l < kMaxLevels; ++l) raw[l] = c->raw[l];
   raw[0] = in.d32;
@@ -282,15 +284,51 @@ void enqueue_local(kfx_ctx *c, FrameInput in, hipEvent_t *ev) {
                          c->p.bfilter_color_sigma, c->p.bfilter_spatial_sigma, c->p.dfilter_dist,
                          c->inv_lambda, c->dl0);
   if (ev) (void)hipEventRecord(ev[1], s);
-  enqueue_track(c, in, ev, false);
+}
+
+void enqueue_local(kfx_ctx *c, FrameInput in, hipEvent_t *ev) {
+  enqueue_pre(c, in, ev);
+  (void)enqueue_track(c, in, ev, false);
+}
+
+// Sharded ICP (kfx_set_icp_allreduce): this rank's band of
+// every level's rows, the 27 exact int64 partials all-reduced over RCCL per
+// iteration, every rank solving the same sums (poses identical to the
+// replicated mode).
+int enqueue_icp_sharded(kfx_ctx *c, bool begin) {
+  hipStream_t s = c->stream;
+  if (begin) launch_frame_begin(s, c->st, nullptr, c->g[0]);
+  long long *sums = reinterpret_cast<long long *>(reinterpret_cast<char *>(c->st) + offsetof(DevState, sums));
+  for (int level = c->L - 1; level >= 0; --level)
+    for (int it = 0; it < c->p.icp_iter_count[level]; ++it) {
+      launch_icp(s, c->g[level], c->cur.v[level], c->cur.n[level], c->prev.v[level], c->prev.n[level],
+                 c->p.icp_dist_threshold, c->angle_thr, c->st, c->icp_shards, c->icp_ticket, 0, 0, c->rank,
+                 c->world);
+      NCCLCHK(ncclAllReduce(sums, sums, 27, ncclInt64, ncclSum, c->comm, s));
+      launch_icp_solve(s, c->st);
+    }
+  return KFX_OK;
+}
+
+// integrate + raycast of the frame whose maps are in the current set
+void enqueue_map(kfx_ctx *c, FrameInput in, hipEvent_t *ev) {
+  hipStream_t s = c->stream;
+  launch_integrate(s, c->vol, c->g[0], c->dl0, in.bgr, c->st, c->pose_log,
+                   to_dev(c->p.volu_pose), nullptr, nullptr);
+  if (ev) (void)hipEventRecord(ev[3], s);
+  launch_raycast(s, c->vol, c->L, c->g, c->cur, c->prev, c->st, c->pose_log,
+                 to_dev(c->p.volu_pose), nullptr, c->slab ? c->key_local : nullptr);
 }
 
 // ICP, integrate and raycast of the frame whose maps are in the current set;
 // begin: the frame's frame_begin has not run yet (overlapped frames)
-void enqueue_track(kfx_ctx *c, FrameInput in, hipEvent_t *ev, bool begin) {
+int enqueue_track(kfx_ctx *c, FrameInput in, hipEvent_t *ev, bool begin) {
   hipStream_t s = c->stream;
   // ICPRegistration::rigidTransform (icp_registration.cpp:16-46)
-  if (c->icp_persistent && c->icp_persistent_enabled) {
+  int r = KFX_OK;
+  if (c->icp_sharded && c->comm) {
+    r = enqueue_icp_sharded(c, begin);
+  } else if (c->icp_persistent && c->icp_persistent_enabled) {
     launch_icp_track(s, c->icp_plan, c->st, c->icp_sync, begin ? 1 : 0);  // folds frame_begin in
   } else {
     if (begin) launch_frame_begin(s, c->st, nullptr, c->g[0]);
@@ -303,11 +341,8 @@ void enqueue_track(kfx_ctx *c, FrameInput in, hipEvent_t *ev, bool begin) {
   }
   if (ev) (void)hipEventRecord(ev[2], s);
   if (begin) (void)hipEventRecord(c->ev_icp, s);  // overlapped frames: the next preprocess waits here
-  launch_integrate(s, c->vol, c->g[0], c->dl0, in.bgr, c->st, c->pose_log,
-                   to_dev(c->p.volu_pose), nullptr, nullptr);
-  if (ev) (void)hipEventRecord(ev[3], s);
-  launch_raycast(s, c->vol, c->L, c->g, c->cur, c->prev, c->st, c->pose_log,
-                 to_dev(c->p.volu_pose), nullptr, c->slab ? c->key_local : nullptr);
+  enqueue_map(c, in, ev);
+  return r;
 }
 
 // Frame overlap: the preprocess of this frame runs on pstream into the set the
@@ -345,9 +380,8 @@ int enqueue_frame_overlap(kfx_ctx *c, FrameInput in, hipEvent_t *ev) {
   HIPCHK(hipEventRecord(c->ev_prep, b));
   HIPCHK(hipStreamWaitEvent(c->stream, c->ev_prep, 0));
   if (ev) HIPCHK(hipEventRecord(ev[1], c->stream));
-  enqueue_track(c, in, ev, true);
-  int r = KFX_OK;
-  if (c->slab) r = enqueue_combine(c);
+  int r = enqueue_track(c, in, ev, true);
+  if (!r && c->slab) r = enqueue_combine(c);
   if (ev) HIPCHK(hipEventRecord(ev[4], c->stream));
   HIPCHK(hipEventRecord(c->ev_free[p], c->stream));
   if (in.done) HIPCHK(hipEventRecord(in.done, c->stream));
@@ -951,6 +985,14 @@ int kfx_set_icp_persistent(kfx_ctx *c, int enabled) {
   if (c->icp_persistent_enabled != (enabled != 0)) destroy_graphs(c);
   c->icp_persistent_enabled = enabled != 0;
   return c->icp_persistent ? 1 : 0;
+}
+
+int kfx_set_icp_allreduce(kfx_ctx *c, int enabled) {
+  if (!c) return set_err(KFX_ERR_ARG, "null context");
+  if (!c->slab) return set_err(KFX_ERR_STATE, "ICP partial all-reduce needs a slab context");
+  if (c->icp_sharded != (enabled != 0)) destroy_graphs(c);
+  c->icp_sharded = enabled != 0;
+  return KFX_OK;
 }
 
 int kfx_get_icp_trace(kfx_ctx *c, uint64_t *out, int max_iters) {
@@ -1669,15 +1711,49 @@ int kfx_pipeline_group(kfx_ctx **cs, int n, const uint8_t *bgr, const float *dep
     }
   }
   int r;
+  const bool sharded = cs[0]->icp_sharded && n > 1;
   for (int k = 0; k < n; ++k) {  // local phase: preprocess, ICP, integrate, slab raycast
     kfx_ctx *c = cs[k];
     if ((r = check_ctx(c))) return r;
     if ((r = ensure_pose_capacity(c, 1))) return r;
+    if (c->icp_sharded != cs[0]->icp_sharded) return set_err(KFX_ERR_ARG, "group members differ in ICP mode");
     HIPCHK(hipMemcpyAsync(c->raw[0], depth_mm, np * 4, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(c->bgr, bgr, np * 3, hipMemcpyHostToDevice, c->stream));
     c->last_bgr = c->bgr;
-    enqueue_local(c, {c->raw[0], nullptr, c->bgr}, nullptr);
+    if (sharded) {
+      enqueue_pre(c, {c->raw[0], nullptr, c->bgr}, nullptr);
+    } else {
+      enqueue_local(c, {c->raw[0], nullptr, c->bgr}, nullptr);
+    }
     HIPCHK(hipGetLastError());
+  }
+  if (sharded) {  // sharded ICP: per iteration, members' bands, in-process sum, solves
+    DevState *sts[kMaxGroup];
+    for (int k = 0; k < n; ++k) sts[k] = cs[k]->st;
+    for (int level = cs[0]->L - 1; level >= 0; --level)
+      for (int it = 0; it < cs[0]->p.icp_iter_count[level]; ++it) {
+        for (int k = 0; k < n; ++k) {
+          kfx_ctx *c = cs[k];
+          if ((r = check_ctx(c))) return r;
+          launch_icp(c->stream, c->g[level], c->cur.v[level], c->cur.n[level], c->prev.v[level],
+                     c->prev.n[level], c->p.icp_dist_threshold, c->angle_thr, c->st, c->icp_shards,
+                     c->icp_ticket, 0, 0, k, n);
+          HIPCHK(hipStreamSynchronize(c->stream));
+        }
+        if ((r = check_ctx(cs[0]))) return r;
+        launch_group_sum_icp(cs[0]->stream, sts, n);
+        HIPCHK(hipStreamSynchronize(cs[0]->stream));
+        for (int k = 0; k < n; ++k) {
+          if ((r = check_ctx(cs[k]))) return r;
+          launch_icp_solve(cs[k]->stream, cs[k]->st);
+        }
+      }
+    for (int k = 0; k < n; ++k) {
+      kfx_ctx *c = cs[k];
+      if ((r = check_ctx(c))) return r;
+      enqueue_map(c, {c->raw[0], nullptr, c->bgr}, nullptr);
+      HIPCHK(hipGetLastError());
+    }
   }
   for (int k = 0; k < n; ++k) {
     if ((r = check_ctx(cs[k]))) return r;

@@ -186,9 +186,16 @@ IcpPlan make_icp_plan(int levels, const LevelGeom *g, const int *iters, FrameVie
 bool icp_persistent_ok(const IcpPlan &pl, int device);  // grid co-resident + slots fit
 // begin: run the frame's frame_begin inside the launch (no separate kernel)
 void launch_icp_track(hipStream_t s, const IcpPlan &pl, DevState *st, IcpSync *sync, int begin = 0);
+// band / nbands: only rows [ye*band/nbands, ye*(band+1)/nbands) of the
+// floor-covered region (a slab rank's share in the sharded ICP mode)
 void launch_icp(hipStream_t s, const LevelGeom &g, const float *cv, const float *cn,
                 const float *pv, const float *pn, float dist_thr, float angle_thr, DevState *st,
-                unsigned long long *shards, unsigned *ticket, int force, int update);
+                unsigned long long *shards, unsigned *ticket, int force, int update, int band = 0,
+                int nbands = 1);
+// one ICP solve (+ pose update) from DevState::sums
+void launch_icp_solve(hipStream_t s, DevState *st);
+// DevState::sums of each of the n members <- their sum
+void launch_group_sum_icp(hipStream_t s, DevState *const *st, int n);
 // The frame's global pose, the integrate/raycast poses and the
 // kinectfusion.cpp:84-104 bookkeeping are derived inside these kernels from
 // DevState + pose log (no separate commit launch).  `xpose` (device, 12 or 21

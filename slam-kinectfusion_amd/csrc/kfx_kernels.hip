@@ -531,13 +531,14 @@ __device__ __forceinline__ int xcd_remap(int b, int nb) {
   return xcd * q + min(xcd, r) + b / 8;
 }
 
+// Pixels [p0, npix) of the floor-covered region (p0 > 0: a slab rank's band).
 __device__ __forceinline__ void icp_load_cur(const LevelGeom &g, int xe, int npix, int grp,
                                              int ppl, const float *__restrict__ cv,
                                              const float *__restrict__ cn, f3 (&n0)[kIcpPix],
-                                             f3 (&v0)[kIcpPix], bool (&ok)[kIcpPix]) {
+                                             f3 (&v0)[kIcpPix], bool (&ok)[kIcpPix], int p0 = 0) {
 #pragma unroll
   for (int q = 0; q < kIcpPix; ++q) {
-    const int i = grp * kIcpThreads * ppl + q * kIcpThreads + threadIdx.x;
+    const int i = p0 + grp * kIcpThreads * ppl + q * kIcpThreads + threadIdx.x;
     ok[q] = q < ppl && i < npix;
     const size_t idx = ok[q] ? (size_t)(i / xe) * g.w + (i % xe) : 0;
     n0[q] = ld3(cn, idx);
@@ -631,7 +632,7 @@ __device__ __forceinline__ long long icp_block_reduce(IcpRed &r, const double (&
 
 // One ICP iteration per launch (stage API seam and the fallback when the
 // persistent kernel's grid cannot be co-resident).
-__global__ __launch_bounds__(kIcpThreads) void k_icp_acc(LevelGeom g, int xe, int npix,
+__global__ __launch_bounds__(kIcpThreads) void k_icp_acc(LevelGeom g, int xe, int p0, int npix,
                                                  const float *__restrict__ cv,
                                                  const float *__restrict__ cn,
                                                  const float *__restrict__ pv,
@@ -644,7 +645,7 @@ __global__ __launch_bounds__(kIcpThreads) void k_icp_acc(LevelGeom g, int xe, in
   const DevPose P = st->icp_pose;
   f3 n0[kIcpPix], v0[kIcpPix];
   bool ok[kIcpPix];
-  icp_load_cur(g, xe, npix, blockIdx.x, kIcpPix, cv, cn, n0, v0, ok);
+  icp_load_cur(g, xe, npix, blockIdx.x, kIcpPix, cv, cn, n0, v0, ok, p0);
   double acc[27];
   icp_lane(g, P, n0, v0, ok, kIcpPix, pv, pn, dist_thr, angle_thr, acc);
   __shared__ IcpRed red;
@@ -2230,6 +2231,11 @@ __global__ __launch_bounds__(256) void k_slab_expand(LevelGeom g, const uint32_t
   st3(prev.n[0], i, nm);
 }
 
+struct GroupSt {
+  DevState *p[kMaxGroup];
+  int n;
+};
+
 // In-process group combine (several slab contexts in one process): element-wise
 // MIN / MAX over the members' u32 buffers, result written back to every member.
 struct GroupBufs {
@@ -2745,11 +2751,50 @@ void launch_icp_track(hipStream_t s, const IcpPlan &pl, DevState *st, IcpSync *s
 
 void launch_icp(hipStream_t s, const LevelGeom &g, const float *cv, const float *cn,
                 const float *pv, const float *pn, float dist_thr, float angle_thr, DevState *st,
-                unsigned long long *shards, unsigned *ticket, int force, int update) {
+                unsigned long long *shards, unsigned *ticket, int force, int update, int band, int nbands) {
   int xe;
   const int n = icp_npix(g, &xe);
-  hipLaunchKernelGGL(k_icp_acc, dim3(icp_blocks(g)), dim3(kIcpThreads), 0, s, g, xe, n, cv, cn, pv, pn,
+  const int ye = n / std::max(xe, 1);  // band = whole rows of the floor-covered region
+  const int p0 = xe * (int)((long long)ye * band / nbands), p1 = xe * (int)((long long)ye * (band + 1) / nbands);
+  const int nb = std::max(1, (p1 - p0 + kIcpBlockPix - 1) / kIcpBlockPix);
+  hipLaunchKernelGGL(k_icp_acc, dim3(nb), dim3(kIcpThreads), 0, s, g, xe, p0, p1, cv, cn, pv, pn,
                      dist_thr, angle_thr, st, shards, ticket, force, update);
+}
+
+// The solve of one ICP iteration from DevState::sums (the all-reduced partials
+// of the sharded mode): icp_registration.cpp:33-42, as in k_icp_acc's last block.
+__global__ void k_icp_solve(DevState *__restrict__ st) {
+  if (st->mode != MODE_TRACK || st->icp_fail) return;
+  __shared__ long long sums[27];
+  if (threadIdx.x < 27) sums[threadIdx.x] = st->sums[threadIdx.x];
+  __syncthreads();
+  DevPose p = st->icp_pose;
+  double x[6];
+  const int f = icp_update(sums, p, x);
+  if (threadIdx.x == 0) {
+    if (f) {
+      st->icp_fail = 1;
+    } else {
+      st->icp_pose = p;
+#pragma unroll
+      for (int i = 0; i < 6; ++i) st->x[i] = x[i];
+    }
+  }
+}
+void launch_icp_solve(hipStream_t s, DevState *st) { hipLaunchKernelGGL(k_icp_solve, dim3(1), dim3(64), 0, s, st); }
+
+// In-process group: DevState::sums of every member <- their sum (int64, exact)
+__global__ void k_group_sum_icp(GroupSt g) {
+  if (threadIdx.x >= 27) return;
+  long long a = 0;
+  for (int k = 0; k < g.n; ++k) a += g.p[k]->sums[threadIdx.x];
+  for (int k = 0; k < g.n; ++k) g.p[k]->sums[threadIdx.x] = a;
+}
+void launch_group_sum_icp(hipStream_t s, DevState *const *st, int n) {
+  GroupSt g{};
+  g.n = n;
+  for (int k = 0; k < n; ++k) g.p[k] = st[k];
+  hipLaunchKernelGGL(k_group_sum_icp, dim3(1), dim3(64), 0, s, g);
 }
 
 void launch_integrate(hipStream_t s, VolView v, LevelGeom g0, const float2 *dl0,

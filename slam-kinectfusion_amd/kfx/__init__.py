@@ -33,7 +33,7 @@ EXPORTS = [
     "kfx_write_poses_txt", "kfx_get_frame_maps", "kfx_set_frame_maps", "kfx_download_tsdf",
     "kfx_upload_tsdf", "kfx_download_volume_soa", "kfx_stage_preprocess", "kfx_stage_icp_accumulate",
     "kfx_stage_icp", "kfx_stage_integrate", "kfx_stage_raycast", "kfx_set_profiling", "kfx_get_stage_ms",
-    "kfx_integrate_counts", "kfx_integrate_stats", "kfx_raycast_stats", "kfx_download_columns", "kfx_pipeline_async", "kfx_pipeline_async_u16", "kfx_slab_mask_payload", "kfx_slab_expand", "kfx_create_slab", "kfx_slab_info", "kfx_comm_get_unique_id", "kfx_comm_init",
+    "kfx_integrate_counts", "kfx_integrate_stats", "kfx_raycast_stats", "kfx_download_columns", "kfx_pipeline_async", "kfx_pipeline_async_u16", "kfx_slab_mask_payload", "kfx_slab_expand", "kfx_set_icp_allreduce", "kfx_create_slab", "kfx_slab_info", "kfx_comm_get_unique_id", "kfx_comm_init",
     "kfx_pipeline_group", "kfx_render", "kfx_volume_checksum", "kfx_extract_points", "kfx_write_ply", "kfx_save_pointcloud",
     "kfx_extract_mesh", "kfx_write_ply_mesh",
     "kfx_dataset_open", "kfx_dataset_info", "kfx_dataset_read", "kfx_dataset_close", "kfx_png_info",
@@ -102,6 +102,7 @@ def lib():
         "kfx_raycast_stats": ([vp, P(C.c_int64)], i),
         "kfx_pipeline_async": ([vp, P(C.c_uint8), P(f)], i),
         "kfx_slab_mask_payload": ([P(C.c_uint32), P(C.c_uint32), P(C.c_uint32), C.c_int64], i),
+        "kfx_set_icp_allreduce": ([vp, i], i),
         "kfx_slab_expand": ([P(C.c_uint32), P(Intrinsics), P(Pose), P(f), P(f), P(f)], i),
         "kfx_pipeline_async_u16": ([vp, P(C.c_uint8), P(C.c_uint16)], i),
         "kfx_download_columns": ([vp, P(C.c_int32), i, P(C.c_int16), P(C.c_int16), P(C.c_uint32)], i),
@@ -376,6 +377,10 @@ class KinectFusion:
     def set_frame_overlap(self, on: bool):
         """Overlap staged frames' preprocess with the previous frame's tracking."""
         _check(lib().kfx_set_frame_overlap(self._h, int(on)), "kfx_set_frame_overlap")
+
+    def set_icp_allreduce(self, on: bool):
+        """Slab contexts: shard the ICP sums over the ranks (all-reduced per iteration)."""
+        _check(lib().kfx_set_icp_allreduce(self._h, int(on)), "kfx_set_icp_allreduce")
 
     def set_icp_persistent(self, on: bool) -> bool:
         """Toggle the one-launch persistent ICP kernel; returns whether it is usable here."""

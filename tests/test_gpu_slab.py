@@ -98,6 +98,27 @@ def test_slab_group_vga_128(seq_qvga):
     single.close()
 
 
+@pytest.mark.parametrize("world", [2, 4])
+def test_slab_group_sharded_icp_matches_single_volume(world, seq_qvga):
+    """kfx_set_icp_allreduce: each slab sums its band of ICP rows, the exact
+    int64 partials are summed over the members per iteration (the RCCL
+    all-reduce of the multi-process path) — poses, maps and volume still equal
+    the single volume's bit for bit."""
+    bgr, dep, _ = seq_qvga
+    intr = synth.Intrinsics.qvga()
+    p = default_params(dims=64, range_m=L_VOL)
+    single, st = _single(intr, p, bgr, dep)
+    members = [KinectFusion(Intrinsics.from_any(intr), p, slab=(r, world)) for r in range(world)]
+    for m in members:
+        m.set_icp_allreduce(True)
+    gst = [pipeline_group(members, bgr[k], dep[k].astype(np.float32)) for k in range(len(dep))]
+    assert gst == st == [KFX_OK] * len(dep)
+    _compare(single, members)
+    for m in members:
+        m.close()
+    single.close()
+
+
 def test_slab_group_tracking_failure(seq_qvga):
     bgr, dep, _ = seq_qvga
     intr = synth.Intrinsics.qvga()
@@ -114,10 +135,11 @@ def test_slab_group_tracking_failure(seq_qvga):
         m.close()
 
 
-@pytest.mark.parametrize("graph", [True, False])
-def test_slab_rccl_single_rank_matches(graph, seq_qvga):
+@pytest.mark.parametrize("graph,icp_ar", [(True, False), (False, False), (True, True)])
+def test_slab_rccl_single_rank_matches(graph, icp_ar, seq_qvga):
     """A one-rank RCCL communicator: the collectives of the slab combine run
-    (captured into the per-frame graph when RCCL allows it)."""
+    (captured into the per-frame graph when RCCL allows it); with icp_ar the
+    19 per-iteration all-reduces of the sharded ICP as well."""
     bgr, dep, _ = seq_qvga
     intr = synth.Intrinsics.qvga()
     p = default_params(dims=64, range_m=L_VOL)
@@ -125,6 +147,7 @@ def test_slab_rccl_single_rank_matches(graph, seq_qvga):
     m = KinectFusion(Intrinsics.from_any(intr), p, slab=(0, 1))
     m.comm_init(comm_unique_id())
     m.set_graph_mode(graph)
+    m.set_icp_allreduce(icp_ar)
     gst = [m.pipeline(bgr[k], dep[k].astype(np.float32)) for k in range(len(dep))]
     assert gst == st
     _compare(single, [m])
