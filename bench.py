@@ -9,15 +9,20 @@ integrate, raycast, resize.  Frames are staged in HBM before the timed region
 (kfx_stage_frames); every timed frame then runs the captured per-frame hipGraph
 on its staged input.
 
+Configs (BASELINE.json configs[1..4], --config): c2 640x480 512^3 @ 4 mm (the
+metric's config, default at N=1), c3 1024^3 @ 2 mm single GPU (recorded beside
+the C2 line at N=1 as "c3_record"), c4 1024^3 @ 2 mm Z-slab sharded over the N
+GPUs (default at N>1), c5 1280x720 2048^3 @ 2 mm.
+
 Multi-GPU (`torchrun --nproc-per-node N`), one process per GPU:
-  --mode replicas (default for N > 1): every rank runs an independent
-      KinectFusion stream on its own camera trajectory (weak scaling, no
-      collective on the data path); value = frames of all ranks / max wall time.
-  --mode slab: ONE stream whose volume is Z-slab sharded over the N ranks
-      (kfx_create_slab + RCCL combine; strong scaling); value =
-      frames of the stream / max wall time.
-  With --mode replicas and N > 1 the JSON line also carries "zslab": the same
-  C2 stream Z-slab sharded over the N ranks, timed after the main measurement.
+  --mode slab (default for N > 1): ONE stream whose volume is Z-slab sharded
+      over the N ranks (kfx_create_slab + RCCL combine; strong
+      scaling); value = frames of the stream / max wall time; "per_rank" holds
+      every rank's ICP / integrate / raycast / combine ms.  --icp allreduce
+      shards the ICP sums too.  Independent replica streams are timed first
+      ("replicas"); if the slab stream fails or hangs, they become the line.
+  --mode replicas: every rank runs an independent stream (weak scaling, no
+      collective on the data path); value = frames of all ranks / max time.
 
 The JSON line also carries:
   stage_ms      per-stage device ms (HIP events on the pipeline stream)
@@ -49,11 +54,14 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=300)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--dims", type=int, default=512)
-    ap.add_argument("--range", type=float, default=2.048)
-    ap.add_argument("--width", type=int, default=640)
-    ap.add_argument("--height", type=int, default=480)
-    ap.add_argument("--unique", type=int, default=48, help="distinct frames rendered (played ping-pong)")
+    ap.add_argument("--config", choices=["auto", "c2", "c3", "c4", "c5"], default="auto",
+                    help="BASELINE config (auto: c2 at N=1, c4 at N>1)")
+    ap.add_argument("--dims", type=int, default=None, help="override the config's volume dims")
+    ap.add_argument("--range", type=float, default=None, help="override the config's volume range (m)")
+    ap.add_argument("--width", type=int, default=None)
+    ap.add_argument("--height", type=int, default=None)
+    ap.add_argument("--unique", type=int, default=0,
+                    help="distinct frames rendered, played ping-pong (0: 48, 16 above 640x480)")
     ap.add_argument("--profile-frames", type=int, default=20)
     ap.add_argument("--cpu-frames", type=int, default=8, help="oracle frames timed for cpu_baseline (0 = skip)")
     ap.add_argument("--host-frames", type=int, default=200,
@@ -68,9 +76,15 @@ def parse():
                     help="time kernels on every k-th timed frame with HIP events (0 = off)")
     ap.add_argument("--no-overlap", action="store_true",
                     help="single-stream frames (no preprocess/ICP overlap across frames)")
-    ap.add_argument("--mode", choices=["auto", "replicas", "slab"], default="auto")
-    ap.add_argument("--zslab", type=int, default=1, help="with replicas at N>1: also time the Z-slab stream")
-    ap.add_argument("--zslab-timeout", type=float, default=240.0)
+    ap.add_argument("--mode", choices=["auto", "single", "replicas", "slab"], default="auto",
+                    help="auto: single at N=1, slab at N>1")
+    ap.add_argument("--icp", choices=["replicated", "allreduce"], default="replicated",
+                    help="slab mode: every rank runs the full ICP, or its band with the partials all-reduced")
+    ap.add_argument("--replicas", type=int, default=1,
+                    help="slab mode at N>1: time independent replica streams first (the fallback line)")
+    ap.add_argument("--zslab-timeout", type=float, default=300.0)
+    ap.add_argument("--c3-frames", type=int, default=20,
+                    help="N=1, C2: timed frames of the C3 record (1024^3 @ 2 mm, same frames; 0 = skip)")
     return ap.parse_args()
 
 
@@ -177,6 +191,17 @@ class Dist:
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t.item())
 
+    def gather(self, row):
+        """Every rank's list of floats, in rank order (on every rank)."""
+        if self.dist is None:
+            return [list(row)]
+        import torch
+        dev = "cuda" if self.dist.get_backend() == "nccl" else "cpu"
+        t = torch.zeros(self.world, len(row), dtype=torch.float64, device=dev)
+        t[self.dist.get_rank()] = torch.tensor(row, dtype=torch.float64, device=dev)
+        self.dist.all_reduce(t)
+        return t.cpu().tolist()
+
     def bcast_bytes(self, b: bytes | None, src: int = 0) -> bytes:
         if self.dist is None:
             return b
@@ -207,84 +232,227 @@ def timed_frames(kf, order, lo, hi, D):
     return elapsed
 
 
-def zslab_stream(a, intr, params, D, rank, world, local):
-    """One C2 stream Z-slab sharded over the ranks (RCCL combine); frames/s."""
+CONFIGS = {  # BASELINE.json configs[1..4]: (width, height, volume dims, volume range m)
+    "c2": (640, 480, 512, 2.048),
+    "c3": (640, 480, 1024, 2.048),
+    "c4": (640, 480, 1024, 2.048),
+    "c5": (1280, 720, 2048, 4.096),
+}
+
+
+def resolve(a, world):
+    """Config and mode: C2 single GPU at N=1, the C4 Z-slab stream at N>1."""
+    name = a.config if a.config != "auto" else ("c2" if world == 1 else "c4")
+    W, H, n, L = CONFIGS[name]
+    over = [a.width, a.height, a.dims, a.range]
+    if any(v is not None for v in over):
+        W, H, n, L = [v if v is not None else d for v, d in zip(over, (W, H, n, L))]
+        name = "custom" if (W, H, n, L) != CONFIGS[name] else name
+    mode = a.mode if a.mode != "auto" else ("slab" if world > 1 else "single")
+    return name, W, H, n, L, mode
+
+
+def workload_text(name, W, H, n, L, mode, world, icp_ar):
+    t = (f"{name.upper()}: synthetic {W}x{H} depth+BGR, {n}^3 TSDF @ {1000 * L / n:.1f} mm, "
+         f"3-level ICP {{10,5,4}}, full pipeline per frame")
+    if mode == "slab":
+        t += (f"; one stream, volume Z-slab sharded over {world} GPUs, raycast combined per frame by RCCL "
+              f"(MIN keys + MAX {{Ts, normal}} payload), ICP " + ("sharded (27 int64 partials all-reduced per "
+                                                                   "iteration)" if icp_ar else "replicated"))
+    elif mode == "replicas":
+        t += f"; {world} independent streams, one per GPU (no collective)"
+    return t
+
+
+def run_stream(a, intr, params, frames, D, local, slab=None, icp_ar=False, timing=True):
+    """Create a context, warm up, time a.steps staged frames (W/K contract).
+    Returns the open context and the timed-region record; the caller closes it."""
     import kfx
-    from kfx import synth
     from kfx.abi import Intrinsics
-    bgr, dep, _ = synth.sequence(a.unique, intr, L=a.range, noise=True, traj_seed=7, dropout=0.005)
-    order = synth.ping_pong(a.unique, a.warmup + a.steps)
-    kf = kfx.KinectFusion(Intrinsics.from_any(intr), params, device=local, slab=(rank, world))
-    uid = D.bcast_bytes(kfx.comm_unique_id() if rank == 0 else None)
-    kf.comm_init(uid)
+    bgr, dep, order = frames
+    kf = kfx.KinectFusion(Intrinsics.from_any(intr), params, device=local, slab=slab)
+    if slab is not None:
+        kf.comm_init(D.bcast_bytes(kfx.comm_unique_id() if slab[0] == 0 else None))
+        kf.set_icp_allreduce(icp_ar)
     kf.set_graph_mode(not a.no_graph)
     kf.set_frame_overlap(not a.no_overlap)
-    kf.stage_frames(bgr, dep.astype(np.float32))
-    for i in range(a.warmup):
-        kf.pipeline_staged(order[i])
-    elapsed = timed_frames(kf, order, a.warmup, a.warmup + a.steps, D)
-    poses = kf.pose_record.shape[0]
-    zb, zn, o0, o1 = kf.slab_info()
-    kf.close()
-    return {"value": round(a.steps / elapsed, 3), "unit": "frames/s", "scaling": "strong",
-            "ms_per_step": round(1000.0 * elapsed / a.steps, 4), "n_gpus": world,
-            "slab_slices": o1 - o0, "stored_slices": zn, "poses": int(poses),
-            "note": "one C2 stream, volume Z-slab sharded over the ranks, raycast combined by "
-                    "RCCL all-reduce MIN(key)+MAX(bits) per frame, ICP replicated"}
-
-
-def main():
-    a = parse()
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    D = Dist(world, local)
-    mode = a.mode if a.mode != "auto" else ("replicas" if world > 1 else "single")
-
-    import kfx
-    from kfx import synth
-    from kfx.abi import Intrinsics, default_params
-
-    intr = intrinsics(a.width, a.height)
-    params = default_params(dims=a.dims, range_m=a.range)
-    W, H = intr.width, intr.height
-    slab_main = mode == "slab"
-    seed = 7 if (slab_main or world == 1) else 7 + rank
-    bgr, dep, gt = synth.sequence(a.unique, intr, L=a.range, noise=True, traj_seed=seed, dropout=0.005)
-    order = synth.ping_pong(a.unique, a.warmup + a.steps + a.profile_frames)
-
-    if slab_main:
-        kf = kfx.KinectFusion(Intrinsics.from_any(intr), params, device=local, slab=(rank, world))
-        kf.comm_init(D.bcast_bytes(kfx.comm_unique_id() if rank == 0 else None))
-    else:
-        kf = kfx.KinectFusion(Intrinsics.from_any(intr), params, device=local)
-    kf.set_graph_mode(not a.no_graph)
-    kf.set_frame_overlap(not a.no_overlap)
-    kf.stage_frames(bgr, dep.astype(np.float32))
-
+    kf.stage_frames(bgr, dep)
     for i in range(a.warmup):
         kf.pipeline_staged(order[i])
     kf.synchronize()
     n_before = kf.pose_record.shape[0]
-    # kernel durations over the timed region: every 8th frame bracketed by HIP
+    # kernel durations over the timed region: every k-th frame bracketed by HIP
     # events on the stream the kernels run on
-    if a.sample_every > 0:
+    if timing and a.sample_every > 0:
         kf.set_kernel_timing(a.sample_every, a.steps // a.sample_every + 2)
     elapsed = timed_frames(kf, order, a.warmup, a.warmup + a.steps, D)
-    ktime = kf.kernel_timing() if a.sample_every > 0 else None
+    ktime = kf.kernel_timing() if timing and a.sample_every > 0 else None
     kf.set_kernel_timing(0)
     tracked = kf.pose_record.shape[0] - n_before  # frames that appended a pose
     if tracked != a.steps:  # a dropped frame (tracking reset) invalidates the measurement
         raise SystemExit(f"bench: {a.steps - tracked} of {a.steps} timed frames were not tracked")
+    if ktime is not None and not ktime["samples"]:
+        ktime = None
+    return kf, {"elapsed": elapsed, "ktime": ktime, "tracked": tracked}
+
+
+def integrate_roofline(work, ms, W, H, ms_source, traffic=None, traffic_src=None):
+    """B_int = 8 N_upd + 8 N_col + 7 W H (N counted on the device)."""
+    b = 8 * work["updated"] + 8 * work["colored"] + 7 * W * H
+    achieved = b / (ms * 1e-3) / 1e9 if ms == ms and ms > 0 else 0.0
+    return {"kernel": "k_integrate", "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "traffic_source": traffic_src or "none: no PMC record of this workload and step count",
+            "algorithmic_bytes_per_launch": int(b), "avg_launch_ms": round(ms, 4), "launch_ms_source": ms_source}
+
+
+def round_ms(d):
+    return {k: round(v, 4) if isinstance(v, float) else v for k, v in d.items()} if d else None
+
+
+def single_record(a, name, intr, n, L, frames, D, local):
+    """A side measurement of one more single-GPU config (C3 at N=1): frames/s
+    over the same W/K contract, kernel ms, integrate roofline."""
+    from kfx.abi import default_params
+    params = default_params(dims=n, range_m=L)
+    kf, r = run_stream(a, intr, params, frames, D, local)
+    wk = kf.integrate_stats()
+    kf.close()
+    kt = r["ktime"]
+    W, H = intr.width, intr.height
+    return {"config": workload_text(name, W, H, n, L, "single", 1, False),
+            "value": round(a.steps / r["elapsed"], 3), "unit": "frames/s",
+            "ms_per_step": round(1000.0 * r["elapsed"] / a.steps, 4), "steps": a.steps, "warmup": a.warmup,
+            "tracked_frames": r["tracked"], "timed_region_kernel_ms": round_ms(kt), "integrate_voxels": wk,
+            "roofline": integrate_roofline(wk, kt["integrate"] if kt else float("nan"), W, H,
+                                           "timed region, HIP-event-bracketed frames")}
+
+
+def main():
+    a = parse()
+    # stdout carries only the JSON line: library banners (RCCL prints its
+    # version there) and any other output go to stderr
+    json_fd = os.dup(1)
+    sys.stdout.flush()
+    os.dup2(2, 1)
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    D = Dist(world, local)
+    name, W, H, n, L, mode = resolve(a, world)
+    icp_ar = a.icp == "allreduce"
+
+    import kfx
+    from kfx import synth
+    from kfx.abi import default_params
+
+    intr = intrinsics(W, H)
+    params = default_params(dims=n, range_m=L)
+    unique = a.unique if a.unique else (16 if W * H > 640 * 480 else 48)
+    # one camera trajectory for every rank: the slab ranks share one stream, and
+    # replica streams are independent whatever frames they replay
+    bgr, dep, _ = synth.sequence(unique, intr, L=L, noise=True, traj_seed=7, dropout=0.005)
+    dep = dep.astype(np.float32)
+    order = synth.ping_pong(unique, a.warmup + a.steps + a.profile_frames)
+    frames = (bgr, dep, order)
+
+    # N>1: the replica streams first (no collective), so that a failing or hung
+    # Z-slab stream still leaves a measured line
+    replicas = None
+    if mode == "slab" and world > 1 and a.replicas:
+        kf, r = run_stream(a, intr, params, frames, D, local, timing=False)
+        kf.close()
+        replicas = {"value": round(a.steps * world / r["elapsed"], 3), "unit": "frames/s", "scaling": "weak",
+                    "ms_per_step": round(1000.0 * r["elapsed"] / a.steps, 4),
+                    "config": workload_text(name, W, H, n, L, "replicas", world, False)}
+
+    lock = threading.Lock()
+    printed = []
+
+    def emit(line):
+        with lock:
+            if printed:
+                return
+            printed.append(1)
+            if rank == 0:
+                os.write(json_fd, (json.dumps(line) + "\n").encode())
+
+    def fallback(err):
+        """The replicas measurement as the line, the slab failure recorded."""
+        line = base_line(a, world, replicas["value"], float(replicas["ms_per_step"]), "weak",
+                         {"workload": replicas["config"], "parallelism": f"replicas x{world}"})
+        line["zslab"] = {"error": err}
+        return line
+
+    timer = None
+    if replicas is not None:
+        def on_timeout():
+            emit(fallback(f"timed out after {a.zslab_timeout:.0f} s"))
+            os._exit(0)
+        timer = threading.Timer(a.zslab_timeout, on_timeout)
+        timer.daemon = True
+        timer.start()
+    try:
+        out = measure_main(a, name, intr, params, frames, D, rank, world, local, mode, icp_ar)
+    except Exception as e:  # noqa: BLE001 -- a failed slab stream falls back to the replicas line
+        if replicas is None:
+            raise
+        out = fallback(f"{type(e).__name__}: {e}"[:300])
+    if timer is not None:
+        timer.cancel()
+    if replicas is not None and "zslab" not in out:
+        out["replicas"] = replicas
+    # N=1: the C3 record (1024^3 @ 2 mm on the same frames) beside the C2 line
+    if world == 1 and mode == "single" and a.c3_frames and name == "c2":
+        import copy
+        b = copy.copy(a)
+        b.steps = a.c3_frames
+        W3, H3, n3, L3 = CONFIGS["c3"]
+        f3 = (bgr, dep, synth.ping_pong(len(bgr), b.warmup + b.steps))
+        out["c3_record"] = single_record(b, "c3", intr, n3, L3, f3, D, local)
+    emit(out)
+    D.close()
+
+
+def base_line(a, world, value, ms, scaling, config):
+    return {
+        "metric": "frames/sec at 640×480, 512³ TSDF; per-stage ms (ICP/integrate/raycast)",
+        "value": round(value, 3),
+        "unit": "frames/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(ms, 4),
+        "higher_is_better": True,
+        "scaling": scaling,
+        "vs_baseline": round(value / (1000.0 / REF_MS_PER_FRAME), 3),
+        "dtype": "f32",
+        "data": "synthetic",
+        "config": config,
+    }
+
+
+def measure_main(a, name, intr, params, frames, D, rank, world, local, mode, icp_ar):
+    import kfx
+    from kfx import synth
+    from kfx.abi import default_params
+    bgr, dep, order = frames
+    W, H = intr.width, intr.height
+    n, L = params.volu_dims[0], params.volu_range[0]
+    slab = (rank, world) if mode == "slab" else None
+    kf, r = run_stream(a, intr, params, frames, D, local, slab=slab, icp_ar=icp_ar)
+    elapsed, ktime, tracked = r["elapsed"], r["ktime"], r["tracked"]
+    ms_source = (f"timed region, {ktime['samples']} HIP-event-bracketed frames" if ktime else "profiled frames")
 
     # host-input throughput (not `value`): the same frames from host memory
     # through kfx_pipeline_async (pinned ring, H2D overlapped with the previous
     # frame), PCIe included, f32 depth as the reference's pipeline() takes it
     host_in = None
-    if a.host_frames > 0:
-        hb = [np.ascontiguousarray(bgr[i]) for i in range(a.unique)]
-        hd = [np.ascontiguousarray(dep[i].astype(np.float32)) for i in range(a.unique)]
-        ho = synth.ping_pong(a.unique, a.host_frames)
+    if a.host_frames > 0 and mode == "single":
+        unique = len(bgr)
+        hb = [np.ascontiguousarray(bgr[i]) for i in range(unique)]
+        hd = [np.ascontiguousarray(dep[i]) for i in range(unique)]
+        ho = synth.ping_pong(unique, a.host_frames)
         kf.synchronize()
         D.barrier()
         t0 = time.perf_counter()
@@ -292,145 +460,109 @@ def main():
             kf.pipeline_async(hb[i], hd[i])
         st_h = kf.synchronize()
         dt_h = D.max(time.perf_counter() - t0)
-        host_in = {"value": round(len(ho) * (world if not slab_main else 1) / dt_h, 3), "unit": "frames/s",
+        host_in = {"value": round(len(ho) * world / dt_h, 3), "unit": "frames/s",
                    "ms_per_step": round(1000.0 * dt_h / len(ho), 4), "frames": len(ho),
                    "status": "ok" if st_h == kfx.KFX_OK else "tracking lost",
                    "bytes_per_frame_h2d": W * H * 7,
                    "path": "kfx_pipeline_async: host frame -> pinned 4-slot ring -> H2D on a copy stream "
                            "overlapped with the previous frame; f32 depth mm + BGR8"}
 
-    # per-stage device ms + integrate roofline on further frames (profiled, eager)
-    kf.set_profiling(True)
+    # per-stage device ms on further frames (profiled, eager; single volume)
     stages = {k: [] for k in ("preprocess", "icp", "integrate", "raycast", "total")}
-    int_bytes, int_ms, int_work = [], [], []
-    for i in range(a.warmup + a.steps, a.warmup + a.steps + a.profile_frames):
-        kf.pipeline_staged(order[i])
-        ms = kf.stage_ms()
-        for k in stages:
-            stages[k].append(ms[k])
-        wk = kf.integrate_stats()
-        nu, nc = wk["updated"], wk["colored"]
-        int_work.append(wk)
-        int_bytes.append(8 * nu + 8 * nc + 7 * W * H)
-        int_ms.append(ms["integrate"])
-    kf.set_profiling(False)
-    ray_work = kf.raycast_stats() if a.profile_frames else None
+    int_ms, int_work = [], []
+    nprof = a.profile_frames if mode != "slab" else 0
+    if nprof:
+        kf.set_profiling(True)
+        for i in range(a.warmup + a.steps, a.warmup + a.steps + nprof):
+            kf.pipeline_staged(order[i])
+            ms = kf.stage_ms()
+            for k in stages:
+                stages[k].append(ms[k])
+            int_work.append(kf.integrate_stats())
+            int_ms.append(ms["integrate"])
+        kf.set_profiling(False)
+    else:
+        int_work.append(kf.integrate_stats())  # the last timed frame's integrate work
+    ray_work = kf.raycast_stats() if nprof else None
+    zb, zn, o0, o1 = kf.slab_info()
     kf.synchronize()
     kf.close()
-    ray_ms = float(ktime["raycast"]) if ktime and ktime["samples"] > 0 else (
-        float(statistics.median(stages["raycast"])) if stages["raycast"] else float("nan"))
-    stage_med = {k: round(statistics.median(v), 4) for k, v in stages.items()} if a.profile_frames else {}
-    avg_bytes = float(np.mean(int_bytes)) if int_bytes else 0.0
+    stage_med = {k: round(statistics.median(v), 4) for k, v in stages.items()} if nprof else {}
+    work = {k: int(np.mean([w[k] for w in int_work])) for k in int_work[0]}
     # the integrate launch duration of the roofline: the HIP-event samples of
     # the timed region (fallback: the profiled frames after it)
-    if ktime and ktime["samples"] > 0:
-        avg_ms, ms_source = float(ktime["integrate"]), f"timed region, {ktime['samples']} event-bracketed frames"
+    if ktime:
+        int_launch_ms = float(ktime["integrate"])
     else:
-        avg_ms, ms_source = (float(np.mean(int_ms)) if int_ms else float("nan")), "profiled frames"
-    achieved = avg_bytes / (avg_ms * 1e-3) / 1e9 if avg_ms == avg_ms else 0.0
+        int_launch_ms = float(np.mean(int_ms)) if int_ms else float("nan")
+    ray_ms = float(ktime["raycast"]) if ktime else (
+        float(statistics.median(stages["raycast"])) if stages["raycast"] else float("nan"))
+
+    # per-rank kernel ms and integrate work (slab ranks integrate different slabs)
+    kt = ktime or {}
+    row = [kt.get("icp", float("nan")), kt.get("integrate", float("nan")), kt.get("raycast_local", float("nan")),
+           kt.get("combine", float("nan")), float(kt.get("samples", 0)), float(work["updated"]),
+           float(work["colored"]), float(o1 - o0), float(zn)]
+    rows = D.gather(row)
+    per_rank = [{"rank": k, "icp_ms": round(x[0], 4), "integrate_ms": round(x[1], 4),
+                 "raycast_ms": round(x[2], 4), "combine_ms": round(x[3], 4), "samples": int(x[4]),
+                 "integrate_updated": int(x[5]), "integrate_colored": int(x[6]), "owned_slices": int(x[7]),
+                 "stored_slices": int(x[8])} for k, x in enumerate(rows)]
+
     # HBM traffic of the integrate launch from a rocprofv3 FETCH_SIZE/WRITE_SIZE
     # record (tools/prof.sh), attached only when that record was measured on
     # this workload with the same step counts (the same saturation regime)
-    traffic, traffic_src = None, "none: no PMC record of this workload and step count"
+    traffic, traffic_src = None, None
     try:
         rec = json.load(open(a.traffic))
-        if (not slab_main and rec.get("workload") == [a.dims, W, H] and rec.get("steps") == a.steps
+        if (mode == "single" and rec.get("workload") == [n, W, H] and rec.get("steps") == a.steps
                 and rec.get("warmup") == a.warmup):
             traffic = rec.get("hbm_bytes_per_launch")
             traffic_src = f"{os.path.relpath(a.traffic, ROOT)}: {rec.get('command')} ({rec.get('regime')})"
     except (OSError, ValueError):
         pass
+    if mode == "slab":
+        # the critical path is the slowest rank's integrate
+        k = max(range(len(per_rank)), key=lambda q: per_rank[q]["integrate_ms"])
+        pr = per_rank[k]
+        roof = integrate_roofline({"updated": pr["integrate_updated"], "colored": pr["integrate_colored"]},
+                                  pr["integrate_ms"], W, H, ms_source + f", slowest rank ({k})")
+    else:
+        roof = integrate_roofline(work, int_launch_ms, W, H, ms_source, traffic, traffic_src)
 
     cpu = c1 = None
     if rank == 0 and world == 1 and a.cpu_frames > 0:
-        cpu = cpu_baseline(intr, params, bgr, dep, synth.ping_pong(a.unique, a.cpu_frames + 1), a.cpu_frames)
+        cpu = cpu_baseline(intr, params, bgr, dep, synth.ping_pong(len(bgr), a.cpu_frames + 1), a.cpu_frames)
     if rank == 0 and world == 1 and a.c1_frames > 0 and (W, H) == (640, 480):
         # BASELINE C1: 128^3 TSDF (16 mm) on the same 640x480 frames, serial oracle
-        c1 = cpu_baseline(intr, default_params(dims=128, range_m=a.range), bgr, dep,
-                          synth.ping_pong(a.unique, a.c1_frames + 1), a.c1_frames)
+        c1 = cpu_baseline(intr, default_params(dims=128, range_m=L), bgr, dep,
+                          synth.ping_pong(len(bgr), a.c1_frames + 1), a.c1_frames)
         c1["config"] = "C1: 128^3 TSDF @ 16 mm, 640x480 synthetic frames (the bundled dataset is absent)"
 
-    frames = a.steps if slab_main else a.steps * world
-    value = frames / elapsed
-    out = {
-        "metric": "frames/sec at 640×480, 512³ TSDF; per-stage ms (ICP/integrate/raycast)",
-        "value": round(value, 3),
-        "unit": "frames/s",
-        "n_gpus": world,
-        "steps": a.steps,
-        "warmup": a.warmup,
-        "ms_per_step": round(1000.0 * elapsed / a.steps, 4),
-        "higher_is_better": True,
-        "scaling": "strong" if slab_main else "weak",
-        "vs_baseline": round(value / (1000.0 / REF_MS_PER_FRAME), 3),
-        "dtype": "f32",
-        "data": "synthetic",
-        "config": {
-            "workload": f"C2: synthetic {W}x{H} depth+BGR, {a.dims}^3 TSDF @ "
-                        f"{1000 * a.range / a.dims:.1f} mm, 3-level ICP {{10,5,4}}, full pipeline per frame",
-            "width": W, "height": H, "volume_dims": a.dims, "volume_range_m": a.range,
-            "frames_unique": a.unique, "graph": not a.no_graph, "overlap": not a.no_overlap,
-            "parallelism": (f"zslab x{world}" if slab_main else
-                            (f"replicas x{world} (independent streams)" if world > 1 else "single")),
-            "tracked_frames": int(tracked),
-            "reference_ms_per_frame": REF_MS_PER_FRAME,
-        },
+    frames_done = a.steps * (world if mode == "replicas" else 1)
+    value = frames_done / elapsed
+    out = base_line(a, world, value, 1000.0 * elapsed / a.steps, "strong" if mode == "slab" else "weak", {
+        "workload": workload_text(name, W, H, n, L, mode, world, icp_ar),
+        "width": W, "height": H, "volume_dims": n, "volume_range_m": L,
+        "frames_unique": len(bgr), "graph": not a.no_graph, "overlap": not a.no_overlap,
+        "parallelism": (f"zslab x{world}" + (" + icp allreduce" if icp_ar else "") if mode == "slab" else
+                        (f"replicas x{world} (independent streams)" if world > 1 else "single")),
+        "tracked_frames": int(tracked),
+        "reference_ms_per_frame": REF_MS_PER_FRAME,
+    })
+    out.update({
         "stage_ms": stage_med,
-        "timed_region_kernel_ms": ({k: round(v, 4) if isinstance(v, float) else v for k, v in ktime.items()}
-                                   if ktime else None),
-        "integrate_voxels": ({k: int(np.mean([w[k] for w in int_work])) for k in int_work[0]}
-                             if int_work else None),
+        "timed_region_kernel_ms": round_ms(ktime),
+        "per_rank": per_rank if world > 1 else None,
+        "integrate_voxels": work,
         "raycast_work": ray_work,
-        "roofline": {
-            "kernel": "k_integrate",
-            "bound": "hbm",
-            "achieved": round(achieved, 1),
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": traffic,
-            "traffic_source": traffic_src,
-            "algorithmic_bytes_per_launch": int(avg_bytes),
-            "avg_launch_ms": round(avg_ms, 4),
-            "launch_ms_source": ms_source,
-        },
+        "roofline": roof,
         "roofline_raycast": raycast_roofline(ray_work, ray_ms, W, H, ms_source),
         "host_input": host_in,
         "cpu_baseline": cpu,
         "c1_record": c1,
-    }
-
-    if mode == "replicas" and a.zslab:
-        # the main measurement is complete: a failure or hang in the Z-slab
-        # side measurement must not lose it
-        lock = threading.Lock()
-        printed = []
-
-        def emit(extra):
-            with lock:
-                if printed:
-                    return
-                printed.append(1)
-                if rank == 0:
-                    out["zslab"] = extra
-                    print(json.dumps(out), flush=True)
-
-        def on_timeout():
-            emit({"error": f"timed out after {a.zslab_timeout:.0f} s"})
-            os._exit(0)
-
-        timer = threading.Timer(a.zslab_timeout, on_timeout)
-        timer.daemon = True
-        timer.start()
-        try:
-            extra = zslab_stream(a, intr, params, D, rank, world, local)
-        except Exception as e:  # noqa: BLE001 — reported in the JSON line
-            extra = {"error": f"{type(e).__name__}: {e}"[:300]}
-        timer.cancel()
-        emit(extra)
-    elif rank == 0:
-        print(json.dumps(out), flush=True)
-    D.close()
+    })
+    return out
 
 
 if __name__ == "__main__":

@@ -133,6 +133,11 @@ int kfx_set_frame_overlap(kfx_ctx *ctx, int enabled);
  * every = 0 turns sampling off. */
 int kfx_set_kernel_timing(kfx_ctx *ctx, int every, int max_samples);
 int kfx_get_kernel_timing(kfx_ctx *ctx, float out_ms[3], int *n_samples);
+/* The same samples split further: ICP, integrate, local raycast (+ resize on a
+ * single volume) and the slab combine (RCCL MIN/MAX all-reduces + expand +
+ * resize; 0 on a single volume).  out_ms[2] + out_ms[3] is
+ * kfx_get_kernel_timing's raycast figure.  Starts a new sample set too. */
+int kfx_get_kernel_timing_ex(kfx_ctx *ctx, float out_ms[4], int *n_samples);
 /* Run all ICP iterations of a frame as one persistent launch (default on; used
  * only when its grid fits co-resident on the device, else one launch per
  * iteration).  Returns 1 if the persistent kernel is usable on this context, 0

@@ -139,7 +139,7 @@ struct kfx_ctx {
   hipGraphExec_t graph[2] = {nullptr, nullptr};  // [u16 input], inputs in raw[0]/bgr
   std::vector<hipGraphExec_t> staged_graph;       // one per staged frame (reads it in place)
   const uint8_t *last_bgr = nullptr;              // colour the last frame integrated
-  hipEvent_t ev[5]{};
+  hipEvent_t ev[6]{};  // stage events; [5]: local raycast done (slab, before the combine)
   float stage_ms[5]{};
   int pending = 0;      // frames enqueued since the last host sync
   int known_poses = 1;  // n_poses at the last sync
@@ -234,6 +234,7 @@ int enqueue_combine(kfx_ctx *c);
 int enqueue_frame(kfx_ctx *c, FrameInput in, hipEvent_t *ev) {
   enqueue_pre(c, in, ev);
   int r = enqueue_track(c, in, ev, false);
+  if (ev) (void)hipEventRecord(ev[5], c->stream);
   if (!r && c->slab) r = enqueue_combine(c);
   if (ev) (void)hipEventRecord(ev[4], c->stream);
   return r;
@@ -381,6 +382,7 @@ int enqueue_frame_overlap(kfx_ctx *c, FrameInput in, hipEvent_t *ev) {
   HIPCHK(hipStreamWaitEvent(c->stream, c->ev_prep, 0));
   if (ev) HIPCHK(hipEventRecord(ev[1], c->stream));
   int r = enqueue_track(c, in, ev, true);
+  if (ev) HIPCHK(hipEventRecord(ev[5], c->stream));
   if (!r && c->slab) r = enqueue_combine(c);
   if (ev) HIPCHK(hipEventRecord(ev[4], c->stream));
   HIPCHK(hipEventRecord(c->ev_free[p], c->stream));
@@ -467,8 +469,8 @@ int run_frame(kfx_ctx *c, FrameInput in, hipGraphExec_t *graph, bool overlap = f
   c->last_bgr = in.bgr;
   hipEvent_t *tev = nullptr;  // this frame's timing sample, if sampled
   if (c->timing_every > 0 && !c->profiling && c->frame_seq++ % c->timing_every == 0 &&
-      5 * (c->tnext + 1) <= c->tsets.size())
-    tev = &c->tsets[5 * c->tnext++];
+      6 * (c->tnext + 1) <= c->tsets.size())
+    tev = &c->tsets[6 * c->tnext++];
   if (overlap && c->overlap && !c->profiling) {
     if ((r = enqueue_frame_overlap(c, in, tev))) return r;
     HIPCHK(hipGetLastError());
@@ -948,29 +950,47 @@ int kfx_set_kernel_timing(kfx_ctx *c, int every, int max_samples) {
   c->frame_seq = 0;
   c->timing_every = every;
   if (every == 0) return KFX_OK;
-  c->tsets.assign(5 * (size_t)max_samples, nullptr);
+  c->tsets.assign(6 * (size_t)max_samples, nullptr);
   // timing-only events: no system-scope fence on record (a fence per event
   // cost ~6 us of GPU time each)
   for (hipEvent_t &e : c->tsets) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
   return KFX_OK;
 }
 
-int kfx_get_kernel_timing(kfx_ctx *c, float out_ms[3], int *n_samples) {
+int kfx_get_kernel_timing_ex(kfx_ctx *c, float out_ms[4], int *n_samples) {
   int r = check_ctx(c);
   if (r) return r;
   if (!out_ms) return set_err(KFX_ERR_ARG, "null out");
   HIPCHK(hipStreamSynchronize(c->stream));
-  double acc[3] = {0, 0, 0};
+  // sample events: [2] ICP done, [3] integrate done, [5] local raycast done,
+  // [4] frame done; [1] the frame's tracking starts
+  static const int kFrom[4] = {1, 2, 3, 5}, kTo[4] = {2, 3, 5, 4};
+  double acc[4] = {0, 0, 0, 0};
   for (size_t k = 0; k < c->tnext; ++k) {
-    for (int i = 0; i < 3; ++i) {
+    for (int i = 0; i < 4; ++i) {
       float ms = 0.f;
-      HIPCHK(hipEventElapsedTime(&ms, c->tsets[5 * k + 1 + i], c->tsets[5 * k + 2 + i]));
+      HIPCHK(hipEventElapsedTime(&ms, c->tsets[6 * k + kFrom[i]], c->tsets[6 * k + kTo[i]]));
       acc[i] += ms;
     }
   }
-  for (int i = 0; i < 3; ++i) out_ms[i] = c->tnext ? (float)(acc[i] / (double)c->tnext) : 0.f;
+  for (int i = 0; i < 4; ++i) out_ms[i] = c->tnext ? (float)(acc[i] / (double)c->tnext) : 0.f;
+  if (!c->slab) {  // a single volume's resize runs after the raycast event pair
+    out_ms[2] += out_ms[3];
+    out_ms[3] = 0.f;
+  }
   if (n_samples) *n_samples = (int)c->tnext;
   c->tnext = 0;
+  return KFX_OK;
+}
+
+int kfx_get_kernel_timing(kfx_ctx *c, float out_ms[3], int *n_samples) {
+  if (!out_ms) return set_err(KFX_ERR_ARG, "null out");
+  float m[4];
+  const int r = kfx_get_kernel_timing_ex(c, m, n_samples);
+  if (r) return r;
+  out_ms[0] = m[0];
+  out_ms[1] = m[1];
+  out_ms[2] = m[2] + m[3];
   return KFX_OK;
 }
 

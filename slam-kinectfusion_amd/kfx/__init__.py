@@ -29,7 +29,7 @@ LIB_PATH = os.environ.get("KFX_LIB_PATH") or os.path.join(_PKG, "lib", "libkfx.s
 EXPORTS = [
     "kfx_abi_version", "kfx_last_error", "kfx_default_params", "kfx_create", "kfx_destroy", "kfx_reset",
     "kfx_pipeline", "kfx_pipeline_u16", "kfx_stage_frames", "kfx_pipeline_staged", "kfx_synchronize",
-    "kfx_set_graph_mode", "kfx_set_frame_overlap", "kfx_set_kernel_timing", "kfx_get_kernel_timing", "kfx_set_icp_persistent", "kfx_get_icp_trace", "kfx_get_cur_camera_pose", "kfx_get_frame_count", "kfx_get_pose_record",
+    "kfx_set_graph_mode", "kfx_set_frame_overlap", "kfx_set_kernel_timing", "kfx_get_kernel_timing", "kfx_get_kernel_timing_ex", "kfx_set_icp_persistent", "kfx_get_icp_trace", "kfx_get_cur_camera_pose", "kfx_get_frame_count", "kfx_get_pose_record",
     "kfx_write_poses_txt", "kfx_get_frame_maps", "kfx_set_frame_maps", "kfx_download_tsdf",
     "kfx_upload_tsdf", "kfx_download_volume_soa", "kfx_stage_preprocess", "kfx_stage_icp_accumulate",
     "kfx_stage_icp", "kfx_stage_integrate", "kfx_stage_raycast", "kfx_set_profiling", "kfx_get_stage_ms",
@@ -79,6 +79,7 @@ def lib():
         "kfx_set_frame_overlap": ([vp, i], i),
         "kfx_set_kernel_timing": ([vp, i, i], i),
         "kfx_get_kernel_timing": ([vp, P(C.c_float), P(C.c_int)], i),
+        "kfx_get_kernel_timing_ex": ([vp, P(C.c_float), P(C.c_int)], i),
         "kfx_set_icp_persistent": ([vp, i], i),
         "kfx_get_icp_trace": ([vp, P(C.c_uint64), i], i),
         "kfx_get_cur_camera_pose": ([vp, P(Pose)], i),
@@ -369,10 +370,12 @@ class KinectFusion:
         _check(lib().kfx_set_kernel_timing(self._h, int(every), int(max_samples)), "kfx_set_kernel_timing")
 
     def kernel_timing(self) -> dict:
-        """Mean ms of ICP / integrate / raycast over the sampled frames (resets the samples)."""
-        a, n = (C.c_float * 3)(), C.c_int()
-        _check(lib().kfx_get_kernel_timing(self._h, a, C.byref(n)), "kfx_get_kernel_timing")
-        return {"icp": a[0], "integrate": a[1], "raycast": a[2], "samples": n.value}
+        """Mean ms of ICP / integrate / raycast (+ slab combine) over the sampled
+        frames, and of the local raycast and the combine apart (resets the samples)."""
+        a, n = (C.c_float * 4)(), C.c_int()
+        _check(lib().kfx_get_kernel_timing_ex(self._h, a, C.byref(n)), "kfx_get_kernel_timing_ex")
+        return {"icp": a[0], "integrate": a[1], "raycast": a[2] + a[3], "raycast_local": a[2],
+                "combine": a[3], "samples": n.value}
 
     def set_frame_overlap(self, on: bool):
         """Overlap staged frames' preprocess with the previous frame's tracking."""

@@ -1,0 +1,81 @@
+"""bench.py's host logic on CPU: config / mode resolution and the per-rank
+gather over gloo (world_size 2), the pieces of the N>1 line that run without a GPU."""
+import importlib.util
+import os
+import socket
+import sys
+import types
+
+import pytest
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def load_bench():
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def args(**kw):
+    base = dict(config="auto", width=None, height=None, dims=None, range=None, mode="auto")
+    base.update(kw)
+    return types.SimpleNamespace(**base)
+
+
+def test_resolve_defaults_follow_baseline_configs():
+    b = load_bench()
+    assert b.resolve(args(), 1) == ("c2", 640, 480, 512, 2.048, "single")
+    assert b.resolve(args(), 8) == ("c4", 640, 480, 1024, 2.048, "slab")
+    assert b.resolve(args(config="c5"), 8) == ("c5", 1280, 720, 2048, 4.096, "slab")
+    assert b.resolve(args(config="c3"), 1) == ("c3", 640, 480, 1024, 2.048, "single")
+    assert b.resolve(args(mode="replicas"), 4)[-1] == "replicas"
+    # an override that changes the geometry is no longer a named config
+    assert b.resolve(args(dims=256), 1)[:4] == ("custom", 640, 480, 256)
+    assert b.resolve(args(dims=512), 1)[0] == "c2"
+
+
+def test_workload_text_names_sharding():
+    b = load_bench()
+    t = b.workload_text("c4", 640, 480, 1024, 2.048, "slab", 8, True)
+    assert t.startswith("C4: synthetic 640x480") and "2.0 mm" in t and "8 GPUs" in t and "all-reduced" in t
+    assert "replicated" in b.workload_text("c4", 640, 480, 1024, 2.048, "slab", 2, False)
+    assert "independent" in b.workload_text("c2", 640, 480, 512, 2.048, "replicas", 2, False)
+
+
+def _gather_rank(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    sys.path.insert(0, ROOT)
+    b = load_bench()
+    D = b.Dist(world, rank)
+    rows = D.gather([float(rank), 10.0 + rank, 0.5])
+    mx = D.max(float(rank) + 0.25)
+    D.close()
+    q.put((rank, rows, mx))
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.timeout(120)
+def test_dist_gather_over_gloo():
+    world, port = 2, free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_gather_rank, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=100) for _ in range(world)]
+    for p in ps:
+        p.join(30)
+        assert p.exitcode == 0
+    for rank, rows, mx in res:
+        assert rows == [[0.0, 10.0, 0.5], [1.0, 11.0, 0.5]]
+        assert mx == 1.25

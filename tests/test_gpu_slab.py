@@ -153,12 +153,21 @@ def test_slab_rccl_single_rank_matches(graph, icp_ar, seq_qvga):
     _compare(single, [m])
     m.stage_frames(bgr, dep.astype(np.float32))
     single.stage_frames(bgr, dep.astype(np.float32))
+    # every other staged frame is an event-bracketed timing sample (eager launch)
+    m.set_kernel_timing(2, 16)
+    single.set_kernel_timing(2, 16)
     for k in range(len(dep)):
         m.pipeline_staged(k)
         single.pipeline_staged(k)
     m.synchronize()
     single.synchronize()
     _compare(single, [m])
+    km, ks = m.kernel_timing(), single.kernel_timing()
+    assert km["samples"] == ks["samples"] == (len(dep) + 1) // 2
+    for k in ("icp", "integrate", "raycast_local", "combine"):
+        assert km[k] > 0, k
+    assert ks["combine"] == 0 and ks["raycast"] == ks["raycast_local"] > 0
+    assert abs(km["raycast"] - km["raycast_local"] - km["combine"]) < 1e-3
     m.close()
     single.close()
 
