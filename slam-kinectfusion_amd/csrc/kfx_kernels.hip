@@ -1034,14 +1034,16 @@ __device__ void frame_bookkeeping(DevState *st, DevPose *log, int kind, const De
 // per column (frustum + max depth, computed in double with margins) skips the
 // projection work outside it; the adds are still replayed there.
 
-// Solve alpha + beta*z >= 0 into [lo, hi].
-__device__ __forceinline__ void clip_lin(double alpha, double beta, double &lo, double &hi) {
-  if (beta > 0.0) {
-    lo = fmax(lo, -alpha / beta);
-  } else if (beta < 0.0) {
-    hi = fmin(hi, -alpha / beta);
-  } else if (alpha < 0.0) {
-    hi = -1.0;
+// Solve alpha + beta*z >= 0 into [lo, hi] (float, approximate quotient: the
+// callers widen the result by 2 slices, far above the float error; a NaN
+// quotient leaves the bound unchanged, an infinite one empties the interval).
+__device__ __forceinline__ void clip_lin(float alpha, float beta, float &lo, float &hi) {
+  if (beta > 0.f) {
+    lo = fmaxf(lo, -alpha * __builtin_amdgcn_rcpf(beta));
+  } else if (beta < 0.f) {
+    hi = fminf(hi, -alpha * __builtin_amdgcn_rcpf(beta));
+  } else if (alpha < 0.f) {
+    hi = -1.f;
   }
 }
 
@@ -1073,8 +1075,8 @@ __device__ __forceinline__ bool column_fast(f3 vc0, f3 zs, int Z) {
   bool ok = true;
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
-    const double bound = 2.0 * ((double)fabsf(c0[k]) + (double)(Z + 1) * (double)fabsf(s[k]));
-    ok = ok && bound <= 0x1p40;  // false for NaN / inf poses
+    const float bound = 2.f * (fabsf(c0[k]) + (float)(Z + 1) * fabsf(s[k]));  // < 2^40 / 1.01
+    ok = ok && bound <= 0x1.fcp39f;  // false for NaN / inf poses
     int e = 1000;
     if (c0[k] != 0.f) e = min(e, exp_of(c0[k]));
     if (s[k] != 0.f) e = min(e, exp_of(s[k]));
@@ -1233,26 +1235,28 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
   for (int i = 0; i < kDmaxShards; ++i) dm = max(dm, dmx[i]);
   const float dmax = __uint_as_float(dm);
   // global z = 1..Z-1 (tsdf_volume.cu:53), restricted to the stored slab
-  double lo = (double)max(1, v.zb), hi = (double)min(v.Z - 1, v.zb + v.zn - 1);
-  const double lo0 = lo, hi0 = hi;
+  // (the linear model vc0 + z zs of the accumulated vc, with 2 pixels and 2
+  // slices of margin: the float accumulation drifts < 0.1 voxel over a column)
+  const int lo0 = max(1, v.zb), hi0 = min(v.Z - 1, v.zb + v.zn - 1);
+  float lo = (float)lo0, hi = (float)hi0;  // lo only grows, hi only shrinks: finite unless emptied
   {
-    const double ax = vc.x, ay = vc.y, az = vc.z, sx = zs.x, sy = zs.y, sz = zs.z;
-    const double M = 2.0;  // pixels
-    clip_lin(az + 1e-3, sz, lo, hi);  // vc.z > 0
-    const double cxl = (double)g.cx + 0.5 + M, cxh = (double)g.w - 0.5 + M - (double)g.cx;
-    const double cyl = (double)g.cy + 0.5 + M, cyh = (double)g.h - 0.5 + M - (double)g.cy;
+    const float ax = vc.x, ay = vc.y, az = vc.z, sx = zs.x, sy = zs.y, sz = zs.z;
+    const float M = 2.f;  // pixels
+    clip_lin(az + 1e-3f, sz, lo, hi);  // vc.z > 0
+    const float cxl = g.cx + 0.5f + M, cxh = (float)g.w - 0.5f + M - g.cx;
+    const float cyl = g.cy + 0.5f + M, cyh = (float)g.h - 0.5f + M - g.cy;
     clip_lin(g.fx * ax + cxl * az, g.fx * sx + cxl * sz, lo, hi);
     clip_lin(cxh * az - g.fx * ax, cxh * sz - g.fx * sx, lo, hi);
     clip_lin(g.fy * ay + cyl * az, g.fy * sy + cyl * sz, lo, hi);
     clip_lin(cyh * az - g.fy * ay, cyh * sz - g.fy * sy, lo, hi);
-    const double zfar = ((double)dmax + (double)v.trunc) * 1.02 + 0.01;
+    const float zfar = (dmax + v.trunc) * 1.02f + 0.01f;
     clip_lin(zfar - az, -sz, lo, hi);
   }
   // this lane's candidate interval [zl, zh] (empty: zl > zh)
   int zl = INT_MAX, zh = INT_MIN;
   if (hi >= lo) {
-    zl = max((int)lo0, (int)floor(lo) - 2);
-    zh = min((int)hi0, (int)ceil(hi) + 2);
+    zl = max(lo0, (int)floorf(lo) - 2);
+    zh = min(hi0, (int)ceilf(hi) + 2);
     if (zh < zl) zl = INT_MAX, zh = INT_MIN;
   }
   // The wave takes a chunk of the UNION of its lanes' intervals, so all 64
@@ -2813,6 +2817,7 @@ void launch_integrate(hipStream_t s, VolView v, LevelGeom g0, const float2 *dl0,
     g_int_trace = trace_buf;
   }
   g_int_trace_waves = (int)(grd.x * grd.y * wpb);
+  (void)hipMemsetAsync(trace_buf, 0, sizeof(unsigned long long) * 4 * g_int_trace_waves, s);  // waves that exit early write none
   if (!counters) {
     hipLaunchKernelGGL((k_integrate<false, true>), grd, dim3(KFX_INT_BLOCK), 0, s, v, g0, dl0, bgr, st, log,
                        vpose, xpose, trace_buf);

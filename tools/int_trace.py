@@ -2,7 +2,7 @@
 """Per-wave timeline of k_integrate (debug library built with -DKFX_INT_TRACE):
 runs the C2 bench workload for a few frames, dumps the last integrate's wave
 records and prints the SIMD/CU occupancy over time and the wave-duration spread.
-usage: KFX_LIB_PATH=<trace lib> python3 tools/int_trace.py [out.npy]"""
+usage: KFX_LIB_PATH=<trace lib> python3 tools/int_trace.py [out.npy|-] [frames]"""
 import ctypes as C
 import os
 import sys
@@ -17,7 +17,7 @@ from kfx.abi import Intrinsics, default_params  # noqa: E402
 intr = synth.Intrinsics.vga()
 params = default_params(dims=512, range_m=2.048)
 bgr, dep, _ = synth.sequence(48, intr, L=2.048, noise=True, traj_seed=7, dropout=0.005)
-order = synth.ping_pong(48, 200)
+order = synth.ping_pong(48, int(sys.argv[2]) if len(sys.argv) > 2 else 200)
 kf = kfx.KinectFusion(Intrinsics.from_any(intr), params, device=0)
 kf.set_graph_mode(False)
 kf.set_frame_overlap(False)
@@ -48,6 +48,12 @@ print(f"SIMD last-wave end us: min {le.min():.1f} p10 {np.percentile(le, 10):.1f
 for q in (10, 25, 50, 75, 90, 100):
     t = np.percentile(en, q) / 1e3
     print(f"  {q:3d}% of waves done by {t:7.1f} us")
-if len(sys.argv) > 1:
+# resident waves over time (fraction of the 8192 slots of 8 waves x 1024 SIMDs)
+span = en.max()
+for k in range(20):
+    t = span * (k + 0.5) / 20
+    print(f"  t={t / 1e3:6.1f} us resident {((st <= t) & (en > t)).sum() / 8192:5.2f}")
+print(f"wave-time / (span x 8192 slots) = {dur.sum() / (span * 8192):.3f}")
+if len(sys.argv) > 1 and sys.argv[1] != "-":
     np.save(sys.argv[1], a)
 kf.close()
