@@ -28,7 +28,7 @@
 #define KFX_INT_OCC 8  // integrate: waves per SIMD the register budget is sized for
 #endif
 #ifndef KFX_INT_BLOCK
-#define KFX_INT_BLOCK 256  // integrate: threads per block (one 8x8 column tile per wave)
+#define KFX_INT_BLOCK 64  // integrate: threads per block (one wave = one 8x8 column tile: wave slots refill one at a time)
 #endif
 #ifndef KFX_INT_CHUNKR
 #define KFX_INT_CHUNKR 65  // integrate: z-chunk c of a column gets weight (r/100)^c
