@@ -140,9 +140,17 @@ int kfx_get_kernel_timing(kfx_ctx *ctx, float out_ms[3], int *n_samples);
 int kfx_get_kernel_timing_ex(kfx_ctx *ctx, float out_ms[4], int *n_samples);
 /* Run all ICP iterations of a frame as one persistent launch (default on; used
  * only when its grid fits co-resident on the device, else one launch per
- * iteration).  Returns 1 if the persistent kernel is usable on this context, 0
- * if not, <0 on error.  Results are identical either way. */
+ * iteration).  enabled: 0 = one launch per iteration, 1 = persistent (plain
+ * launch), 2 = persistent through a cooperative launch (co-residency
+ * guaranteed by the runtime, ~15 us slower per frame).  A context whose grid
+ * barrier watchdog fires (the frame reports KFX_ERR_HIP and is dropped with a
+ * volume reset) switches to mode 2 by itself.  Returns 1 if the persistent
+ * kernel is usable on this context, 0 if not, <0 on error.  Results are
+ * identical in every mode. */
 int kfx_set_icp_persistent(kfx_ctx *ctx, int enabled);
+/* Test hook: the next tracked frame's persistent-ICP barrier never completes
+ * (its watchdog fires after 0.2 s). */
+int kfx_debug_force_icp_stall(kfx_ctx *ctx);
 /* Slab contexts (SURVEY.md §8e alternative): instead of every rank running
  * the whole ICP (default), rank r accumulates the 27 products over its band
  * of each level's rows and the exact int64 partials are all-reduced (SUM)

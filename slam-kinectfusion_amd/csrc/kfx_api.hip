@@ -125,6 +125,7 @@ struct kfx_ctx {
   IcpPlan icp_plan{};
   bool icp_persistent = false;  // plan fits and its grid is co-resident
   bool icp_persistent_enabled = true;
+  bool icp_coop = false;  // cooperative launch of the persistent ICP (after a watchdog stall, or asked for)
   bool icp_sharded = false;  // slab ranks: ICP partials all-reduced (kfx_set_icp_allreduce)
   unsigned long long *counters = nullptr;
   float *xpose = nullptr;  // explicit stage poses (21 floats: pose R,t + Rinv)
@@ -330,7 +331,7 @@ int enqueue_track(kfx_ctx *c, FrameInput in, hipEvent_t *ev, bool begin) {
   if (c->icp_sharded && c->comm) {
     r = enqueue_icp_sharded(c, begin);
   } else if (c->icp_persistent && c->icp_persistent_enabled) {
-    launch_icp_track(s, c->icp_plan, c->st, c->icp_sync, begin ? 1 : 0);  // folds frame_begin in
+    launch_icp_track(s, c->icp_plan, c->st, c->icp_sync, begin ? 1 : 0, c->icp_coop);  // folds frame_begin in
   } else {
     if (begin) launch_frame_begin(s, c->st, nullptr, c->g[0]);
     for (int level = c->L - 1; level >= 0; --level) {
@@ -508,9 +509,18 @@ int check_status(kfx_ctx *c, const DevState &s) {
   const bool lost = s.fails != c->known_fails;
   c->known_fails = s.fails;
   if (s.icp_stalled) {
+    // the frame's ICP failed (its volume was reset, like a tracking loss);
+    // later frames launch the persistent ICP cooperatively, which guarantees
+    // the co-residency its grid barrier needs
     HIPCHK(hipMemsetAsync(c->icp_sync, 0, sizeof(IcpSync), c->stream));
-    const int r = write_field(c, offsetof(DevState, icp_stalled), 0);
-    return r ? r : set_err(KFX_ERR_HIP, "ICP grid barrier watchdog fired (grid not co-resident)");
+    int r = write_field(c, offsetof(DevState, icp_stalled), 0);
+    if (!r) r = write_field(c, offsetof(DevState, debug_stall), 0);
+    if (!c->icp_coop) {
+      c->icp_coop = true;
+      destroy_graphs(c);  // captured with the plain launch
+    }
+    return r ? r : set_err(KFX_ERR_HIP, "ICP grid barrier watchdog fired (grid not co-resident); "
+                                        "persistent ICP switched to cooperative launches");
   }
   return lost ? KFX_TRACKING_LOST : KFX_OK;
 }
@@ -1001,10 +1011,22 @@ int kfx_set_graph_mode(kfx_ctx *c, int enabled) {
 }
 
 int kfx_set_icp_persistent(kfx_ctx *c, int enabled) {
-  if (!c) return set_err(KFX_ERR_ARG, "null context");
-  if (c->icp_persistent_enabled != (enabled != 0)) destroy_graphs(c);
-  c->icp_persistent_enabled = enabled != 0;
+  int r = check_ctx(c);
+  if (r) return r;
+  if (enabled < 0 || enabled > 2) return set_err(KFX_ERR_ARG, "icp persistent mode must be 0, 1 or 2");
+  HIPCHK(hipStreamSynchronize(c->stream));
+  const bool on = enabled != 0, coop = enabled == 2;
+  if (c->icp_persistent_enabled != on || (on && c->icp_coop != coop)) destroy_graphs(c);
+  c->icp_persistent_enabled = on;
+  if (on) c->icp_coop = coop;
   return c->icp_persistent ? 1 : 0;
+}
+
+int kfx_debug_force_icp_stall(kfx_ctx *c) {
+  int r = check_ctx(c);
+  if (r) return r;
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return write_field(c, offsetof(DevState, debug_stall), 1);
 }
 
 int kfx_set_icp_allreduce(kfx_ctx *c, int enabled) {
@@ -1313,7 +1335,7 @@ int kfx_stage_icp(kfx_ctx *c, kfx_pose *out) {
   s.icp_pose = identity_pose();
   HIPCHK(hipMemcpyAsync(c->st, &s, sizeof(s), hipMemcpyHostToDevice, c->stream));
   if (c->icp_persistent && c->icp_persistent_enabled) {
-    launch_icp_track(c->stream, c->icp_plan, c->st, c->icp_sync);
+    launch_icp_track(c->stream, c->icp_plan, c->st, c->icp_sync, 0, c->icp_coop);
   } else {
     for (int level = c->L - 1; level >= 0; --level) {
       for (int it = 0; it < c->p.icp_iter_count[level]; ++it)
@@ -1326,9 +1348,15 @@ int kfx_stage_icp(kfx_ctx *c, kfx_pose *out) {
   if ((r = read_state(c, &s))) return r;
   if (s.icp_stalled) {
     HIPCHK(hipMemsetAsync(c->icp_sync, 0, sizeof(IcpSync), c->stream));
+    s0.debug_stall = 0;
     HIPCHK(hipMemcpyAsync(c->st, &s0, sizeof(s0), hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
-    return set_err(KFX_ERR_HIP, "ICP grid barrier watchdog fired (grid not co-resident)");
+    if (!c->icp_coop) {
+      c->icp_coop = true;
+      destroy_graphs(c);
+    }
+    return set_err(KFX_ERR_HIP, "ICP grid barrier watchdog fired (grid not co-resident); "
+                                "persistent ICP switched to cooperative launches");
   }
   if (out) *out = to_api(s.icp_pose);
   const int failed = s.icp_fail;

@@ -34,6 +34,7 @@ struct DevState {
   double x[6];          // last ICP increment
   int icp_stalled;      // persistent ICP barrier watchdog fired (reported as KFX_ERR_HIP)
   int fails;            // frames dropped by a tracking failure (reset) so far
+  int debug_stall;      // test hook: block 0 withholds its first ICP arrival (kfx_debug_force_icp_stall)
 };
 
 struct LevelGeom {
@@ -185,7 +186,9 @@ IcpPlan make_icp_plan(int levels, const LevelGeom *g, const int *iters, FrameVie
                       FrameView prev, float dist_thr, float angle_thr);
 bool icp_persistent_ok(const IcpPlan &pl, int device);  // grid co-resident + slots fit
 // begin: run the frame's frame_begin inside the launch (no separate kernel)
-void launch_icp_track(hipStream_t s, const IcpPlan &pl, DevState *st, IcpSync *sync, int begin = 0);
+// coop: cooperative launch (the runtime guarantees the grid co-resident)
+void launch_icp_track(hipStream_t s, const IcpPlan &pl, DevState *st, IcpSync *sync, int begin = 0,
+                      bool coop = false);
 // band / nbands: only rows [ye*band/nbands, ye*(band+1)/nbands) of the
 // floor-covered region (a slab rank's share in the sharded ICP mode)
 void launch_icp(hipStream_t s, const LevelGeom &g, const float *cv, const float *cn,

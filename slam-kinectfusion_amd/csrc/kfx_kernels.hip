@@ -729,6 +729,7 @@ __global__ __launch_bounds__(kIcpThreads, 2) void k_icp_track(IcpPlan pl, DevSta
   __shared__ DevPose spose;
   __shared__ int sfail, sstall;
   int fail = 0;
+  const bool withhold = blockIdx.x == 0 && st->debug_stall;  // test hook: never arrive at slot 0
   unsigned target = 0;
   int slot = 0;
   for (int l = pl.levels - 1; l >= 0 && !fail; --l) {
@@ -767,7 +768,7 @@ __global__ __launch_bounds__(kIcpThreads, 2) void k_icp_track(IcpPlan pl, DevSta
 #ifdef KFX_ICP_BLOCK_TRACE
           if (threadIdx.x == 0 && blockIdx.x < 512) sy->blk[slot][blockIdx.x][1] = wall_clock64();
 #endif
-          if (threadIdx.x == 0) {
+          if (threadIdx.x == 0 && !(withhold && slot == 0)) {
             // the last arriver releases the iteration: spinners poll 8 flag
             // copies instead of the contended arrival counter
             const unsigned n =
@@ -2749,7 +2750,19 @@ bool icp_persistent_ok(const IcpPlan &pl, int device) {
   return (long long)per_cu * cus >= pl.nblocks;
 }
 
-void launch_icp_track(hipStream_t s, const IcpPlan &pl, DevState *st, IcpSync *sync, int begin) {
+void launch_icp_track(hipStream_t s, const IcpPlan &pl, DevState *st, IcpSync *sync, int begin, bool coop) {
+  if (coop) {
+    // the runtime guarantees the grid co-resident (or fails the launch), so
+    // the grid barrier cannot wait on an unscheduled block (~15 us slower)
+    IcpPlan a0 = pl;
+    DevState *a1 = st;
+    IcpSync *a2 = sync;
+    int a3 = begin;
+    void *args[] = {&a0, &a1, &a2, &a3};
+    (void)hipLaunchCooperativeKernel(reinterpret_cast<const void *>(k_icp_track), dim3(pl.nblocks),
+                                     dim3(kIcpThreads), args, 0, s);
+    return;
+  }
   hipLaunchKernelGGL(k_icp_track, dim3(pl.nblocks), dim3(kIcpThreads), 0, s, pl, st, sync, begin);
 }
 

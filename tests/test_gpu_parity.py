@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 
 import oracle as O
-from kfx import KFX_FRAME_CUR, KFX_FRAME_PREV, KFX_OK, KFX_TRACKING_LOST, KinectFusion, synth
+from kfx import KFX_FRAME_CUR, KFX_FRAME_PREV, KFX_OK, KFX_TRACKING_LOST, KfxError, KinectFusion, synth
 from kfx.abi import Intrinsics, Pose, default_params
 
 pytestmark = pytest.mark.gpu
@@ -249,7 +249,7 @@ def test_pipeline_modes_and_inputs_identical(seq_qvga):
     intr = synth.Intrinsics.qvga()
     res = []
     for mode in ("graph", "eager", "profile", "u16", "staged", "staged_graph", "staged_mixed",
-                 "staged_per_iter", "icp_per_iter"):
+                 "staged_per_iter", "icp_per_iter", "icp_coop", "staged_coop"):
         kf, p = make(intr, dims=64)
         if mode == "staged_graph":  # staged frames without the two-stream overlap
             kf.set_frame_overlap(False)
@@ -258,9 +258,11 @@ def test_pipeline_modes_and_inputs_identical(seq_qvga):
         if mode in ("icp_per_iter", "staged_per_iter"):
             assert kf.set_icp_persistent(False)  # persistent path was the one in use
             kf.set_graph_mode(False)
+        if mode in ("icp_coop", "staged_coop"):  # cooperative launch of the persistent ICP
+            assert kf.set_icp_persistent(2)
         if mode == "profile":
             kf.set_profiling(True)
-        if mode in ("staged", "staged_graph", "staged_per_iter"):
+        if mode in ("staged", "staged_graph", "staged_per_iter", "staged_coop"):
             kf.stage_frames(bgr, dep.astype(np.float32))
             for k in range(len(dep)):
                 kf.pipeline_staged(k)
@@ -283,6 +285,41 @@ def test_pipeline_modes_and_inputs_identical(seq_qvga):
         assert np.array_equal(poses, res[0][0])
         for a, b in zip(vol, res[0][1]):
             assert np.array_equal(a, b)
+
+
+def test_icp_watchdog_stall_switches_to_cooperative_launch(seq_qvga):
+    """A persistent-ICP grid barrier that never completes (test hook: block 0
+    withholds its first arrival) fires the watchdog: that frame reports an
+    error and is dropped with a volume reset (as on a tracking loss); later
+    frames run the persistent ICP through a cooperative launch and track again,
+    with graphs and with staged overlapped frames."""
+    bgr, dep, gt = seq_qvga
+    intr = synth.Intrinsics.qvga()
+    kf, p = make(intr, dims=64)
+    assert kf.set_icp_persistent(True)
+    for k in range(3):
+        assert kf.pipeline(bgr[k], dep[k].astype(np.float32)) == KFX_OK
+    kf.debug_force_icp_stall()
+    with pytest.raises(KfxError, match="cooperative"):
+        kf.pipeline(bgr[3], dep[3].astype(np.float32))
+    n = kf.pose_record.shape[0]
+    for k in range(4, 7):
+        assert kf.pipeline(bgr[k], dep[k].astype(np.float32)) == KFX_OK
+    kf.stage_frames(bgr, dep.astype(np.float32))
+    for k in range(7, len(dep)):
+        kf.pipeline_staged(k)
+    assert kf.synchronize() == KFX_OK
+    # the stalled frame is an ICP failure (reset, like the reference's failed
+    # rigidTransform): the oracle with a failing (blank) frame 3 gives the same poses
+    I = Intrinsics.from_any(intr)
+    pipe = O.Pipeline(I, p)
+    for k in range(len(dep)):
+        d = dep[k].astype(np.float32) if k != 3 else np.zeros_like(dep[k], dtype=np.float32)
+        pipe.process(bgr[k], d)
+    op = pipe.poses()
+    assert kf.pose_record.shape == op.shape and n == 1
+    assert np.abs(kf.pose_record - op).max() <= 1e-6
+    kf.close()
 
 
 def test_tracking_failure_resets_like_reference(seq_qvga):
