@@ -771,6 +771,14 @@ static int create_impl(const kfx_intrinsics *intr, const kfx_params *params, int
   if ((r = dalloc(c, (void **)&c->vol.rgb, n * 4))) return fail(r);
   if ((r = dalloc(c, (void **)&c->vol.bocc, c->vol.bocc_bytes()))) return fail(r);
   if ((r = dalloc(c, (void **)&c->vol.socc, c->vol.socc_bytes()))) return fail(r);
+  {  // integrate dispatch order: identity until the first integrate has measured the intervals
+    const size_t tiles = (size_t)c->vol.tiles_x * c->vol.tiles_y, items = tiles * integrate_chunks(c->vol);
+    if ((r = dalloc(c, (void **)&c->vol.iwork, tiles * 4))) return fail(r);
+    if ((r = dalloc(c, (void **)&c->vol.iperm, items * 4))) return fail(r);
+    std::vector<unsigned> iota(items);
+    for (size_t i = 0; i < items; ++i) iota[i] = (unsigned)i;
+    HIPCHK(hipMemcpy(c->vol.iperm, iota.data(), items * 4, hipMemcpyHostToDevice));
+  }
   if ((r = dalloc(c, (void **)&c->st, sizeof(DevState)))) return fail(r);
   c->pose_cap = kInitialPoseCap;
   if ((r = dalloc(c, (void **)&c->pose_log, sizeof(DevPose) * (size_t)c->pose_cap))) return fail(r);

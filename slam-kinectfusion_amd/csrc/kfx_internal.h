@@ -106,6 +106,14 @@ struct VolView {
   uint32_t *socc;
   int bz0, nbz, bw;
   int sz0, nsz, sw, stx, sty;
+  // Integrate dispatch order (KFX_INT_LPT): iwork[tile] = the length of the
+  // tile's wave-uniform z interval in the last integrate, iperm[b] = the
+  // (chunk * tiles + tile) item block b runs (longest estimated first; any
+  // permutation gives the same volume), inchunk = chunks per tile.
+  unsigned *iwork;
+  unsigned *iperm;
+  int inchunk;
+  int iadapt;  // length-capped chunks + longest-first order (deep volumes), else geometric chunks
   __host__ __device__ size_t bocc_bytes() const { return (size_t)tiles_x * tiles_y * bw * 8; }
   __host__ __device__ size_t socc_bytes() const { return (size_t)stx * sty * sw * 4; }
   __host__ __device__ size_t local_voxels() const { return slice * (size_t)zn; }
@@ -259,6 +267,8 @@ void launch_export_soa(hipStream_t s, VolView v, int z0, int nz, int16_t *t, int
 // clear the occupancy maps and re-mark every brick holding a negative tsdf
 // (after a volume upload)
 void launch_occ_rebuild(hipStream_t s, VolView v);
+// z-chunks per column tile of k_integrate (the iperm item count is tiles x this)
+int integrate_chunks(const VolView &v);
 // owned-slice records of n (x, y) columns (device cols), column-major outputs
 void launch_gather_columns(hipStream_t s, VolView v, const int32_t *cols, int n, int16_t *t, int16_t *w,
                            uint32_t *c);

@@ -31,7 +31,22 @@
 #define KFX_INT_BLOCK 64  // integrate: threads per block (one wave = one 8x8 column tile: wave slots refill one at a time)
 #endif
 #ifndef KFX_INT_CHUNKR
-#define KFX_INT_CHUNKR 65  // integrate: z-chunk c of a column gets weight (r/100)^c
+#define KFX_INT_CHUNKR 65  // integrate, shallow volumes: chunk c of a tile's interval gets weight (r/100)^c
+#endif
+#ifndef KFX_INT_ADAPT_ZN
+// integrate chunking by volume (slab) depth zn, measured per config: for
+// ADAPT_ZN <= zn < ADAPT_ZN_END, length-capped chunks dispatched longest-first
+// by the last frame's intervals (C3: -12 % frame time); otherwise geometric
+// chunks in block order (C2 and C4 slabs: the capped chunks' replay and
+// prologue cost more than the tail they cut; C5's 2048-slice columns: 65536
+// tiles already balance, and capping them costs long replays)
+#define KFX_INT_ADAPT_ZN 1024
+#endif
+#ifndef KFX_INT_ADAPT_ZN_END
+#define KFX_INT_ADAPT_ZN_END 2048
+#endif
+#ifndef KFX_INT_NC
+#define KFX_INT_NC 4  // integrate, deep volumes: chunks of a full-length tile interval
 #endif
 #ifndef KFX_INT_MAXCHUNK
 #define KFX_INT_MAXCHUNK 8  // integrate: most z-chunks per column tile
@@ -1192,17 +1207,19 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
         gp = frame_pose(st, log, kind);
         s_pose = pose_mul(pose_inv(gp), vpose);  // tsdf_volume.cpp:50
       }
-      if (!kCount && blockIdx.x == 0 && blockIdx.y == 0) frame_bookkeeping(st, log, kind, gp);
+      if (!kCount && blockIdx.x == 0) frame_bookkeeping(st, log, kind, gp);
     }
   }
   __syncthreads();
 #ifdef KFX_INT_TRACE
   const unsigned long long t_start = wall_clock64();
 #endif
+  static_assert(KFX_INT_BLOCK == 64, "one wave per block: block b runs item iperm[b]");
   const int lane = threadIdx.x & 63;
-  const int tile = blockIdx.x * (KFX_INT_BLOCK / 64) + (threadIdx.x >> 6);
-  if (tile >= v.tiles_x * v.tiles_y) return;
-  const int chunk = blockIdx.y, nchunk = gridDim.y;
+  const int ntiles = v.tiles_x * v.tiles_y, nchunk = v.inchunk;
+  const unsigned item = v.iperm ? v.iperm[blockIdx.x] : blockIdx.x;  // chunk * tiles + tile
+  const int tile = (int)(item % (unsigned)ntiles), chunk = (int)(item / (unsigned)ntiles);
+  if (chunk >= nchunk) return;
   const int x = (tile % v.tiles_x) * 8 + (lane & 7);
   const int y = (tile / v.tiles_x) * 8 + (lane >> 3);
   const size_t base = (size_t)tile * v.tile_voxels() + lane;  // this column's (x, y, zb)
@@ -1270,10 +1287,20 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
     wl = min(wl, __shfl_xor(wl, off));
     wh = max(wh, __shfl_xor(wh, off));
   }
+  // the next frame's dispatch order (k_int_order) from this interval length
+  if (!kCount && chunk == 0 && lane == 0 && v.iwork) v.iwork[tile] = wh >= wl ? (unsigned)(wh - wl + 1) : 0u;
   if (wh < wl) return;  // wave-uniform
   int za, zb;
   {
     const int len = wh - wl + 1;
+    if (v.iadapt == 1) {
+      // length-capped: chunks of about zn / nchunk slices (a short interval
+      // takes fewer; the surplus items, ordered last, exit here)
+      const int ct = min(nchunk, max(1, (int)(((long long)len * nchunk + v.zn - 1) / v.zn)));
+      if (chunk >= ct) return;  // wave-uniform
+      za = wl + (int)((long long)len * chunk / ct);
+      zb = wl + (int)((long long)len * (chunk + 1) / ct) - 1;
+    } else {
 #if KFX_INT_CHUNKR == 100
     za = wl + (int)((long long)len * chunk / nchunk);
     zb = wl + (int)((long long)len * (chunk + 1) / nchunk) - 1;
@@ -1285,6 +1312,7 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
     za = wl + (int)((float)len * ((1.f - __powf(r, (float)chunk)) / den));
     zb = chunk + 1 == nchunk ? wh : wl + (int)((float)len * ((1.f - __powf(r, (float)(chunk + 1))) / den)) - 1;
 #endif
+    }
   }
   const int la = max(za, zl), lb = min(zb, zh);  // this lane's voxels of the chunk
   const bool live = lb >= la;
@@ -1460,7 +1488,7 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
   if (!kCount) occ_mark_wave(v, tile, nlo, nhi, lane);  // raycast skip maps
 #ifdef KFX_INT_TRACE
   if (!kCount && counters && lane == 0) {  // debug: per-wave timeline
-    unsigned long long *r = counters + 4 * ((size_t)(blockIdx.y * gridDim.x + blockIdx.x) * (KFX_INT_BLOCK / 64) + (threadIdx.x >> 6));
+    unsigned long long *r = counters + 4 * (size_t)blockIdx.x;
     r[0] = t_start;
     r[1] = wall_clock64();
     r[2] = ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |
@@ -2814,14 +2842,69 @@ void launch_group_sum_icp(hipStream_t s, DevState *const *st, int n) {
   hipLaunchKernelGGL(k_group_sum_icp, dim3(1), dim3(64), 0, s, g);
 }
 
+// VolView::iadapt: 1 = capped chunks longest-first, 0 = geometric chunks in block order
+static int integrate_mode(const VolView &v) {
+  return v.zn >= KFX_INT_ADAPT_ZN && v.zn < KFX_INT_ADAPT_ZN_END ? 1 : 0;
+}
+
+int integrate_chunks(const VolView &v) {
+  const int tiles = v.tiles_x * v.tiles_y;
+  if (integrate_mode(v) == 1) return std::max(1, std::min(KFX_INT_NC, v.zn / 32));  // chunks of >= 32 slices
+  // z-chunks so that >= KFX_INT_WAVES waves exist (16 per SIMD on 1024 SIMDs)
+  return std::max(1, std::min(KFX_INT_MAXCHUNK, (KFX_INT_WAVES + tiles - 1) / tiles));
+}
+
+// Longest-first dispatch order of k_integrate's (tile, chunk) items for the
+// next frame (VolView::iadapt): item c of tile t is one of ct(len_t) capped
+// chunks of len_t / ct slices, len_t = the tile's interval length in the last
+// integrate (frames are temporally coherent); surplus items (c >= ct) go last.
+// A counting sort into descending length buckets by one block; any
+// permutation integrates the same volume.
+constexpr int kOrderBuckets = 1024;
+__global__ __launch_bounds__(1024) void k_int_order(const unsigned *__restrict__ work, unsigned *__restrict__ perm,
+                                                    int tiles, int nchunk, int zn) {
+  __shared__ unsigned hist[kOrderBuckets];
+  __shared__ unsigned wsum[16];
+  const int t = threadIdx.x;
+  hist[t] = 0u;
+  __syncthreads();
+  const int n = tiles * nchunk;
+  const float scale = (float)(kOrderBuckets - 2) / ((float)zn / (float)nchunk + 2.f);
+  auto bucket = [&](int item) {
+    const unsigned len = work[item % tiles];
+    const int ct = min(nchunk, max(1, (int)(((long long)len * nchunk + zn - 1) / zn)));
+    if (len == 0u || item / tiles >= ct) return kOrderBuckets - 1;
+    return kOrderBuckets - 2 - min(kOrderBuckets - 2, (int)((float)len / (float)ct * scale));
+  };
+  for (int i = t; i < n; i += 1024) atomicAdd(&hist[bucket(i)], 1u);
+  __syncthreads();
+  // exclusive scan of the 1024 bucket counts: waves, then wave totals
+  const unsigned c = hist[t];
+  unsigned incl = c;
+  for (int off = 1; off < 64; off <<= 1) {
+    const unsigned u = __shfl_up(incl, off);
+    if ((t & 63) >= off) incl += u;
+  }
+  if ((t & 63) == 63) wsum[t >> 6] = incl;
+  __syncthreads();
+  unsigned base = 0;
+  for (int w = 0; w < (t >> 6); ++w) base += wsum[w];
+  __syncthreads();
+  hist[t] = base + incl - c;
+  __syncthreads();
+  for (int i = t; i < n; i += 1024) perm[atomicAdd(&hist[bucket(i)], 1u)] = (unsigned)i;
+}
+
 void launch_integrate(hipStream_t s, VolView v, LevelGeom g0, const float2 *dl0,
                       const uint8_t *bgr, DevState *st, DevPose *log, DevPose vpose,
                       const float *xpose, unsigned long long *counters) {
   const int tiles = v.tiles_x * v.tiles_y;
-  // z-chunks so that >= KFX_INT_WAVES waves exist (16 per SIMD on 1024 SIMDs)
-  const int nchunk = std::max(1, std::min(KFX_INT_MAXCHUNK, (KFX_INT_WAVES + tiles - 1) / tiles));
-  constexpr int wpb = KFX_INT_BLOCK / 64;  // waves (column tiles) per block
-  dim3 grd((tiles + wpb - 1) / wpb, nchunk);
+  const int nchunk = integrate_chunks(v);
+  v.inchunk = nchunk;
+  v.iadapt = integrate_mode(v);
+  if (!v.iadapt) v.iperm = nullptr, v.iwork = nullptr;  // geometric chunks in block order
+  if (counters) v.iwork = nullptr;  // the count-only pass leaves the order alone
+  dim3 grd(tiles * nchunk);  // one wave (block) per (tile, chunk) item
   const bool idx32 = v.local_voxels() < (1ull << 31);  // 32-bit tsdf/weight byte offsets
 #ifdef KFX_INT_TRACE
   static unsigned long long *trace_buf = nullptr;
@@ -2829,7 +2912,7 @@ void launch_integrate(hipStream_t s, VolView v, LevelGeom g0, const float2 *dl0,
     (void)hipMalloc(&trace_buf, sizeof(unsigned long long) * 4 * (1 << 20));
     g_int_trace = trace_buf;
   }
-  g_int_trace_waves = (int)(grd.x * grd.y * wpb);
+  g_int_trace_waves = (int)grd.x;
   (void)hipMemsetAsync(trace_buf, 0, sizeof(unsigned long long) * 4 * g_int_trace_waves, s);  // waves that exit early write none
   if (!counters) {
     hipLaunchKernelGGL((k_integrate<false, true>), grd, dim3(KFX_INT_BLOCK), 0, s, v, g0, dl0, bgr, st, log,
@@ -2846,6 +2929,8 @@ void launch_integrate(hipStream_t s, VolView v, LevelGeom g0, const float2 *dl0,
   else
     hipLaunchKernelGGL((k_integrate<false, false>), grd, dim3(KFX_INT_BLOCK), 0, s, v, g0, dl0, bgr, st, log,
                        vpose, xpose, counters);
+  if (!counters && v.iwork && v.iperm)
+    hipLaunchKernelGGL(k_int_order, dim3(1), dim3(1024), 0, s, v.iwork, v.iperm, tiles, nchunk, v.zn);
 }
 
 #ifdef KFX_RAY_TRACE
