@@ -248,6 +248,61 @@ __device__ void occ_mark(const VolView &v, int tx, int ty, int zlo, int zhi, int
                  min((zhi >> 5) + 1 - v.sz0, v.nsz - 1));
   }
 }
+// Brick-exact marking of a chunk (integrate): bit k of u = global brick gbs + k
+// (k < 62) holds a negative tsdf written by some lane of the wave (u is the
+// wave OR, uniform); dilated by one brick / super-brick and OR-ed into the 3x3
+// tiles / super tiles (lanes 0..8 / 9..17) like occ_mark.
+__device__ void occ_mark_bricks(const VolView &v, int tile, int gbs, unsigned long long u, int lane) {
+  if (!u) return;
+  const int tx = tile % v.tiles_x, ty = tile / v.tiles_x;
+  if (lane < 9) {
+    const int x = tx + lane % 3 - 1, y = ty + lane / 3 - 1;
+    if (x < 0 || y < 0 || x >= v.tiles_x || y >= v.tiles_y) return;
+    unsigned long long d = (u << 1) | u | (u << 2);  // bricks gbs-1 .. gbs+62, bit k+1 = brick gbs+k
+    int lb = gbs - 1 - v.bz0;                          // local brick of bit 0
+    if (lb < 0) {
+      d >>= -lb;
+      lb = 0;
+    }
+    unsigned long long *w = v.bocc + (size_t)(y * v.tiles_x + x) * v.bw;
+    const int w0 = lb >> 6, off = lb & 63;
+    auto put = [&](int wi, unsigned long long m) {
+      if (wi >= v.bw || !m) return;
+      const int hi = v.nbz - wi * 64;  // valid bits of this word
+      if (hi < 64) m &= (1ull << max(hi, 0)) - 1ull;
+      if (m && (w[wi] & m) != m) atomicOr(&w[wi], m);
+    };
+    put(w0, d << off);
+    if (off) put(w0 + 1, d >> (64 - off));
+  } else if (lane < 18) {
+    const int k = lane - 9;
+    const int x = (tx >> 2) + k % 3 - 1, y = (ty >> 2) + k / 3 - 1;
+    if (x < 0 || y < 0 || x >= v.stx || y >= v.sty) return;
+    // super-bricks (global brick >> 2) of the set bricks, dilated by one,
+    // relative to sbase = (gbs >> 2) - 1 (at most 18 bits)
+    const int a = gbs & 3;  // bit m of (vhi:vlo) = global brick (gbs & ~3) + m
+    const unsigned long long vlo = u << a, vhi = a ? u >> (64 - a) : 0ull;
+    unsigned sm = 0u;  // bit g = super-brick (gbs >> 2) + g holds a set brick
+#pragma unroll
+    for (int g = 0; g < 17; ++g) sm |= (((g < 16 ? vlo >> (4 * g) : vhi) & 0xFull) != 0ull ? 1u : 0u) << g;
+    sm = (sm << 1) | sm | (sm << 2);  // dilated, bit 0 = super-brick (gbs >> 2) - 1
+    int ls = (gbs >> 2) - 1 - v.sz0;
+    if (ls < 0) {
+      sm >>= -ls;
+      ls = 0;
+    }
+    uint32_t *w = v.socc + (size_t)(y * v.stx + x) * v.sw;
+    const int w0 = ls >> 5, off = ls & 31;
+    auto put = [&](int wi, unsigned m) {
+      if (wi >= v.sw || !m) return;
+      const int hi = v.nsz - wi * 32;
+      if (hi < 32) m &= (1u << max(hi, 0)) - 1u;
+      if (m && (w[wi] & m) != m) atomicOr(&w[wi], m);
+    };
+    put(w0, sm << off);
+    if (off) put(w0 + 1, sm >> (32 - off));
+  }
+}
 // Wave-wide [min lo, max hi] then occ_mark (all 64 lanes active).
 __device__ __forceinline__ void occ_mark_wave(const VolView &v, int tile, int lo, int hi, int lane) {
 #pragma unroll
@@ -1322,7 +1377,10 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
   const float thres_color = trunc / 2;
   // kCount: updated, coloured, visited, gathered voxels; wave batches
   unsigned cu = 0, cc = 0, cv = 0, cg = 0, cb = 0;
-  int nlo = INT_MAX, nhi = -1;  // global z range of the negative tsdf this lane wrote
+  // negative tsdf this lane wrote: bricks gbs .. gbs+61 as bits, beyond as a z range
+  const int gbs = za >> 3;
+  unsigned long long nbm = 0ull;
+  int nlo = INT_MAX, nhi = -1;
   int z = 1;
 #pragma unroll 8
   for (; z < za; ++z) vc = add(vc, zs);
@@ -1460,8 +1518,13 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
       int q = (int)(new_t * (float)kShortMax);
       q = max(-kShortMax, min(kShortMax, q));
       if (q < 0) {
-        nlo = min(nlo, z + j);
-        nhi = max(nhi, z + j);
+        const int k = ((z + j) >> 3) - gbs;
+        if (k < 62) {
+          nbm |= 1ull << k;
+        } else {
+          nlo = min(nlo, z + j);
+          nhi = max(nhi, z + j);
+        }
       }
       // saturated voxels (w = 64 at a tsdf fixed point) keep their values:
       // skipping those stores changes nothing and saves write bandwidth
@@ -1485,7 +1548,15 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
       }
     }
   }
-  if (!kCount) occ_mark_wave(v, tile, nlo, nhi, lane);  // raycast skip maps
+  if (!kCount) {  // raycast skip maps
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const unsigned lo = __shfl_xor((unsigned)nbm, off), hi = __shfl_xor((unsigned)(nbm >> 32), off);
+      nbm |= ((unsigned long long)hi << 32) | lo;
+    }
+    occ_mark_bricks(v, tile, gbs, nbm, lane);
+    occ_mark_wave(v, tile, nlo, nhi, lane);
+  }
 #ifdef KFX_INT_TRACE
   if (!kCount && counters && lane == 0) {  // debug: per-wave timeline
     unsigned long long *r = counters + 4 * (size_t)blockIdx.x;
