@@ -442,6 +442,7 @@ int ensure_pose_capacity(kfx_ctx *c, int more) {
   c->pose_log = nl;
   c->pose_cap = ncap;
   r = write_field(c, offsetof(DevState, pose_cap), ncap);
+  if (!r) r = write_field(c, offsetof(DevState, log), nl);
   if (r) return r;
   destroy_graphs(c);  // the integrate/raycast nodes hold the old pointer
   return KFX_OK;
@@ -609,6 +610,8 @@ int do_reset(kfx_ctx *c) {
   s.n_poses = 1;
   s.pose_cap = c->pose_cap;
   s.icp_pose = identity_pose();
+  s.log = c->pose_log;
+  s.back = identity_pose();
   const DevPose I = identity_pose();
   HIPCHK(hipMemcpyAsync(c->st, &s, sizeof(s), hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipMemcpyAsync(c->pose_log, &I, sizeof(I), hipMemcpyHostToDevice, c->stream));

@@ -35,6 +35,8 @@ struct DevState {
   int icp_stalled;      // persistent ICP barrier watchdog fired (reported as KFX_ERR_HIP)
   int fails;            // frames dropped by a tracking failure (reset) so far
   int debug_stall;      // test hook: block 0 withholds its first ICP arrival (kfx_debug_force_icp_stall)
+  DevPose *log;         // the device pose log (the host keeps it current)
+  DevPose back;         // log[n_poses - 1] at frame begin: the frame pose's base, one load away
 };
 
 struct LevelGeom {

@@ -204,6 +204,7 @@ __device__ __forceinline__ void frame_begin(DevState *st) {
   st->icp_fail = 0;
   st->n_base = st->n_poses;
   st->icp_pose = pose_identity();
+  st->back = st->log[st->n_poses - 1];
 }
 // the frame's max-depth shards live after the level-0 dl table (one per cur buffer)
 __device__ __forceinline__ unsigned *dmax_shards(const float2 *dl0, const LevelGeom &g0) {
@@ -1070,7 +1071,8 @@ __device__ __forceinline__ int frame_kind(const DevState *st) {
   return st->mode == MODE_BOOT ? 0 : (st->icp_fail ? 2 : 1);
 }
 __device__ __forceinline__ DevPose frame_pose(const DevState *st, const DevPose *log, int kind) {
-  const DevPose back = log[st->n_base - 1];
+  (void)log;  // st->back = log[n_base - 1], copied by frame_begin (one dependent load fewer)
+  const DevPose back = st->back;
   return kind == 0 ? back : pose_mul(back, st->icp_pose);
 }
 // pose_record push / reset (one thread of one block); only fields that no
