@@ -336,10 +336,10 @@ void kfo_pose_identity(kfx_pose *out) {
 
 // D: cos / sin of the Rodrigues angle (cv::Affine3f(rvec, t) uses std::cos /
 // std::sin).  For theta < 0.5 (every ICP increment in practice) their Taylor
-// polynomials in theta^2, Horner form with separately rounded double ops
-// (truncation < 1e-19 relative; within an ulp or two of the libm values, then
-// rounded to float): the same operations as the kernel's det_sincos, so GPU
-// and oracle agree bit for bit; larger angles use libm on both sides.
+// polynomials in theta^2, Horner form with fused multiply-adds (truncation
+// < 1e-19 relative; within an ulp or two of the libm values, then rounded to
+// float): the same operations as the kernel's det_sincos, so GPU and oracle
+// agree bit for bit; larger angles use libm on both sides.
 void kfo_sincos(double theta, double *s, double *c) {
   if (!(theta < 0.5)) {
     *s = std::sin(theta);
@@ -348,21 +348,21 @@ void kfo_sincos(double theta, double *s, double *c) {
   }
   const double x2 = theta * theta;
   double ps = -1.0 / 1307674368000.0;
-  ps = ps * x2 + 1.0 / 6227020800.0;
-  ps = ps * x2 + -1.0 / 39916800.0;
-  ps = ps * x2 + 1.0 / 362880.0;
-  ps = ps * x2 + -1.0 / 5040.0;
-  ps = ps * x2 + 1.0 / 120.0;
-  ps = ps * x2 + -1.0 / 6.0;
-  *s = theta + theta * (x2 * ps);
+  ps = std::fma(ps, x2, 1.0 / 6227020800.0);
+  ps = std::fma(ps, x2, -1.0 / 39916800.0);
+  ps = std::fma(ps, x2, 1.0 / 362880.0);
+  ps = std::fma(ps, x2, -1.0 / 5040.0);
+  ps = std::fma(ps, x2, 1.0 / 120.0);
+  ps = std::fma(ps, x2, -1.0 / 6.0);
+  *s = std::fma(theta, x2 * ps, theta);
   double pc = -1.0 / 87178291200.0;
-  pc = pc * x2 + 1.0 / 479001600.0;
-  pc = pc * x2 + -1.0 / 3628800.0;
-  pc = pc * x2 + 1.0 / 40320.0;
-  pc = pc * x2 + -1.0 / 720.0;
-  pc = pc * x2 + 1.0 / 24.0;
-  pc = pc * x2 + -0.5;
-  *c = 1.0 + x2 * pc;
+  pc = std::fma(pc, x2, 1.0 / 479001600.0);
+  pc = std::fma(pc, x2, -1.0 / 3628800.0);
+  pc = std::fma(pc, x2, 1.0 / 40320.0);
+  pc = std::fma(pc, x2, -1.0 / 720.0);
+  pc = std::fma(pc, x2, 1.0 / 24.0);
+  pc = std::fma(pc, x2, -0.5);
+  *c = std::fma(x2, pc, 1.0);
 }
 
 // icp_registration.cpp:33-42: A/b unpack (rigid_icp.cu:156-165), det check
@@ -381,21 +381,21 @@ int kfo_icp_update(const int64_t sums[27], kfx_pose *pose, double x_out[6]) {
         A[i][j] = A[j][i] = v;
     }
   // D: A = JᵀJ is symmetric: LDLᵀ factorisation (no pivoting, one division
-  // per column) instead of cv::solve(DECOMP_SVD); det = d0·…·d5 as
-  // cv::determinant's value of A.
+  // per column, fused multiply-subtracts) instead of cv::solve(DECOMP_SVD);
+  // det = d0·…·d5 as cv::determinant's value of A.
   double L[6][6] = {}, d[6], rd[6];
   for (int j = 0; j < 6; ++j) {
     double w[6];
     double dj = A[j][j];
     for (int k = 0; k < j; ++k) {
       w[k] = L[j][k] * d[k];
-      dj = dj - L[j][k] * w[k];
+      dj = std::fma(-L[j][k], w[k], dj);
     }
     d[j] = dj;
     rd[j] = 1.0 / dj;
     for (int i = j + 1; i < 6; ++i) {
       double s = A[i][j];
-      for (int k = 0; k < j; ++k) s = s - L[i][k] * w[k];
+      for (int k = 0; k < j; ++k) s = std::fma(-L[i][k], w[k], s);
       L[i][j] = s * rd[j];
     }
   }
@@ -405,12 +405,12 @@ int kfo_icp_update(const int64_t sums[27], kfx_pose *pose, double x_out[6]) {
   double y[6], x[6];
   for (int i = 0; i < 6; ++i) {  // L y = b
     double acc = b[i];
-    for (int k = 0; k < i; ++k) acc = acc - L[i][k] * y[k];
+    for (int k = 0; k < i; ++k) acc = std::fma(-L[i][k], y[k], acc);
     y[i] = acc;
   }
   for (int i = 5; i >= 0; --i) {  // Lᵀ x = D⁻¹ y
     double acc = y[i] * rd[i];
-    for (int k = i + 1; k < 6; ++k) acc = acc - L[k][i] * x[k];
+    for (int k = i + 1; k < 6; ++k) acc = std::fma(-L[k][i], x[k], acc);
     x[i] = acc;
   }
   if (x_out)

@@ -54,7 +54,7 @@ struct IcpPlan {
   int xe[kMaxLevels], npix[kMaxLevels], groups[kMaxLevels], iters[kMaxLevels];
   int ppl[kMaxLevels];  // pixels per lane at each level
   const float *cv[kMaxLevels], *cn[kMaxLevels], *pv[kMaxLevels], *pn[kMaxLevels];
-  float dist_thr, angle_thr;
+  float dist2_max, sine2_max;  // sqrt_le_bound of the distance / sine thresholds
 };
 
 // Device workspace of the persistent ICP kernel; zero between launches

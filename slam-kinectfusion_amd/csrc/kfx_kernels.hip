@@ -8,6 +8,8 @@
 // are bit-identical to the CPU oracle (oracle/kfx_oracle.cpp) on the same inputs.
 #include <algorithm>
 #include <climits>
+#include <cmath>
+#include <limits>
 #include <type_traits>
 
 #include "kfx_internal.h"
@@ -61,7 +63,7 @@ namespace {
 constexpr float kDivShortMax = 0.0000305185f;  // device_utils.cuh:6
 constexpr int kShortMax = 32767;               // device_utils.cuh:7
 constexpr int kMaxWeight = 64;                 // device_utils.cuh:5 (A10)
-constexpr float kFix = 4294967296.0f;          // ICP fixed point 2^32 (D)
+constexpr float kFixHalf = 65536.0f;           // ICP fixed point 2^32 (D) = 2^16 per factor of a product
 constexpr int kDmaxShards = 16;
 
 struct f3 {
@@ -518,6 +520,9 @@ __global__ __launch_bounds__(256) void k_preprocess_maps(BilatArgs a) {
 #define KFX_ICP_PIX 4
 #endif
 constexpr int kIcpPix = KFX_ICP_PIX;
+#ifndef KFX_RAY_N32
+#define KFX_RAY_N32 1  // raycast normals: 32-bit tile-column offsets + buffer loads (kIdx32 volumes)
+#endif
 #ifndef KFX_ICP_THREADS
 #define KFX_ICP_THREADS 256  // ICP: threads per block
 #endif
@@ -525,7 +530,9 @@ constexpr int kIcpThreads = KFX_ICP_THREADS;
 constexpr int kIcpWaves = kIcpThreads / 64;
 constexpr int kIcpBlockPix = kIcpThreads * kIcpPix;
 constexpr unsigned long long kIcpWatchdogTicks = 20000000ull;  // >= 0.2 s of s_memrealtime
-__device__ int icp_update(const long long *sums, DevPose &pose, double *xo);
+__device__ int icp_update(const double *a27, DevPose &pose, double *xo);
+// rigid_icp.cu:156-165's unpack of one int64 fixed-point sum (exact scaling)
+__device__ __forceinline__ double icp_sum_value(long long s) { return (double)s * (1.0 / 4294967296.0); }
 
 // Per-lane part of one ICP iteration: kIcpPix pixels whose current-frame
 // vertex/normal (n0, v0, validity ok0) are already in registers; gathers the
@@ -538,8 +545,8 @@ __device__ __forceinline__ void icp_lane(const LevelGeom &g, const DevPose &P,
                                          const f3 (&n0)[kIcpPix], const f3 (&v0)[kIcpPix],
                                          const bool (&ok0)[kIcpPix], int ppl,
                                          const float *__restrict__ pv,
-                                         const float *__restrict__ pn, float dist_thr,
-                                         float angle_thr, double (&acc)[27]) {
+                                         const float *__restrict__ pn, float dist2_max,
+                                         float sine2_max, double (&acc)[27]) {
   const f3 t = {P.t[0], P.t[1], P.t[2]};
 #pragma unroll
   for (int k = 0; k < 27; ++k) acc[k] = 0.0;
@@ -570,24 +577,29 @@ __device__ __forceinline__ void icp_lane(const LevelGeom &g, const DevPose &P,
 #pragma unroll
   for (int q = 0; q < kIcpPix; ++q) {
     if (!ok[q]) continue;
+    // rigid_icp.cu's sqrtf(|d|^2) <= dist_thr and sqrtf(|sa|^2) <= angle_thr,
+    // as one compare each: RN(sqrt(x)) is monotonic in x, so it is <= t exactly
+    // when x <= sqrt_le_bound(t) (host; NaN fails both forms)
     const f3 dd = sub(vcur[q], vpre[q]);
-    const float dist = sqrtf(dot(dd, dd));
-    if (!(dist <= dist_thr)) continue;
+    if (!(dot(dd, dd) <= dist2_max)) continue;
     const f3 ncur = rmul(P.R, n0[q]);
     const f3 sa = cross(ncur, npre[q]);
-    const float sine = sqrtf(dot(sa, sa));
-    if (!(sine <= angle_thr)) continue;
+    if (!(dot(sa, sa) <= sine2_max)) continue;
     const f3 c = cross(vcur[q], npre[q]);
     const float row[7] = {c.x,       c.y,       c.z, npre[q].x, npre[q].y,
                           npre[q].z, dot(npre[q], sub(vpre[q], vcur[q]))};
+    // rintf(RN(ra * rb) * 2^32) as rintf(RN(ra' * rb')) with x' = x * 2^16
+    // (exact power-of-two scalings of finite |x| < 2^7): equal whenever the
+    // product is normal, and when it is not (|ra * rb| < 2^-126) both round to
+    // a zero of the product's sign
+    float rs[7];
+#pragma unroll
+    for (int a = 0; a < 7; ++a) rs[a] = row[a] * kFixHalf;
     int s = 0;
 #pragma unroll
     for (int a = 0; a < 6; ++a)
 #pragma unroll
-      for (int b = a; b < 7; ++b) {
-        const float prod = row[a] * row[b];
-        acc[s++] += (double)rintf(prod * kFix);
-      }
+      for (int b = a; b < 7; ++b) acc[s++] += (double)rintf(rs[a] * rs[b]);
   }
 }
 
@@ -707,8 +719,8 @@ __global__ __launch_bounds__(kIcpThreads) void k_icp_acc(LevelGeom g, int xe, in
                                                  const float *__restrict__ cv,
                                                  const float *__restrict__ cn,
                                                  const float *__restrict__ pv,
-                                                 const float *__restrict__ pn, float dist_thr,
-                                                 float angle_thr, DevState *__restrict__ st,
+                                                 const float *__restrict__ pn, float dist2_max,
+                                                 float sine2_max, DevState *__restrict__ st,
                                                  unsigned long long *__restrict__ shards,
                                                  unsigned *__restrict__ ticket, int force,
                                                  int update) {
@@ -718,7 +730,7 @@ __global__ __launch_bounds__(kIcpThreads) void k_icp_acc(LevelGeom g, int xe, in
   bool ok[kIcpPix];
   icp_load_cur(g, xe, npix, blockIdx.x, kIcpPix, cv, cn, n0, v0, ok, p0);
   double acc[27];
-  icp_lane(g, P, n0, v0, ok, kIcpPix, pv, pn, dist_thr, angle_thr, acc);
+  icp_lane(g, P, n0, v0, ok, kIcpPix, pv, pn, dist2_max, sine2_max, acc);
   __shared__ IcpRed red;
   const long long bsum = icp_block_reduce(red, acc);
   // Cross-block sum + solve in the same launch: wave 0 adds the block's 27
@@ -739,7 +751,7 @@ __global__ __launch_bounds__(kIcpThreads) void k_icp_acc(LevelGeom g, int xe, in
   }
   __syncthreads();
   if (!last) return;
-  __shared__ long long sums[27];
+  __shared__ double sumd[27];
   // one read-and-clear per thread (a thread's atomics serialise)
   if (threadIdx.x < kIcpShards * 27)
     red.red2[threadIdx.x] = __longlong_as_double((long long)__hip_atomic_exchange(
@@ -750,14 +762,14 @@ __global__ __launch_bounds__(kIcpThreads) void k_icp_acc(LevelGeom g, int xe, in
     long long a = 0;
 #pragma unroll
     for (int sh = 0; sh < kIcpShards; ++sh) a += __double_as_longlong(red.red2[sh * 27 + threadIdx.x]);
-    sums[threadIdx.x] = a;
+    sumd[threadIdx.x] = icp_sum_value(a);
     st->sums[threadIdx.x] = a;
   }
   __syncthreads();
   if (threadIdx.x < 64 && update) {  // wave 0 solves
     DevPose p = st->icp_pose;
     double x[6];
-    const int f = icp_update(sums, p, x);
+    const int f = icp_update(sumd, p, x);
     if (threadIdx.x == 0) {
       if (f) {
         st->icp_fail = 1;
@@ -797,6 +809,7 @@ __global__ __launch_bounds__(kIcpThreads, 2) void k_icp_track(IcpPlan pl, DevSta
   }
   __shared__ IcpRed red;
   __shared__ long long sums[27];
+  __shared__ double sumd[27];  // the same sums unpacked (one conversion per thread, not per solver lane)
   __shared__ DevPose spose;
   __shared__ int sfail, sstall;
   int fail = 0;
@@ -821,7 +834,7 @@ __global__ __launch_bounds__(kIcpThreads, 2) void k_icp_track(IcpPlan pl, DevSta
 #endif
       if (mine) {
         double acc[27];
-        icp_lane(g, P, n0, v0, ok, pl.ppl[l], pl.pv[l], pl.pn[l], pl.dist_thr, pl.angle_thr, acc);
+        icp_lane(g, P, n0, v0, ok, pl.ppl[l], pl.pv[l], pl.pn[l], pl.dist2_max, pl.sine2_max, acc);
         if (tr && blockIdx.x == 0) sy->trace[slot][8] = wall_clock64() + (acc[3] == -1.5 ? 1 : 0);
         const long long bsum = icp_block_reduce(red, acc);
         if (tr && blockIdx.x == 0) sy->trace[slot][9] = wall_clock64() + (bsum == -7 ? 1 : 0);
@@ -878,13 +891,14 @@ __global__ __launch_bounds__(kIcpThreads, 2) void k_icp_track(IcpPlan pl, DevSta
 #pragma unroll
         for (int k = 0; k < kIcpShards; ++k) a += __double_as_longlong(red.red2[k * 27 + threadIdx.x]);
         sums[threadIdx.x] = a;
+        sumd[threadIdx.x] = icp_sum_value(a);
       }
       __syncthreads();
       if (tr && blockIdx.x == 0) sy->trace[slot][5] = wall_clock64();
       if (threadIdx.x < 64) {  // wave 0 solves (every block, identical result)
         DevPose p = P;
         double x[6];
-        int f = icp_update(sums, p, x);
+        int f = icp_update(sumd, p, x);
         if (tr && blockIdx.x == 0) sy->trace[slot][6] = __builtin_amdgcn_readfirstlane((int)x[0]) + wall_clock64();
         if (sstall) f = 1;  // a stalled block stops; the others stall at the next barrier
         if (threadIdx.x < 27 && blockIdx.x == 0) st->sums[threadIdx.x] = sums[threadIdx.x];
@@ -949,10 +963,11 @@ __device__ __forceinline__ double bcast(double v, int src) {
 // no cross-lane traffic on the critical path).  Each double operation is the
 // oracle's (kfo_icp_update) in the same order, so the result is
 // bit-identical.  (The earlier partial-pivot LU spent most of its ~3.4k
-// cycles on data-dependent row moves.)  sums: 27 int64 (any memory, read by
-// all lanes).
+// cycles on data-dependent row moves.)  a27: the 27 sums already unpacked by
+// icp_sum_value (any memory, read by all lanes; the unpack is done once per
+// value by 27 threads, not 27 times per solver lane).
 // D: cos / sin of the Rodrigues angle as the oracle's kfo_sincos (theta < 0.5:
-// Taylor polynomials in theta^2, separately rounded double ops; else ocml) —
+// Taylor polynomials in theta^2, Horner form with fused multiply-adds; else ocml) —
 // bit-identical to the oracle and far shorter than ocml's sincos.
 __device__ __forceinline__ void det_sincos(double theta, double *s, double *c) {
   if (!(theta < 0.5)) {  // wave-uniform
@@ -961,24 +976,24 @@ __device__ __forceinline__ void det_sincos(double theta, double *s, double *c) {
   }
   const double x2 = theta * theta;
   double ps = -1.0 / 1307674368000.0;
-  ps = ps * x2 + 1.0 / 6227020800.0;
-  ps = ps * x2 + -1.0 / 39916800.0;
-  ps = ps * x2 + 1.0 / 362880.0;
-  ps = ps * x2 + -1.0 / 5040.0;
-  ps = ps * x2 + 1.0 / 120.0;
-  ps = ps * x2 + -1.0 / 6.0;
-  *s = theta + theta * (x2 * ps);
+  ps = fma(ps, x2, 1.0 / 6227020800.0);
+  ps = fma(ps, x2, -1.0 / 39916800.0);
+  ps = fma(ps, x2, 1.0 / 362880.0);
+  ps = fma(ps, x2, -1.0 / 5040.0);
+  ps = fma(ps, x2, 1.0 / 120.0);
+  ps = fma(ps, x2, -1.0 / 6.0);
+  *s = fma(theta, x2 * ps, theta);
   double pc = -1.0 / 87178291200.0;
-  pc = pc * x2 + 1.0 / 479001600.0;
-  pc = pc * x2 + -1.0 / 3628800.0;
-  pc = pc * x2 + 1.0 / 40320.0;
-  pc = pc * x2 + -1.0 / 720.0;
-  pc = pc * x2 + 1.0 / 24.0;
-  pc = pc * x2 + -0.5;
-  *c = 1.0 + x2 * pc;
+  pc = fma(pc, x2, 1.0 / 479001600.0);
+  pc = fma(pc, x2, -1.0 / 3628800.0);
+  pc = fma(pc, x2, 1.0 / 40320.0);
+  pc = fma(pc, x2, -1.0 / 720.0);
+  pc = fma(pc, x2, 1.0 / 24.0);
+  pc = fma(pc, x2, -0.5);
+  *c = fma(x2, pc, 1.0);
 }
 
-__device__ int icp_update(const long long *sums, DevPose &pose, double *xo) {
+__device__ int icp_update(const double *a27, DevPose &pose, double *xo) {
   double A[6][7];  // column 6 = b
   {
     int q = 0;
@@ -986,13 +1001,14 @@ __device__ int icp_update(const long long *sums, DevPose &pose, double *xo) {
     for (int i = 0; i < 6; ++i)
 #pragma unroll
       for (int j = i; j < 7; ++j) {
-        const double v = (double)sums[q++] * (1.0 / 4294967296.0);
+        const double v = a27[q++];
         A[i][j] = v;
         if (j < 6) A[j][i] = v;
       }
   }
   // LDLᵀ of the symmetric A (no pivoting: no data-dependent register moves;
-  // one division per column), det = d0·…·d5
+  // one division per column; fused multiply-subtracts as the oracle's),
+  // det = d0·…·d5
   double L[6][6], d[6], rd[6];
 #pragma unroll
   for (int j = 0; j < 6; ++j) {
@@ -1001,7 +1017,7 @@ __device__ int icp_update(const long long *sums, DevPose &pose, double *xo) {
 #pragma unroll
     for (int k = 0; k < j; ++k) {
       w[k] = L[j][k] * d[k];
-      dj = dj - L[j][k] * w[k];
+      dj = fma(-L[j][k], w[k], dj);
     }
     d[j] = dj;
     rd[j] = 1.0 / dj;
@@ -1009,7 +1025,7 @@ __device__ int icp_update(const long long *sums, DevPose &pose, double *xo) {
     for (int i = j + 1; i < 6; ++i) {
       double s = A[i][j];
 #pragma unroll
-      for (int k = 0; k < j; ++k) s = s - L[i][k] * w[k];
+      for (int k = 0; k < j; ++k) s = fma(-L[i][k], w[k], s);
       L[i][j] = s * rd[j];
     }
   }
@@ -1022,14 +1038,14 @@ __device__ int icp_update(const long long *sums, DevPose &pose, double *xo) {
   for (int i = 0; i < 6; ++i) {  // L y = b
     double acc = A[i][6];
 #pragma unroll
-    for (int k = 0; k < i; ++k) acc = acc - L[i][k] * y[k];
+    for (int k = 0; k < i; ++k) acc = fma(-L[i][k], y[k], acc);
     y[i] = acc;
   }
 #pragma unroll
   for (int i = 5; i >= 0; --i) {  // Lᵀ x = D⁻¹ y
     double acc = y[i] * rd[i];
 #pragma unroll
-    for (int k = i + 1; k < 6; ++k) acc = acc - L[k][i] * x[k];
+    for (int k = i + 1; k < 6; ++k) acc = fma(-L[k][i], x[k], acc);
     x[i] = acc;
   }
 #pragma unroll
@@ -1626,16 +1642,51 @@ __device__ __forceinline__ float interp(const VolView &v, f3 cf) {
   return s;
 }
 
+// interp for volumes whose local voxel count fits 32-bit offsets (k_raycast's
+// kIdx32): the same corners, weights and sum order, but one tile-column index
+// for (gx, gy, gz) and the other seven corners as offsets from it (z + 1 is
+// always the next 64-voxel slice of the same column; x + 1 / y + 1 cross into
+// the next tile only at x & 7 == 7 / y & 7 == 7), read by buffer loads.
+__device__ __forceinline__ float interp32(const VolView &v, __amdgpu_buffer_rsrc_t t, f3 cf) {
+  const int gx = f2i_rd(cf.x), gy = f2i_rd(cf.y), gz = f2i_rd(cf.z);
+  if (gx < 0 || gx >= v.X - 1 || gy < 0 || gy >= v.Y - 1 || gz < 0 || gz >= v.Z - 1) return NAN;
+  if ((unsigned)(gz - v.zb) >= (unsigned)(v.zn - 1)) return NAN;
+  const float a = cf.x - (float)gx, b = cf.y - (float)gy, c = cf.z - (float)gz;
+  const unsigned col = (unsigned)v.zn << 6;  // voxels per tile column
+  const unsigned tile = __umul24((unsigned)gy >> 3, (unsigned)v.tiles_x) + ((unsigned)gx >> 3);
+  const unsigned i0 = ((tile * (unsigned)v.zn + (unsigned)(gz - v.zb)) << 6) | (((unsigned)gy & 7u) << 3 | ((unsigned)gx & 7u));
+  const unsigned dx = (gx & 7) == 7 ? col - 7u : 1u;
+  const unsigned dy = (gy & 7) == 7 ? __umul24((unsigned)v.tiles_x, col) - 56u : 8u;
+  auto ld = [&](unsigned i) {
+    return (float)(int16_t)__builtin_amdgcn_raw_buffer_load_b16(t, i << 1, 0, 0) * kDivShortMax;
+  };
+  const float t000 = ld(i0), t001 = ld(i0 + 64u), t010 = ld(i0 + dy), t011 = ld(i0 + dy + 64u);
+  const float t100 = ld(i0 + dx), t101 = ld(i0 + dx + 64u), t110 = ld(i0 + dx + dy), t111 = ld(i0 + dx + dy + 64u);
+  float s = 0.f;
+  s += t000 * (1 - a) * (1 - b) * (1 - c);
+  s += t001 * (1 - a) * (1 - b) * c;
+  s += t010 * (1 - a) * b * (1 - c);
+  s += t011 * (1 - a) * b * c;
+  s += t100 * a * (1 - b) * (1 - c);
+  s += t101 * a * (1 - b) * c;
+  s += t110 * a * b * (1 - c);
+  s += t111 * a * b * c;
+  return s;
+}
+
+template <bool kIdx32 = false>
 __device__ f3 compute_normal(const VolView &v, const RayConsts &rc, f3 p) {
+  const __amdgpu_buffer_rsrc_t t = make_rsrc(v.tsdf, kIdx32 ? (unsigned)(2 * v.local_voxels()) : 0u);
+  auto ip = [&](f3 q) { return kIdx32 ? interp32(v, t, mulc(q, rc.vs_inv)) : interp(v, mulc(q, rc.vs_inv)); };
   f3 n;
-  const float fx1 = interp(v, mulc({p.x + rc.gd.x, p.y, p.z}, rc.vs_inv));
-  const float fx2 = interp(v, mulc({p.x - rc.gd.x, p.y, p.z}, rc.vs_inv));
+  const float fx1 = ip({p.x + rc.gd.x, p.y, p.z});
+  const float fx2 = ip({p.x - rc.gd.x, p.y, p.z});
   n.x = (fx1 - fx2) / rc.gd.x;
-  const float fy1 = interp(v, mulc({p.x, p.y + rc.gd.y, p.z}, rc.vs_inv));
-  const float fy2 = interp(v, mulc({p.x, p.y - rc.gd.y, p.z}, rc.vs_inv));
+  const float fy1 = ip({p.x, p.y + rc.gd.y, p.z});
+  const float fy2 = ip({p.x, p.y - rc.gd.y, p.z});
   n.y = (fy1 - fy2) / rc.gd.y;
-  const float fz1 = interp(v, mulc({p.x, p.y, p.z + rc.gd.z}, rc.vs_inv));
-  const float fz2 = interp(v, mulc({p.x, p.y, p.z - rc.gd.z}, rc.vs_inv));
+  const float fz1 = ip({p.x, p.y, p.z + rc.gd.z});
+  const float fz2 = ip({p.x, p.y, p.z - rc.gd.z});
   n.z = (fz1 - fz2) / rc.gd.z;
   return normalized(n);
 }
@@ -2042,7 +2093,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KFX_RAY_OCC
 #ifdef KFX_RAY_NONORMAL  // timing experiment only (wrong values)
       const f3 n = {cvert.x, 0.5f, 0.5f};
 #else
-      const f3 n = compute_normal(v, rc, cvert);
+      const f3 n = compute_normal<kIdx32 && KFX_RAY_N32>(v, rc, cvert);
 #endif
       if (!isnan(n.x * n.y * n.z)) {
         // Rinv re-read from LDS here (volatile LDS reads: not held in
@@ -2816,12 +2867,31 @@ int icp_blocks(const LevelGeom &g) {
   return nb < 1 ? 1 : nb;
 }
 
+// The largest float x with RN(sqrtf(x)) <= t (x >= 0), so that the ICP lane's
+// `sqrtf(x) <= t` is the single compare `x <= bound` for every non-negative x
+// (RN(sqrt) is monotonic; a NaN x fails both).  t < 0 admits nothing, t NaN
+// nothing (the bound is NaN), t = +inf everything.
+float sqrt_le_bound(float t) {
+  if (std::isnan(t)) return t;
+  if (t < 0.f) return -1.f;
+  if (std::isinf(t)) return t;
+  float x = t * t;
+  if (std::isinf(x)) x = std::numeric_limits<float>::max();
+  while (x > 0.f && std::sqrt(x) > t) x = std::nextafter(x, 0.f);
+  for (;;) {
+    const float n = std::nextafter(x, std::numeric_limits<float>::infinity());
+    if (std::isinf(n) || std::sqrt(n) > t) break;
+    x = n;
+  }
+  return x;
+}
+
 IcpPlan make_icp_plan(int levels, const LevelGeom *g, const int *iters, FrameView cur,
                       FrameView prev, float dist_thr, float angle_thr) {
   IcpPlan pl{};
   pl.levels = levels;
-  pl.dist_thr = dist_thr;
-  pl.angle_thr = angle_thr;
+  pl.dist2_max = sqrt_le_bound(dist_thr);
+  pl.sine2_max = sqrt_le_bound(angle_thr);
   for (int l = 0; l < levels; ++l) {
     pl.g[l] = g[l];
     pl.npix[l] = icp_npix(g[l], &pl.xe[l]);
@@ -2876,19 +2946,19 @@ void launch_icp(hipStream_t s, const LevelGeom &g, const float *cv, const float 
   const int p0 = xe * (int)((long long)ye * band / nbands), p1 = xe * (int)((long long)ye * (band + 1) / nbands);
   const int nb = std::max(1, (p1 - p0 + kIcpBlockPix - 1) / kIcpBlockPix);
   hipLaunchKernelGGL(k_icp_acc, dim3(nb), dim3(kIcpThreads), 0, s, g, xe, p0, p1, cv, cn, pv, pn,
-                     dist_thr, angle_thr, st, shards, ticket, force, update);
+                     sqrt_le_bound(dist_thr), sqrt_le_bound(angle_thr), st, shards, ticket, force, update);
 }
 
 // The solve of one ICP iteration from DevState::sums (the all-reduced partials
 // of the sharded mode): icp_registration.cpp:33-42, as in k_icp_acc's last block.
 __global__ void k_icp_solve(DevState *__restrict__ st) {
   if (st->mode != MODE_TRACK || st->icp_fail) return;
-  __shared__ long long sums[27];
-  if (threadIdx.x < 27) sums[threadIdx.x] = st->sums[threadIdx.x];
+  __shared__ double sumd[27];
+  if (threadIdx.x < 27) sumd[threadIdx.x] = icp_sum_value(st->sums[threadIdx.x]);
   __syncthreads();
   DevPose p = st->icp_pose;
   double x[6];
-  const int f = icp_update(sums, p, x);
+  const int f = icp_update(sumd, p, x);
   if (threadIdx.x == 0) {
     if (f) {
       st->icp_fail = 1;

@@ -12,6 +12,7 @@ namespace kfx {
 namespace {
 __global__ void k_solve_bench(const long long *sums_in, float *out, int iters, unsigned long long *cyc) {
   __shared__ long long sums[27];
+  __shared__ double sumd[27];
   if (threadIdx.x < 27) sums[threadIdx.x] = sums_in[threadIdx.x];
   __syncthreads();
   DevPose p = pose_identity();
@@ -21,9 +22,11 @@ __global__ void k_solve_bench(const long long *sums_in, float *out, int iters, u
   for (int i = 0; i < iters; ++i) {
     if (threadIdx.x == 0) sums[0] += (long long)(acc != 0.f);  // keeps the solve inside the loop
     __syncthreads();
+    if (threadIdx.x < 27) sumd[threadIdx.x] = icp_sum_value(sums[threadIdx.x]);  // as k_icp_track
+    __syncthreads();
     DevPose q = p;
-    const int f = icp_update(sums, q, x);
-    acc += q.t[0] + (float)f;
+    const int f = icp_update(sumd, q, x);
+    acc += q.t[0] + q.R[1] + q.R[5] + (float)f;  // rotation too: the Rodrigues update stays timed
     p.t[0] = acc * 1e-30f;  // carry a dependency into the next solve
   }
   const unsigned long long t1 = __builtin_amdgcn_s_memtime();
