@@ -26,8 +26,8 @@ Multi-GPU (`torchrun --nproc-per-node N`), one process per GPU:
 
 The JSON line also carries:
   stage_ms      per-stage device ms (HIP events on the pipeline stream)
-  roofline      integrate kernel: algorithmic bytes (8*N_upd + 8*N_col + 7*W*H,
-                SURVEY.md §8d; N counted on the device) / its event-timed
+  roofline      integrate kernel: algorithmic bytes (6*N_upd + 8*N_col + 7*W*H:
+                SURVEY.md §8d with the u8 weight store; N counted on the device) / its event-timed
                 duration vs 8 TB/s HBM; traffic = HBM bytes per launch from the
                 committed rocprofv3 PMC summary (profiles/integrate_pmc.json)
   cpu_baseline  the serial C++ oracle running the same pipeline on host cores
@@ -297,13 +297,20 @@ def run_stream(a, intr, params, frames, D, local, slab=None, icp_ar=False, timin
 
 
 def integrate_roofline(work, ms, W, H, ms_source, traffic=None, traffic_src=None):
-    """B_int = 8 N_upd + 8 N_col + 7 W H (N counted on the device)."""
-    b = 8 * work["updated"] + 8 * work["colored"] + 7 * W * H
-    achieved = b / (ms * 1e-3) / 1e9 if ms == ms and ms > 0 else 0.0
+    """SURVEY.md §8d's B_int = 8 N_upd + 8 N_col + 7 W H (N counted on the device)
+    with the per-updated-voxel term of THIS storage format: int16 tsdf + u8 weight
+    read and written = 6 B (the reference's int16 weight makes it 8 B;
+    `achieved_ref_format` is the same time priced at the survey's 8 B)."""
+    b = 6 * work["updated"] + 8 * work["colored"] + 7 * W * H
+    b_ref = 8 * work["updated"] + 8 * work["colored"] + 7 * W * H
+    ok = ms == ms and ms > 0
+    achieved = b / (ms * 1e-3) / 1e9 if ok else 0.0
+    achieved_ref = b_ref / (ms * 1e-3) / 1e9 if ok else 0.0
     return {"kernel": "k_integrate", "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
             "traffic_source": traffic_src or "none: no PMC record of this workload and step count",
-            "algorithmic_bytes_per_launch": int(b), "avg_launch_ms": round(ms, 4), "launch_ms_source": ms_source}
+            "algorithmic_bytes_per_launch": int(b), "bytes_formula": "6*N_upd + 8*N_col + 7*W*H (u8 weight store)",
+            "achieved_ref_format": round(achieved_ref, 1), "avg_launch_ms": round(ms, 4), "launch_ms_source": ms_source}
 
 
 def round_ms(d):

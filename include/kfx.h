@@ -186,6 +186,9 @@ int kfx_set_frame_maps(kfx_ctx *ctx, int which, int level, const float *vmap,
  * reference's 8-byte x-fastest records {int16 tsdf, int16 weight, u8 c0,c1,c2,
  * u8 pad=0} (device_types.hpp:51-56).  dst holds X*Y*Z*8 bytes. */
 int kfx_download_tsdf(kfx_ctx *ctx, void *dst_records);
+/* Import records in the same format (test seam; no reference counterpart).
+ * Weights are stored as u8 on the device (the reference's never exceed
+ * MAX_WEIGHT = 64): a record weight outside 0..255 fails with KFX_ERR_ARG. */
 int kfx_upload_tsdf(kfx_ctx *ctx, const void *src_records);
 /* SoA export: tsdf int16[N], weight int16[N], colour u8x4[N] (any may be NULL). */
 int kfx_download_volume_soa(kfx_ctx *ctx, int16_t *tsdf, int16_t *weight,

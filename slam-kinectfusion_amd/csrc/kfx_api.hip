@@ -592,7 +592,7 @@ VolView make_vol(const kfx_params &p, int rank, int world) {
 int do_reset(kfx_ctx *c) {
   const size_t n = nvox(c);
   HIPCHK(hipMemsetAsync(c->vol.tsdf, 0, n * sizeof(int16_t), c->stream));
-  HIPCHK(hipMemsetAsync(c->vol.weight, 0, n * sizeof(int16_t), c->stream));
+  HIPCHK(hipMemsetAsync(c->vol.weight, 0, n * sizeof(uint8_t), c->stream));
   HIPCHK(hipMemsetAsync(c->vol.rgb, 0, n * sizeof(uint32_t), c->stream));
   HIPCHK(hipMemsetAsync(c->vol.bocc, 0, c->vol.bocc_bytes(), c->stream));
   HIPCHK(hipMemsetAsync(c->vol.socc, 0, c->vol.socc_bytes(), c->stream));
@@ -763,13 +763,13 @@ static int create_impl(const kfx_intrinsics *intr, const kfx_params *params, int
   c->vol = make_vol(p, rank, world);
   const size_t n = nvox(c);
   {
-    // tsdf and weight in ONE allocation, weight at a fixed offset (2 MiB-rounded
-    // + 4 KiB): with two allocations the relative physical placement of
-    // tsdf[i] and weight[i] (read together by integrate) changed from run to
-    // run and integrate took 172-185 us; fixed, 169-172 us
+    // tsdf and weight in ONE allocation, weight (u8) at a fixed offset (2 MiB-
+    // rounded + 4 KiB): with two allocations the relative physical placement
+    // of tsdf[i] and weight[i] (read together by integrate) changed from run
+    // to run and integrate took 172-185 us; fixed, 169-172 us
     const size_t off = ((n * 2 + (2u << 20) - 1) & ~(size_t)((2u << 20) - 1)) + KFX_VOL_PAD;
-    if ((r = dalloc(c, (void **)&c->vol.tsdf, off + n * 2))) return fail(r);
-    c->vol.weight = (int16_t *)((char *)c->vol.tsdf + off);
+    if ((r = dalloc(c, (void **)&c->vol.tsdf, off + n))) return fail(r);
+    c->vol.weight = (uint8_t *)((char *)c->vol.tsdf + off);
   }
   if ((r = dalloc(c, (void **)&c->vol.rgb, n * 4))) return fail(r);
   if ((r = dalloc(c, (void **)&c->vol.bocc, c->vol.bocc_bytes()))) return fail(r);
@@ -1201,14 +1201,17 @@ int kfx_upload_tsdf(kfx_ctx *c, const void *src) {
   HIPCHK(hipStreamSynchronize(c->stream));
   const int nz = slab_z(c, 8);
   uint64_t *tmp = nullptr;
-  HIPCHK(hipMalloc(&tmp, c->vol.slice * 8 * (size_t)nz));
+  const size_t tbytes = c->vol.slice * 8 * (size_t)nz;
+  HIPCHK(hipMalloc(&tmp, tbytes + 64));
+  unsigned *bad = reinterpret_cast<unsigned *>((char *)tmp + tbytes);  // weight outside 0..255
+  HIPCHK(hipMemsetAsync(bad, 0, 4, c->stream));
   const int zend = c->vol.zb + c->vol.zn;
   for (int z0 = c->vol.zb; z0 < zend; z0 += nz) {  // stored slices, halo included
     const int k = std::min(nz, zend - z0);
     hipError_t e = hipMemcpyAsync(tmp, (const char *)src + c->vol.slice * 8 * (size_t)z0,
                                   c->vol.slice * 8 * (size_t)k, hipMemcpyHostToDevice, c->stream);
     if (e == hipSuccess) {
-      launch_import_records(c->stream, c->vol, z0, k, tmp);
+      launch_import_records(c->stream, c->vol, z0, k, tmp, bad);
       e = hipStreamSynchronize(c->stream);
     }
     if (e != hipSuccess) {
@@ -1216,7 +1219,11 @@ int kfx_upload_tsdf(kfx_ctx *c, const void *src) {
       return set_err(KFX_ERR_HIP, std::string("upload_tsdf: ") + hipGetErrorString(e));
     }
   }
+  unsigned nbad = 0;
+  HIPCHK(hipMemcpy(&nbad, bad, 4, hipMemcpyDeviceToHost));
   HIPCHK(hipFree(tmp));
+  if (nbad)  // the volume contents are then undefined; the reference never holds such weights
+    return set_err(KFX_ERR_ARG, "upload_tsdf: a weight outside 0..255 (u8 weight store; the reference's are 0..64)");
   launch_occ_rebuild(c->stream, c->vol);  // the raycast's skip maps of the new contents
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(c->stream));

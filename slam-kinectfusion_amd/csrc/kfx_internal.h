@@ -85,7 +85,7 @@ struct IcpSync {
 constexpr int kSlabHalo = 4;
 struct VolView {
   int16_t *tsdf;
-  int16_t *weight;
+  uint8_t *weight;  // D: u8 storage of the reference's int16 weight (values 0..MAX_WEIGHT; 0..255 accepted on upload)
   uint32_t *rgb;  // u8 c0,c1,c2,pad
   int X, Y, Z;
   int zb, zn;      // stored global slices [zb, zb+zn)
@@ -263,7 +263,7 @@ size_t scan_blocks(size_t n);  // bsum entries launch_scan needs (<= 65536)
 void launch_scan(hipStream_t s, const unsigned *counts, unsigned long long *offsets,
                  unsigned long long *bsum, size_t n, unsigned long long *total);
 void launch_export_records(hipStream_t s, VolView v, int z0, int nz, uint64_t *dst);
-void launch_import_records(hipStream_t s, VolView v, int z0, int nz, const uint64_t *src);
+void launch_import_records(hipStream_t s, VolView v, int z0, int nz, const uint64_t *src, unsigned *bad);
 void launch_export_soa(hipStream_t s, VolView v, int z0, int nz, int16_t *t, int16_t *w,
                        uint32_t *c);
 // clear the occupancy maps and re-mark every brick holding a negative tsdf

@@ -810,7 +810,6 @@ __global__ __launch_bounds__(kIcpThreads, 2) void k_icp_track(IcpPlan pl, DevSta
   __shared__ IcpRed red;
   __shared__ long long sums[27];
   __shared__ double sumd[27];  // the same sums unpacked (one conversion per thread, not per solver lane)
-  __shared__ DevPose spose;
   __shared__ int sfail, sstall;
   int fail = 0;
   const bool withhold = blockIdx.x == 0 && st->debug_stall;  // test hook: never arrive at slot 0
@@ -895,17 +894,15 @@ __global__ __launch_bounds__(kIcpThreads, 2) void k_icp_track(IcpPlan pl, DevSta
       }
       __syncthreads();
       if (tr && blockIdx.x == 0) sy->trace[slot][5] = wall_clock64();
-      if (threadIdx.x < 64) {  // wave 0 solves (every block, identical result)
+      {  // every wave solves (every block, identical result): no broadcast of
+         // the pose through LDS and no barrier after the solve (the next
+         // writes of sums / sumd / red come after the block reduce's barrier)
         DevPose p = P;
         double x[6];
         int f = icp_update(sumd, p, x);
         if (tr && blockIdx.x == 0) sy->trace[slot][6] = __builtin_amdgcn_readfirstlane((int)x[0]) + wall_clock64();
         if (sstall) f = 1;  // a stalled block stops; the others stall at the next barrier
         if (threadIdx.x < 27 && blockIdx.x == 0) st->sums[threadIdx.x] = sums[threadIdx.x];
-        if (threadIdx.x == 0) {
-          sfail = f;
-          if (!f) spose = p;
-        }
         if (threadIdx.x == 0 && blockIdx.x == 0) {
           if (f) {
             st->icp_fail = 1;
@@ -914,17 +911,15 @@ __global__ __launch_bounds__(kIcpThreads, 2) void k_icp_track(IcpPlan pl, DevSta
             for (int i = 0; i < 6; ++i) st->x[i] = x[i];
           }
         }
-      }
-      __syncthreads();
-      if (tr && blockIdx.x == 0) sy->trace[slot][3] = wall_clock64();
-      fail = __builtin_amdgcn_readfirstlane(sfail);
-      if (!fail) {  // block-uniform: keep the pose in SGPRs
+        if (tr && blockIdx.x == 0) sy->trace[slot][3] = wall_clock64();
+        fail = __builtin_amdgcn_readfirstlane(f);
+        if (!fail) {  // wave-uniform: keep the pose in SGPRs
 #pragma unroll
-        for (int k = 0; k < 9; ++k) P.R[k] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(spose.R[k])));
+          for (int k = 0; k < 9; ++k) P.R[k] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(p.R[k])));
 #pragma unroll
-        for (int k = 0; k < 3; ++k) P.t[k] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(spose.t[k])));
+          for (int k = 0; k < 3; ++k) P.t[k] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(p.t[k])));
+        }
       }
-      __syncthreads();  // spose/sums/red are rewritten next iteration
     }
   }
   if (threadIdx.x == 0) {
@@ -1195,27 +1190,28 @@ struct VoxMem<true> {
   __device__ VoxMem(const VolView &v) : c(v.rgb) {
     const size_t n = v.local_voxels();
     t = make_rsrc(v.tsdf, (unsigned)min(2 * n, (size_t)0xFFFFFFFFu));
-    w = make_rsrc(v.weight, (unsigned)min(2 * n, (size_t)0xFFFFFFFFu));
+    w = make_rsrc(v.weight, (unsigned)min(n, (size_t)0xFFFFFFFFu));
   }
   __device__ int16_t ld_t(Idx i) const { return __builtin_amdgcn_raw_buffer_load_b16(t, i << 1, 0, 0); }
-  __device__ int16_t ld_w(Idx i) const { return __builtin_amdgcn_raw_buffer_load_b16(w, i << 1, 0, 0); }
+  __device__ int16_t ld_w(Idx i) const { return (int16_t)__builtin_amdgcn_raw_buffer_load_b8(w, i, 0, 0); }
   __device__ uint32_t ld_c(Idx i) const { return c[i]; }  // only for voxels that pass
   __device__ void st_t(Idx i, int16_t x) const { __builtin_amdgcn_raw_buffer_store_b16(x, t, i << 1, 0, 0); }
-  __device__ void st_w(Idx i, int16_t x) const { __builtin_amdgcn_raw_buffer_store_b16(x, w, i << 1, 0, 0); }
+  __device__ void st_w(Idx i, int16_t x) const { __builtin_amdgcn_raw_buffer_store_b8((uint8_t)x, w, i, 0, 0); }
   __device__ void st_c(Idx i, uint32_t x) const { c[i] = x; }
   static constexpr Idx kNone = 0x7FFFFFFFu;  // byte offsets past every buffer
 };
 template <>
 struct VoxMem<false> {
   using Idx = size_t;
-  int16_t *t, *w;
+  int16_t *t;
+  uint8_t *w;
   uint32_t *c;
   __device__ VoxMem(const VolView &v) : t(v.tsdf), w(v.weight), c(v.rgb) {}
   __device__ int16_t ld_t(Idx i) const { return t[i]; }
-  __device__ int16_t ld_w(Idx i) const { return w[i]; }
+  __device__ int16_t ld_w(Idx i) const { return (int16_t)w[i]; }
   __device__ uint32_t ld_c(Idx i) const { return c[i]; }
   __device__ void st_t(Idx i, int16_t x) const { t[i] = x; }
-  __device__ void st_w(Idx i, int16_t x) const { w[i] = x; }
+  __device__ void st_w(Idx i, int16_t x) const { w[i] = (uint8_t)x; }
   __device__ void st_c(Idx i, uint32_t x) const { c[i] = x; }
   static constexpr Idx kNone = 0;  // rejected lanes read voxel 0 (never written by them)
 };
@@ -2660,7 +2656,7 @@ __global__ void k_export_records(VolView v, int z0, int nz, uint64_t *dst) {
   }
 }
 
-__global__ void k_import_records(VolView v, int z0, int nz, const uint64_t *src) {
+__global__ void k_import_records(VolView v, int z0, int nz, const uint64_t *src, unsigned *bad) {
   const size_t n = v.slice * (size_t)nz;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (size_t)gridDim.x * blockDim.x) {
@@ -2670,7 +2666,9 @@ __global__ void k_import_records(VolView v, int z0, int nz, const uint64_t *src)
     const size_t s = vox_index(v, x, y, z);
     const uint64_t rec = src[i];
     v.tsdf[s] = (int16_t)(rec & 0xffffu);
-    v.weight[s] = (int16_t)((rec >> 16) & 0xffffu);
+    const int w = (int16_t)((rec >> 16) & 0xffffu);
+    if ((unsigned)w > 255u) *bad = 1u;  // not representable in the u8 weight store
+    v.weight[s] = (uint8_t)w;
     v.rgb[s] = (uint32_t)((rec >> 32) & 0xffffffu);
   }
 }
@@ -3256,8 +3254,8 @@ static dim3 slab_grid(const VolView &v, int nz) {
 void launch_export_records(hipStream_t s, VolView v, int z0, int nz, uint64_t *dst) {
   hipLaunchKernelGGL(k_export_records, slab_grid(v, nz), dim3(256), 0, s, v, z0, nz, dst);
 }
-void launch_import_records(hipStream_t s, VolView v, int z0, int nz, const uint64_t *src) {
-  hipLaunchKernelGGL(k_import_records, slab_grid(v, nz), dim3(256), 0, s, v, z0, nz, src);
+void launch_import_records(hipStream_t s, VolView v, int z0, int nz, const uint64_t *src, unsigned *bad) {
+  hipLaunchKernelGGL(k_import_records, slab_grid(v, nz), dim3(256), 0, s, v, z0, nz, src, bad);
 }
 void launch_checksum(hipStream_t s, VolView v, unsigned long long *out) {
   hipLaunchKernelGGL(k_checksum, dim3(2048), dim3(256), 0, s, v, out);

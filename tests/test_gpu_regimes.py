@@ -20,7 +20,7 @@ import numpy as np
 import pytest
 
 import oracle as O
-from kfx import KFX_FRAME_PREV, KFX_OK, KinectFusion, pipeline_group, synth
+from kfx import KFX_FRAME_PREV, KFX_OK, KfxError, KinectFusion, pipeline_group, synth
 from kfx.abi import Intrinsics, Pose, default_params
 
 pytestmark = pytest.mark.gpu
@@ -88,6 +88,27 @@ def saturated_volume(n, seed):
 @pytest.fixture(scope="module")
 def seq_qvga():
     return synth.sequence(10, synth.Intrinsics.qvga(), noise=True, dropout=0.01)
+
+
+def test_upload_rejects_weights_outside_u8():
+    """The device stores weights as u8 (the reference's never exceed
+    MAX_WEIGHT = 64): an uploaded record weight outside 0..255 is refused
+    (KFX_ERR_ARG), 255 itself is kept exactly."""
+    n = 64
+    p = default_params(dims=n, range_m=L_VOL)
+    kf = KinectFusion(Intrinsics.from_any(synth.Intrinsics.qvga()), p)
+    t = np.zeros(n ** 3, np.int16)
+    w = np.zeros(n ** 3, np.int16)
+    c = np.zeros(4 * n ** 3, np.uint8)
+    w[12345], t[12345] = 255, -77
+    kf.upload_tsdf(records(t, w, c))
+    gt, gw, _ = kf.volume_soa()
+    assert gw[12345] == 255 and gt[12345] == -77 and (gw != 0).sum() == 1
+    for bad in (256, -1):
+        w[999] = bad
+        with pytest.raises(KfxError, match="0..255"):
+            kf.upload_tsdf(records(t, w, c))
+    kf.close()
 
 
 @pytest.mark.parametrize("n", [64, 128])
