@@ -135,7 +135,7 @@ def cpu_baseline(intr, params, bgr, dep, order, n):
             "host_cpus": os.cpu_count(), "cpu": _cpu_model()}
 
 
-def raycast_roofline(work, ms, W, H, ms_source):
+def raycast_roofline(work, ms, W, H, ms_source, traffic=None, traffic_src=None):
     """B_ray = 2 N_uniq + 24 W H, N_uniq = the distinct voxels
     the reference raycast (no skipping) reads, counted on the device on the
     last frame's state (kfx_raycast_stats, pinned against the oracle's count).
@@ -147,7 +147,8 @@ def raycast_roofline(work, ms, W, H, ms_source):
     b = 2 * work["ref_uniq_voxels"] + 24 * W * H
     achieved = b / (ms * 1e-3) / 1e9
     return {"kernel": "k_raycast", "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "traffic_source": traffic_src or "none: no PMC record of this workload and step count",
             "algorithmic_bytes_per_launch": int(b), "avg_launch_ms": round(ms, 4), "launch_ms_source": ms_source,
             "ref_uniq_voxels": work["ref_uniq_voxels"], "ref_tsdf_reads": work["ref_reads"],
             "kernel_tsdf_reads": int(14 * work["batches"] + work["blocked_lookups"] + 48 * work["normal_candidates"])}
@@ -519,12 +520,13 @@ def measure_main(a, name, intr, params, frames, D, rank, world, local, mode, icp
     # HBM traffic of the integrate launch from a rocprofv3 FETCH_SIZE/WRITE_SIZE
     # record (tools/prof.sh), attached only when that record was measured on
     # this workload with the same step counts (the same saturation regime)
-    traffic, traffic_src = None, None
+    traffic, traffic_src, ray_traffic = None, None, None
     try:
         rec = json.load(open(a.traffic))
         if (mode == "single" and rec.get("workload") == [n, W, H] and rec.get("steps") == a.steps
                 and rec.get("warmup") == a.warmup):
             traffic = rec.get("hbm_bytes_per_launch")
+            ray_traffic = rec.get("raycast_hbm_bytes_per_launch")
             traffic_src = f"{os.path.relpath(a.traffic, ROOT)}: {rec.get('command')} ({rec.get('regime')})"
     except (OSError, ValueError):
         pass
@@ -564,7 +566,8 @@ def measure_main(a, name, intr, params, frames, D, rank, world, local, mode, icp
         "integrate_voxels": work,
         "raycast_work": ray_work,
         "roofline": roof,
-        "roofline_raycast": raycast_roofline(ray_work, ray_ms, W, H, ms_source),
+        "roofline_raycast": raycast_roofline(ray_work, ray_ms, W, H, ms_source, ray_traffic,
+                                             traffic_src if ray_traffic else None),
         "host_input": host_in,
         "cpu_baseline": cpu,
         "c1_record": c1,
