@@ -523,6 +523,9 @@ constexpr int kIcpPix = KFX_ICP_PIX;
 #ifndef KFX_RAY_N32
 #define KFX_RAY_N32 1  // raycast normals: 32-bit tile-column offsets + buffer loads (kIdx32 volumes)
 #endif
+#ifndef KFX_ICP_PPLCAP
+#define KFX_ICP_PPLCAP 256  // ICP plan: a level takes the fewest pixels per lane that keep it within this many blocks
+#endif
 #ifndef KFX_ICP_THREADS
 #define KFX_ICP_THREADS 256  // ICP: threads per block
 #endif
@@ -2895,7 +2898,7 @@ IcpPlan make_icp_plan(int levels, const LevelGeom *g, const int *iters, FrameVie
     pl.npix[l] = icp_npix(g[l], &pl.xe[l]);
     // pixels per lane: the fewest that keep the level within one block per
     // CU (256), so coarse levels spread over more waves (shorter lane phase)
-    pl.ppl[l] = std::max(1, std::min(kIcpPix, (pl.npix[l] + 256 * kIcpThreads - 1) / (256 * kIcpThreads)));
+    pl.ppl[l] = std::max(1, std::min(kIcpPix, (pl.npix[l] + KFX_ICP_PPLCAP * kIcpThreads - 1) / (KFX_ICP_PPLCAP * kIcpThreads)));
     pl.groups[l] = std::max(1, (pl.npix[l] + kIcpThreads * pl.ppl[l] - 1) / (kIcpThreads * pl.ppl[l]));
     pl.iters[l] = iters[l];
     pl.cv[l] = cur.v[l];
