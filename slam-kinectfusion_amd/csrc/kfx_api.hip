@@ -785,9 +785,9 @@ static int create_impl(const kfx_intrinsics *intr, const kfx_params *params, int
   if ((r = dalloc(c, (void **)&c->st, sizeof(DevState)))) return fail(r);
   c->pose_cap = kInitialPoseCap;
   if ((r = dalloc(c, (void **)&c->pose_log, sizeof(DevPose) * (size_t)c->pose_cap))) return fail(r);
-  if ((r = dalloc(c, (void **)&c->icp_shards, sizeof(unsigned long long) * 8 * 27 + 64)))
+  if ((r = dalloc(c, (void **)&c->icp_shards, sizeof(unsigned long long) * kIcpShards * 27 + 64)))
     return fail(r);
-  c->icp_ticket = reinterpret_cast<unsigned *>(c->icp_shards + 8 * 27);
+  c->icp_ticket = reinterpret_cast<unsigned *>(c->icp_shards + kIcpShards * 27);
   if ((r = dalloc(c, (void **)&c->icp_sync, sizeof(IcpSync)))) return fail(r);
   for (int b = 0; b < 2; ++b)
     c->planb[b] = make_icp_plan(c->L, c->g, c->p.icp_iter_count, c->curb[b], c->prev,

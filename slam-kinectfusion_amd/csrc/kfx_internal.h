@@ -44,7 +44,10 @@ struct LevelGeom {
   float fx, fy, cx, cy;
 };
 
-constexpr int kIcpShards = 8;
+#ifndef KFX_ICP_SHARDS
+#define KFX_ICP_SHARDS 8  // ICP: partial-sum rows (atomic spread vs rows every solver reads)
+#endif
+constexpr int kIcpShards = KFX_ICP_SHARDS;
 constexpr int kIcpMaxSlots = 64;  // ICP iterations per frame in the persistent kernel
 
 // Per-frame plan of the persistent ICP kernel (all levels, all iterations).

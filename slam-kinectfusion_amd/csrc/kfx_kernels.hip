@@ -756,9 +756,9 @@ __global__ __launch_bounds__(kIcpThreads) void k_icp_acc(LevelGeom g, int xe, in
   if (!last) return;
   __shared__ double sumd[27];
   // one read-and-clear per thread (a thread's atomics serialise)
-  if (threadIdx.x < kIcpShards * 27)
-    red.red2[threadIdx.x] = __longlong_as_double((long long)__hip_atomic_exchange(
-        &shards[threadIdx.x], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  for (int i = threadIdx.x; i < kIcpShards * 27; i += kIcpThreads)
+    red.red2[i] = __longlong_as_double((long long)__hip_atomic_exchange(
+        &shards[i], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   if (threadIdx.x == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
   if (threadIdx.x < 27) {
@@ -884,9 +884,9 @@ __global__ __launch_bounds__(kIcpThreads, 2) void k_icp_track(IcpPlan pl, DevSta
       }
       __syncthreads();
       // one coherent load per thread (a thread's atomic loads serialise)
-      if (threadIdx.x < kIcpShards * 27)
-        red.red2[threadIdx.x] = __longlong_as_double((long long)__hip_atomic_load(
-            &sh[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      for (int i = threadIdx.x; i < kIcpShards * 27; i += kIcpThreads)
+        red.red2[i] = __longlong_as_double((long long)__hip_atomic_load(
+            &sh[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
       __syncthreads();
       if (threadIdx.x < 27) {
         long long a = 0;
