@@ -526,6 +526,9 @@ constexpr int kIcpPix = KFX_ICP_PIX;
 #ifndef KFX_ICP_PPLCAP
 #define KFX_ICP_PPLCAP 256  // ICP plan: a level takes the fewest pixels per lane that keep it within this many blocks
 #endif
+#ifndef KFX_ICP_SLEEP
+#define KFX_ICP_SLEEP 1  // ICP release poll: s_sleep units (64 clocks) between polls (0: busy poll)
+#endif
 #ifndef KFX_ICP_THREADS
 #define KFX_ICP_THREADS 256  // ICP: threads per block
 #endif
@@ -872,7 +875,7 @@ __global__ __launch_bounds__(kIcpThreads, 2) void k_icp_track(IcpPlan pl, DevSta
         int stalled = 0;
         const unsigned *flag = &sy->release[blockIdx.x & 7].v;
         while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)(slot + 1)) {
-          __builtin_amdgcn_s_sleep(1);
+          if (KFX_ICP_SLEEP) __builtin_amdgcn_s_sleep(KFX_ICP_SLEEP);
           if (wall_clock64() - t0 > kIcpWatchdogTicks) {
             stalled = 1;
             break;
