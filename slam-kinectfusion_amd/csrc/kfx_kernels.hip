@@ -54,7 +54,7 @@
 #define KFX_INT_MAXCHUNK 8  // integrate: most z-chunks per column tile
 #endif
 #ifndef KFX_INT_WAVES
-#define KFX_INT_WAVES 16384  // integrate: target wave count (z-chunks per column tile)
+#define KFX_INT_WAVES 12288  // integrate: target wave count (z-chunks per column tile; C2: 3 chunks of 4096 tiles)
 #endif
 
 namespace kfx {
@@ -2997,7 +2997,7 @@ static int integrate_mode(const VolView &v) {
 int integrate_chunks(const VolView &v) {
   const int tiles = v.tiles_x * v.tiles_y;
   if (integrate_mode(v) == 1) return std::max(1, std::min(KFX_INT_NC, v.zn / 32));  // chunks of >= 32 slices
-  // z-chunks so that >= KFX_INT_WAVES waves exist (16 per SIMD on 1024 SIMDs)
+  // z-chunks so that >= KFX_INT_WAVES waves exist (12 per SIMD on 1024 SIMDs)
   return std::max(1, std::min(KFX_INT_MAXCHUNK, (KFX_INT_WAVES + tiles - 1) / tiles));
 }
 
