@@ -68,9 +68,9 @@ def parse():
                     help="frames fed from host memory through kfx_pipeline_async for host_input (0 = skip)")
     ap.add_argument("--c1-frames", type=int, default=100,
                     help="oracle frames of the C1 record (128^3, same frames; 0 = skip)")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r02_integrate_pmc.json"),
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r03_integrate_pmc.json"),
                     help="integrate PMC traffic record; attached only when it was measured on this command's "
-                         "workload and step counts")
+                         "workload and step counts with the same libkfx.so (sha256)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--sample-every", type=int, default=8,
                     help="time kernels on every k-th timed frame with HIP events (0 = off)")
@@ -152,6 +152,14 @@ def raycast_roofline(work, ms, W, H, ms_source, traffic=None, traffic_src=None):
             "algorithmic_bytes_per_launch": int(b), "avg_launch_ms": round(ms, 4), "launch_ms_source": ms_source,
             "ref_uniq_voxels": work["ref_uniq_voxels"], "ref_tsdf_reads": work["ref_reads"],
             "kernel_tsdf_reads": int(14 * work["batches"] + work["blocked_lookups"] + 48 * work["normal_candidates"])}
+
+
+def file_sha256(path):
+    import hashlib
+    try:
+        return hashlib.sha256(open(path, "rb").read()).hexdigest()
+    except OSError:
+        return None
 
 
 def _cpu_model():
@@ -520,14 +528,22 @@ def measure_main(a, name, intr, params, frames, D, rank, world, local, mode, icp
     # HBM traffic of the integrate launch from a rocprofv3 FETCH_SIZE/WRITE_SIZE
     # record (tools/prof.sh), attached only when that record was measured on
     # this workload with the same step counts (the same saturation regime)
-    traffic, traffic_src, ray_traffic = None, None, None
+    # and on the very library this process loaded (sha256 of libkfx.so)
+    traffic, traffic_src, ray_traffic, sq = None, None, None, None
+    lib_hash = file_sha256(kfx.LIB_PATH)
     try:
         rec = json.load(open(a.traffic))
-        if (mode == "single" and rec.get("workload") == [n, W, H] and rec.get("steps") == a.steps
-                and rec.get("warmup") == a.warmup):
+        same_run = (mode == "single" and rec.get("workload") == [n, W, H] and rec.get("steps") == a.steps
+                    and rec.get("warmup") == a.warmup)
+        if same_run and rec.get("lib_sha256") == lib_hash:
             traffic = rec.get("hbm_bytes_per_launch")
             ray_traffic = rec.get("raycast_hbm_bytes_per_launch")
-            traffic_src = f"{os.path.relpath(a.traffic, ROOT)}: {rec.get('command')} ({rec.get('regime')})"
+            sq = {"integrate": rec.get("integrate_sq"), "raycast": rec.get("raycast_sq")}
+            traffic_src = (f"{os.path.relpath(a.traffic, ROOT)}: {rec.get('command')} ({rec.get('regime')}); "
+                           f"libkfx.so sha256 {lib_hash[:16]} (commit {rec.get('commit')})")
+        elif same_run:
+            traffic_src = (f"none: {os.path.relpath(a.traffic, ROOT)} was measured on libkfx.so sha256 "
+                           f"{str(rec.get('lib_sha256'))[:16]}, this run loaded {str(lib_hash)[:16]}")
     except (OSError, ValueError):
         pass
     if mode == "slab":
@@ -538,6 +554,11 @@ def measure_main(a, name, intr, params, frames, D, rank, world, local, mode, icp
                                   pr["integrate_ms"], W, H, ms_source + f", slowest rank ({k})")
     else:
         roof = integrate_roofline(work, int_launch_ms, W, H, ms_source, traffic, traffic_src)
+        roof["lib_sha256"] = lib_hash
+        if sq and sq.get("integrate"):
+            q = sq["integrate"]
+            roof["issue"] = {k: q.get(k) for k in ("valu_issue_frac_2cyc", "valu_active_frac", "valu_insts_per_wave",
+                                                   "wave_cycles_split", "kernel_cycles")}
 
     cpu = c1 = None
     if rank == 0 and world == 1 and a.cpu_frames > 0:

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define KFX_ABI_VERSION 1
+#define KFX_ABI_VERSION 2 /* 2: kfx_synchronize/kfx_pipeline report earlier frames; u8 weight uploads */
 #define KFX_MAX_LEVELS 4
 
 /* status codes */
@@ -345,7 +345,23 @@ int kfx_comm_init(kfx_ctx *ctx, const uint8_t id[KFX_COMM_ID_BYTES]);
  * one GPU or on several with peer access): one pipeline() frame. */
 int kfx_pipeline_group(kfx_ctx **ctxs, int n, const uint8_t *bgr, const float *depth_mm);
 /* kfx_download_tsdf / kfx_download_volume_soa on a slab write its owned slices
- * only (at their global offsets); kfx_upload_tsdf reads its stored slices. */
+ * only (at their global offsets); kfx_upload_tsdf reads its stored slices.
+ * With kfx_set_kernel_timing on the members, kfx_pipeline_group runs them one
+ * after another (each alone on its GPU, as one rank per GPU would) and every
+ * member's kfx_get_kernel_timing_ex reports its own ICP / integrate / local
+ * raycast / combine ms. */
+/* One slab frame with the exchange done by the caller over any transport
+ * (gloo, MPI, ...; a slab context without a communicator):
+ * kfx_slab_frame_local runs pipeline()'s frame on this slab up to its local
+ * raycast and downloads its per-pixel event keys (n = width*height u32) and
+ * {Ts, nx, ny, nz} payload planes (4n u32).  The caller all-reduces the keys
+ * with MIN over the slabs, applies kfx_slab_mask_payload with them, all-reduces
+ * the payload with MAX and passes it to kfx_slab_frame_finish, which rebuilds
+ * the model maps and the pyramid on the device exactly like the RCCL combine
+ * and returns pipeline()'s status. */
+int kfx_slab_frame_local(kfx_ctx *ctx, const uint8_t *bgr, const float *depth_mm, uint32_t *keys,
+                         uint32_t *payload);
+int kfx_slab_frame_finish(kfx_ctx *ctx, const uint32_t *payload);
 
 #ifdef __cplusplus
 }

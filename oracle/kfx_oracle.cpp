@@ -464,6 +464,20 @@ int kfo_icp_track(float **cur_v, float **cur_n, float **pre_v, float **pre_n,
 
 // tsdfhelper::operator() (tsdf_volume.cu:41-99).  Column (x,y) sweeps z=1..Z-1
 // with vc accumulated by repeated float adds (z=0 never updated).
+// One voxel's running average (tsdfhelper, tsdf_volume.cu:72-81), for a
+// voxel that passed sdf >= -trunc.
+void kfo_tsdf_update(int t0, int w0, float sdf, float trunc, int *q_out, int *w_out) {
+  const float ts = std::fmin(1.f, sdf / trunc);
+  const float pre_t = (float)t0 * kDivShortMax;
+  const int pre_w = w0;
+  const int new_w = (pre_w + 1 < kMaxWeight) ? pre_w + 1 : kMaxWeight;
+  const float new_t = std::fma(pre_t, (float)pre_w, ts) / (float)(pre_w + 1);
+  int q = (int)(new_t * (float)kShortMax);
+  q = q < -kShortMax ? -kShortMax : (q > kShortMax ? kShortMax : q);
+  *q_out = q;
+  *w_out = new_w;
+}
+
 void kfo_integrate(int16_t *tsdf, int16_t *weight, uint8_t *rgb, const int dims[3],
                    const float vs[3], float trunc, const kfx_intrinsics *in,
                    const kfx_pose *pose, const float *dmap, const uint8_t *bgr,
@@ -502,13 +516,8 @@ void kfo_integrate(int16_t *tsdf, int16_t *weight, uint8_t *rgb, const int dims[
       const float sdf = -((1.f / lambda) * std::sqrt(dot(vc, vc)) - depth);
       if (sdf >= -trunc) {
         ++cu;
-        const float ts = std::fmin(1.f, sdf / trunc);
-        const float pre_t = (float)tsdf[idx] * kDivShortMax;
-        const int pre_w = weight[idx];
-        const int new_w = (pre_w + 1 < kMaxWeight) ? pre_w + 1 : kMaxWeight;
-        const float new_t = std::fma(pre_t, (float)pre_w, ts) / (float)(pre_w + 1);
-        int q = (int)(new_t * (float)kShortMax);
-        q = q < -kShortMax ? -kShortMax : (q > kShortMax ? kShortMax : q);
+        int q, new_w;
+        kfo_tsdf_update(tsdf[idx], weight[idx], sdf, trunc, &q, &new_w);
         tsdf[idx] = (int16_t)q;
         weight[idx] = (int16_t)new_w;
         if (sdf <= thres_color && sdf >= -thres_color) {
@@ -727,6 +736,7 @@ int64_t kfo_extract_points(const int16_t *tsdf, const int16_t *weight, const int
   auto idx = [&](int x, int y, int z) { return (int64_t)x + (int64_t)y * X + (int64_t)z * slice; };
   const V3 t = {aff->t[0], aff->t[1], aff->t[2]};
   int64_t n = 0;
+  zlo = std::max(zlo, 0), zhi = std::min(zhi, dims[2] - 1);  // a voxel's +z neighbour must exist
   const int a0 = (zlo / 8) * 8;
   for (int c0 = a0; c0 < zhi; c0 += 8)
     for (int ty = 0; ty < Y / 8; ++ty)
@@ -839,6 +849,7 @@ int64_t kfo_extract_mesh(const int16_t *tsdf, const int16_t *weight, const int d
   auto idx = [&](int x, int y, int z) { return (int64_t)x + (int64_t)y * X + (int64_t)z * slice; };
   const V3 t = {aff->t[0], aff->t[1], aff->t[2]};
   int64_t n = 0;
+  zlo = std::max(zlo, 0), zhi = std::min(zhi, dims[2] - 1);  // a cube's upper corners must exist
   for (int c0 = (zlo / 8) * 8; c0 < zhi; c0 += 8)
     for (int ty = 0; ty < Y / 8; ++ty)
       for (int tx = 0; tx < X / 8; ++tx)

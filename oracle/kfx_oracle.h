@@ -80,6 +80,8 @@ void kfo_pose_identity(kfx_pose *out);
  * tsdf int16[N], weight int16[N], rgb u8x4[N]; idx = x + y*X + z*X*Y.
  * cols: optional list of (x,y) pairs to restrict to (NULL = all columns).
  * n_upd / n_col: counts of updated / colour-updated voxels (may be NULL). */
+/* One voxel's tsdf / weight running average (tsdf_volume.cu:72-81). */
+void kfo_tsdf_update(int t0, int w0, float sdf, float trunc, int *q, int *new_w);
 void kfo_integrate(int16_t *tsdf, int16_t *weight, uint8_t *rgb, const int dims[3],
                    const float voxel_size[3], float trunc_dist,
                    const kfx_intrinsics *intr, const kfx_pose *vol2cam,

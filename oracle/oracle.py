@@ -54,6 +54,7 @@ def lib():
         L.kfo_icp_update.restype = i
         L.kfo_pose_mul.argtypes = [P(Pose), P(Pose), P(Pose)]
         L.kfo_pose_inv.argtypes = [P(Pose), P(Pose)]
+        L.kfo_tsdf_update.argtypes = [i, i, f, f, P(i), P(i)]
         L.kfo_integrate.argtypes = [P(C.c_int16), P(C.c_int16), P(C.c_uint8), P(i), P(f), f,
                                     P(Intrinsics), P(Pose), P(f), P(C.c_uint8), P(C.c_int32), C.c_int64,
                                     P(C.c_int64), P(C.c_int64)]
@@ -210,6 +211,13 @@ class Volume:
         self.rgb = np.zeros(4 * X * Y * Z, np.uint8)
         self.range = np.array(range_m, np.float32)
         self.voxel_size = (self.range / self.dims.astype(np.float32)).astype(np.float32)
+
+
+def tsdf_update(t0: int, w0: int, sdf: float, trunc: float) -> tuple:
+    """One voxel's (tsdf, weight) after an update (tsdf_volume.cu:72-81)."""
+    q, w = C.c_int(), C.c_int()
+    lib().kfo_tsdf_update(int(t0), int(w0), float(sdf), float(trunc), C.byref(q), C.byref(w))
+    return q.value, w.value
 
 
 def integrate(vol: Volume, trunc: float, intr: Intrinsics, vol2cam: Pose, dmap_m: np.ndarray,

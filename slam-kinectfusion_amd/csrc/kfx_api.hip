@@ -161,8 +161,11 @@ struct kfx_ctx {
   hipEvent_t ring_h2d[kRing]{}, ring_done[kRing]{};
   bool ring_used[kRing]{};
   int ring_next = 0;
+  bool ring_ready = false;  // every ring resource above created
   hipStream_t cstream = nullptr;
   ncclComm_t comm = nullptr;      // RCCL communicator over the slab ranks (one process per GPU)
+  bool ext_open = false;          // kfx_slab_frame_local done, kfx_slab_frame_finish due
+  hipEvent_t *ext_pending = nullptr;  // that frame's timing sample
 };
 
 namespace {
@@ -322,6 +325,17 @@ void enqueue_map(kfx_ctx *c, FrameInput in, hipEvent_t *ev) {
                  to_dev(c->p.volu_pose), nullptr, c->slab ? c->key_local : nullptr);
 }
 
+// The persistent ICP launch, if this context uses it.  False when it does not,
+// or when the runtime refused the launch (a cooperative grid it cannot make
+// co-resident): the context then takes the per-iteration launches from now on.
+bool try_icp_persistent(kfx_ctx *c, hipStream_t s, int begin) {
+  if (!c->icp_persistent || !c->icp_persistent_enabled) return false;
+  if (launch_icp_track(s, c->icp_plan, c->st, c->icp_sync, begin, c->icp_coop) == hipSuccess) return true;
+  (void)hipGetLastError();
+  c->icp_persistent_enabled = false;
+  return false;
+}
+
 // ICP, integrate and raycast of the frame whose maps are in the current set;
 // begin: the frame's frame_begin has not run yet (overlapped frames)
 int enqueue_track(kfx_ctx *c, FrameInput in, hipEvent_t *ev, bool begin) {
@@ -330,9 +344,7 @@ int enqueue_track(kfx_ctx *c, FrameInput in, hipEvent_t *ev, bool begin) {
   int r = KFX_OK;
   if (c->icp_sharded && c->comm) {
     r = enqueue_icp_sharded(c, begin);
-  } else if (c->icp_persistent && c->icp_persistent_enabled) {
-    launch_icp_track(s, c->icp_plan, c->st, c->icp_sync, begin ? 1 : 0, c->icp_coop);  // folds frame_begin in
-  } else {
+  } else if (!try_icp_persistent(c, s, begin ? 1 : 0)) {  // (the persistent launch folds frame_begin in)
     if (begin) launch_frame_begin(s, c->st, nullptr, c->g[0]);
     for (int level = c->L - 1; level >= 0; --level) {
       for (int it = 0; it < c->p.icp_iter_count[level]; ++it)
@@ -463,16 +475,22 @@ int ensure_graph(kfx_ctx *c, FrameInput in, hipGraphExec_t *graph) {
   return r;
 }
 
+// The event set of this frame's kernel-timing sample (kfx_set_kernel_timing),
+// or null when the frame is not sampled.
+hipEvent_t *timing_sample(kfx_ctx *c) {
+  if (c->timing_every > 0 && !c->profiling && c->frame_seq++ % c->timing_every == 0 &&
+      6 * (c->tnext + 1) <= c->tsets.size())
+    return &c->tsets[6 * c->tnext++];
+  return nullptr;
+}
+
 // graph: the cached executable for this input (built on first use), or null
 // overlap: the input stays valid until the frame completes (staged frames)
 int run_frame(kfx_ctx *c, FrameInput in, hipGraphExec_t *graph, bool overlap = false) {
   int r = ensure_pose_capacity(c, 1);
   if (r) return r;
   c->last_bgr = in.bgr;
-  hipEvent_t *tev = nullptr;  // this frame's timing sample, if sampled
-  if (c->timing_every > 0 && !c->profiling && c->frame_seq++ % c->timing_every == 0 &&
-      6 * (c->tnext + 1) <= c->tsets.size())
-    tev = &c->tsets[6 * c->tnext++];
+  hipEvent_t *tev = timing_sample(c);  // this frame's timing sample, if sampled
   if (overlap && c->overlap && !c->profiling) {
     if ((r = enqueue_frame_overlap(c, in, tev))) return r;
     HIPCHK(hipGetLastError());
@@ -863,15 +881,19 @@ static int pipeline_async(kfx_ctx *c, const uint8_t *bgr, const void *depth, boo
   if (r) return r;
   if (!bgr || !depth) return set_err(KFX_ERR_ARG, "null image");
   const size_t np = (size_t)c->intr.width * c->intr.height;
-  if (!c->ring_host) {  // first use: pinned + device rings, copy stream, events
+  if (!c->ring_ready) {  // first use: pinned + device rings, copy stream, events
+    // (each resource is created once; a failure leaves ring_ready false and
+    // the next call creates only what is still missing)
     c->ring_slot = (np * 4 + np * 3 + 255) & ~(size_t)255;
-    HIPCHK(hipHostMalloc((void **)&c->ring_host, c->ring_slot * kfx_ctx::kRing, hipHostMallocDefault));
-    if ((r = dalloc(c, (void **)&c->ring_dev, c->ring_slot * kfx_ctx::kRing))) return r;
-    HIPCHK(hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
+    if (!c->ring_host)
+      HIPCHK(hipHostMalloc((void **)&c->ring_host, c->ring_slot * kfx_ctx::kRing, hipHostMallocDefault));
+    if (!c->ring_dev && (r = dalloc(c, (void **)&c->ring_dev, c->ring_slot * kfx_ctx::kRing))) return r;
+    if (!c->cstream) HIPCHK(hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
     for (int k = 0; k < kfx_ctx::kRing; ++k) {
-      HIPCHK(hipEventCreateWithFlags(&c->ring_h2d[k], hipEventDisableTiming));
-      HIPCHK(hipEventCreateWithFlags(&c->ring_done[k], hipEventDisableTiming));
+      if (!c->ring_h2d[k]) HIPCHK(hipEventCreateWithFlags(&c->ring_h2d[k], hipEventDisableTiming));
+      if (!c->ring_done[k]) HIPCHK(hipEventCreateWithFlags(&c->ring_done[k], hipEventDisableTiming));
     }
+    c->ring_ready = true;
   }
   const int k = c->ring_next;
   c->ring_next = (k + 1) % kfx_ctx::kRing;
@@ -1198,6 +1220,16 @@ int kfx_upload_tsdf(kfx_ctx *c, const void *src) {
   int r = check_ctx(c);
   if (r) return r;
   if (!src) return set_err(KFX_ERR_ARG, "null src");
+  // refuse before writing anything: every stored record's weight must fit the
+  // u8 weight store, so a refused upload leaves the volume and its raycast
+  // skip maps untouched (the reference never holds weights above 64)
+  {
+    const uint64_t *rec = static_cast<const uint64_t *>(src) + c->vol.slice * (size_t)c->vol.zb;
+    const size_t n = c->vol.slice * (size_t)c->vol.zn;
+    uint64_t any = 0;
+    for (size_t i = 0; i < n; ++i) any |= rec[i] & 0xff000000ull;  // weight bits 24..31 (or its sign)
+    if (any) return set_err(KFX_ERR_ARG, "upload_tsdf: a weight outside 0..255 (u8 weight store; the reference's are 0..64)");
+  }
   HIPCHK(hipStreamSynchronize(c->stream));
   const int nz = slab_z(c, 8);
   uint64_t *tmp = nullptr;
@@ -1222,11 +1254,11 @@ int kfx_upload_tsdf(kfx_ctx *c, const void *src) {
   unsigned nbad = 0;
   HIPCHK(hipMemcpy(&nbad, bad, 4, hipMemcpyDeviceToHost));
   HIPCHK(hipFree(tmp));
-  if (nbad)  // the volume contents are then undefined; the reference never holds such weights
-    return set_err(KFX_ERR_ARG, "upload_tsdf: a weight outside 0..255 (u8 weight store; the reference's are 0..64)");
   launch_occ_rebuild(c->stream, c->vol);  // the raycast's skip maps of the new contents
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(c->stream));
+  if (nbad)  // unreachable after the host check (device-side guard; skip maps rebuilt above)
+    return set_err(KFX_ERR_ARG, "upload_tsdf: a weight outside 0..255 (u8 weight store; the reference's are 0..64)");
   return KFX_OK;
 }
 
@@ -1352,9 +1384,7 @@ int kfx_stage_icp(kfx_ctx *c, kfx_pose *out) {
   s.icp_fail = 0;
   s.icp_pose = identity_pose();
   HIPCHK(hipMemcpyAsync(c->st, &s, sizeof(s), hipMemcpyHostToDevice, c->stream));
-  if (c->icp_persistent && c->icp_persistent_enabled) {
-    launch_icp_track(c->stream, c->icp_plan, c->st, c->icp_sync, 0, c->icp_coop);
-  } else {
+  if (!try_icp_persistent(c, c->stream, 0)) {
     for (int level = c->L - 1; level >= 0; --level) {
       for (int it = 0; it < c->p.icp_iter_count[level]; ++it)
         launch_icp(c->stream, c->g[level], c->cur.v[level], c->cur.n[level], c->prev.v[level],
@@ -1778,6 +1808,7 @@ int kfx_pipeline_group(kfx_ctx **cs, int n, const uint8_t *bgr, const float *dep
   }
   int r;
   const bool sharded = cs[0]->icp_sharded && n > 1;
+  hipEvent_t *tev[kMaxGroup] = {};  // members' timing samples (replicated ICP only)
   for (int k = 0; k < n; ++k) {  // local phase: preprocess, ICP, integrate, slab raycast
     kfx_ctx *c = cs[k];
     if ((r = check_ctx(c))) return r;
@@ -1789,7 +1820,12 @@ int kfx_pipeline_group(kfx_ctx **cs, int n, const uint8_t *bgr, const float *dep
     if (sharded) {
       enqueue_pre(c, {c->raw[0], nullptr, c->bgr}, nullptr);
     } else {
-      enqueue_local(c, {c->raw[0], nullptr, c->bgr}, nullptr);
+      tev[k] = timing_sample(c);
+      enqueue_local(c, {c->raw[0], nullptr, c->bgr}, tev[k]);
+      if (tev[k]) {  // timed: this member runs alone, as on a GPU of its own
+        HIPCHK(hipEventRecord(tev[k][5], c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+      }
     }
     HIPCHK(hipGetLastError());
   }
@@ -1853,6 +1889,7 @@ int kfx_pipeline_group(kfx_ctx **cs, int n, const uint8_t *bgr, const float *dep
     launch_slab_expand(c->stream, c->g[0], c->key_local + np, c->cur, c->prev, c->st, c->pose_log,
                        to_dev(c->p.volu_pose));
     launch_resize(c->stream, c->L, c->g, c->cur, c->prev, c->st, nullptr);
+    if (tev[k]) HIPCHK(hipEventRecord(tev[k][4], c->stream));  // combine = in-process reductions + expand + resize
     HIPCHK(hipGetLastError());
     c->pending += 1;
     const int s = finish_frame(c);
@@ -1861,6 +1898,50 @@ int kfx_pipeline_group(kfx_ctx **cs, int n, const uint8_t *bgr, const float *dep
     else if (s != status) return set_err(KFX_ERR_STATE, "slab members disagree on the tracking status");
   }
   return status;
+}
+
+int kfx_slab_frame_local(kfx_ctx *c, const uint8_t *bgr, const float *depth_mm, uint32_t *keys,
+                         uint32_t *payload) {
+  int r = check_ctx(c);
+  if (r) return r;
+  if (!bgr || !depth_mm || !keys || !payload) return set_err(KFX_ERR_ARG, "null argument");
+  if (!c->slab || c->comm) return set_err(KFX_ERR_STATE, "kfx_slab_frame_local needs a slab context without a communicator");
+  if (c->icp_sharded) return set_err(KFX_ERR_STATE, "the external combine runs the replicated ICP (kfx_set_icp_allreduce 0)");
+  if ((r = ensure_pose_capacity(c, 1))) return r;
+  const size_t np = (size_t)c->intr.width * c->intr.height;
+  HIPCHK(hipStreamSynchronize(c->pstream));  // an overlapped frame's preprocess may still use set 0's inputs
+  set_par(c, 0);
+  HIPCHK(hipMemcpyAsync(c->raw[0], depth_mm, np * 4, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(c->bgr, bgr, np * 3, hipMemcpyHostToDevice, c->stream));
+  c->last_bgr = c->bgr;
+  hipEvent_t *tev = timing_sample(c);
+  enqueue_local(c, {c->raw[0], nullptr, c->bgr}, tev);
+  if (tev) HIPCHK(hipEventRecord(tev[5], c->stream));
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(keys, c->key_local, np * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipMemcpyAsync(payload, c->key_local + np, 4 * np * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  c->ext_pending = tev;
+  c->ext_open = true;
+  return KFX_OK;
+}
+
+int kfx_slab_frame_finish(kfx_ctx *c, const uint32_t *payload) {
+  int r = check_ctx(c);
+  if (r) return r;
+  if (!payload) return set_err(KFX_ERR_ARG, "null payload");
+  if (!c->ext_open) return set_err(KFX_ERR_STATE, "kfx_slab_frame_finish without kfx_slab_frame_local");
+  c->ext_open = false;
+  const size_t np = (size_t)c->intr.width * c->intr.height;
+  uint32_t *pay = c->key_local + np;
+  HIPCHK(hipMemcpyAsync(pay, payload, 4 * np * 4, hipMemcpyHostToDevice, c->stream));
+  launch_slab_expand(c->stream, c->g[0], pay, c->cur, c->prev, c->st, c->pose_log, to_dev(c->p.volu_pose));
+  launch_resize(c->stream, c->L, c->g, c->cur, c->prev, c->st, nullptr);
+  if (c->ext_pending) HIPCHK(hipEventRecord(c->ext_pending[4], c->stream));
+  c->ext_pending = nullptr;
+  HIPCHK(hipGetLastError());
+  c->pending += 1;
+  return finish_frame(c);
 }
 
 }  // extern "C"

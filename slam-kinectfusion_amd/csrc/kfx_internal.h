@@ -200,8 +200,10 @@ IcpPlan make_icp_plan(int levels, const LevelGeom *g, const int *iters, FrameVie
 bool icp_persistent_ok(const IcpPlan &pl, int device);  // grid co-resident + slots fit
 // begin: run the frame's frame_begin inside the launch (no separate kernel)
 // coop: cooperative launch (the runtime guarantees the grid co-resident)
-void launch_icp_track(hipStream_t s, const IcpPlan &pl, DevState *st, IcpSync *sync, int begin = 0,
-                      bool coop = false);
+// Returns the launch error (a refused cooperative launch: the caller falls
+// back to per-iteration launches).
+hipError_t launch_icp_track(hipStream_t s, const IcpPlan &pl, DevState *st, IcpSync *sync, int begin = 0,
+                            bool coop = false);
 // band / nbands: only rows [ye*band/nbands, ye*(band+1)/nbands) of the
 // floor-covered region (a slab rank's share in the sharded ICP mode)
 void launch_icp(hipStream_t s, const LevelGeom &g, const float *cv, const float *cn,

@@ -53,6 +53,9 @@
 #ifndef KFX_INT_MAXCHUNK
 #define KFX_INT_MAXCHUNK 8  // integrate: most z-chunks per column tile
 #endif
+#ifndef KFX_INT_FREE
+#define KFX_INT_FREE 1  // integrate: free-space updates at the tsdf fixed points without divisions
+#endif
 #ifndef KFX_INT_WAVES
 #define KFX_INT_WAVES 12288  // integrate: target wave count (z-chunks per column tile; C2: 3 chunks of 4096 tiles)
 #endif
@@ -886,6 +889,10 @@ __global__ __launch_bounds__(kIcpThreads, 2) void k_icp_track(IcpPlan pl, DevSta
         if (tr && blockIdx.x == 0) sy->trace[slot][2] = wall_clock64();
       }
       __syncthreads();
+      // read before the next two barriers: thread 0 may write sstall again at
+      // the next iteration's poll (blocks that are not `mine` skip the block
+      // reduce and its barrier), but only after every wave has passed them
+      const int stall_seen = sstall;
       // one coherent load per thread (a thread's atomic loads serialise)
       for (int i = threadIdx.x; i < kIcpShards * 27; i += kIcpThreads)
         red.red2[i] = __longlong_as_double((long long)__hip_atomic_load(
@@ -901,13 +908,15 @@ __global__ __launch_bounds__(kIcpThreads, 2) void k_icp_track(IcpPlan pl, DevSta
       __syncthreads();
       if (tr && blockIdx.x == 0) sy->trace[slot][5] = wall_clock64();
       {  // every wave solves (every block, identical result): no broadcast of
-         // the pose through LDS and no barrier after the solve (the next
-         // writes of sums / sumd / red come after the block reduce's barrier)
+         // the pose through LDS and no barrier after the solve.  The next
+         // writes of red come after the block reduce's barrier; sums / sumd are
+         // rewritten only after the next iteration's first two barriers, which
+         // every wave reaches after finishing this solve
         DevPose p = P;
         double x[6];
         int f = icp_update(sumd, p, x);
         if (tr && blockIdx.x == 0) sy->trace[slot][6] = __builtin_amdgcn_readfirstlane((int)x[0]) + wall_clock64();
-        if (sstall) f = 1;  // a stalled block stops; the others stall at the next barrier
+        if (stall_seen) f = 1;  // a stalled block stops; the others stall at the next barrier
         if (threadIdx.x < 27 && blockIdx.x == 0) st->sums[threadIdx.x] = sums[threadIdx.x];
         if (threadIdx.x == 0 && blockIdx.x == 0) {
           if (f) {
@@ -1264,11 +1273,12 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
                                                    DevState *__restrict__ st, DevPose *log,
                                                    DevPose vpose, const float *xpose,
                                                    unsigned long long *counters) {
-  // rtab[d] = RN(1/d), d = 1..65: the weight divisors of the running averages
-  __shared__ float rtab[66];
+  // rtab[d] = RN(1/d), d = 1..256: the weight divisors of the running averages
+  // (stored weights are u8, so pre_w + 1 <= 256 and no divisor falls outside)
+  __shared__ float rtab[257];
   __shared__ DevPose s_pose;
   __shared__ int s_kind;
-  for (int i = threadIdx.x; i < 66; i += KFX_INT_BLOCK) rtab[i] = 1.f / (float)max(1, i);
+  for (int i = threadIdx.x; i < 257; i += KFX_INT_BLOCK) rtab[i] = 1.f / (float)max(1, i);
   if (threadIdx.x == 0) {
     if (xpose) {  // stage seam: explicit vol2cam
       s_kind = 1;
@@ -1527,14 +1537,30 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
       // saturated free space (w = 64 at the tsdf fixed point T* of a ts = 1
       // update, sdf >= trunc so ts = 1 and no colour band): the update is
       // the identity — skip it (same stores skipped as below)
-      if (!ok[j] || (w0[j] == kMaxWeight && t0[j] == v.tsat && sdf[j] >= trunc)) continue;
+      if (!ok[j]) continue;
+#if KFX_INT_FREE
+      // free space (sdf >= trunc, so ts = 1 exactly) at the fixed points of
+      // such updates: the reference's average gives 32767 from weight 0 and
+      // 32766 from t0 in {32766, 32767} at weights 1..64 (every weight it
+      // writes; exhaustive check against the oracle's update,
+      // tests/test_oracle_kat.py) — no divisions, no colour band, q > 0.
+      // Saturated free space (t0 = 32766, w = 64) stores nothing.
+      if (sdf[j] >= trunc && (w0[j] == 0 || (t0[j] >= kShortMax - 1 && w0[j] <= kMaxWeight))) {
+        const int q = w0[j] == 0 ? kShortMax : kShortMax - 1;
+        const int nw = min(w0[j] + 1, kMaxWeight);
+        if (q != t0[j]) mem.st_t(vi[j], (int16_t)q);
+        if (nw != w0[j]) mem.st_w(vi[j], (int16_t)nw);
+        continue;
+      }
+#else
+      if (w0[j] == kMaxWeight && t0[j] == v.tsat && sdf[j] >= trunc) continue;
+#endif
       const Idx i = vi[j];
       const int pre_w = w0[j];
       const float ts = fminf(1.f, div_rn(sdf[j], trunc, v.inv_trunc));
       const float pre_t = (float)t0[j] * kDivShortMax;
       const int new_w = min(pre_w + 1, kMaxWeight);
-      const float new_t = div_rn(fmaf(pre_t, (float)pre_w, ts), (float)(pre_w + 1),
-                                 (unsigned)pre_w <= (unsigned)kMaxWeight ? rtab[pre_w + 1] : 1.f / (float)(pre_w + 1));
+      const float new_t = div_rn(fmaf(pre_t, (float)pre_w, ts), (float)(pre_w + 1), rtab[pre_w + 1]);
       int q = (int)(new_t * (float)kShortMax);
       q = max(-kShortMax, min(kShortMax, q));
       if (q < 0) {
@@ -1556,7 +1582,7 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
         const uint32_t c0 = mem.ld_c(i);
         const uint8_t *px = bgr + 3 * (size_t)(pix[j] >> 3);
         const float c = (float)(new_w + 1);
-        const float rc = (unsigned)new_w <= (unsigned)kMaxWeight ? rtab[new_w + 1] : 1.f / c;
+        const float rc = rtab[new_w + 1];
         uint32_t out = 0u;
 #pragma unroll
         for (int ch = 0; ch < 3; ++ch) {
@@ -2925,7 +2951,7 @@ bool icp_persistent_ok(const IcpPlan &pl, int device) {
   return (long long)per_cu * cus >= pl.nblocks;
 }
 
-void launch_icp_track(hipStream_t s, const IcpPlan &pl, DevState *st, IcpSync *sync, int begin, bool coop) {
+hipError_t launch_icp_track(hipStream_t s, const IcpPlan &pl, DevState *st, IcpSync *sync, int begin, bool coop) {
   if (coop) {
     // the runtime guarantees the grid co-resident (or fails the launch), so
     // the grid barrier cannot wait on an unscheduled block (~15 us slower)
@@ -2934,11 +2960,11 @@ void launch_icp_track(hipStream_t s, const IcpPlan &pl, DevState *st, IcpSync *s
     IcpSync *a2 = sync;
     int a3 = begin;
     void *args[] = {&a0, &a1, &a2, &a3};
-    (void)hipLaunchCooperativeKernel(reinterpret_cast<const void *>(k_icp_track), dim3(pl.nblocks),
-                                     dim3(kIcpThreads), args, 0, s);
-    return;
+    return hipLaunchCooperativeKernel(reinterpret_cast<const void *>(k_icp_track), dim3(pl.nblocks),
+                                      dim3(kIcpThreads), args, 0, s);
   }
   hipLaunchKernelGGL(k_icp_track, dim3(pl.nblocks), dim3(kIcpThreads), 0, s, pl, st, sync, begin);
+  return hipGetLastError();
 }
 
 void launch_icp(hipStream_t s, const LevelGeom &g, const float *cv, const float *cn,

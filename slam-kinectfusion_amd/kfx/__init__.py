@@ -34,7 +34,7 @@ EXPORTS = [
     "kfx_upload_tsdf", "kfx_download_volume_soa", "kfx_stage_preprocess", "kfx_stage_icp_accumulate",
     "kfx_stage_icp", "kfx_stage_integrate", "kfx_stage_raycast", "kfx_set_profiling", "kfx_get_stage_ms",
     "kfx_integrate_counts", "kfx_integrate_stats", "kfx_raycast_stats", "kfx_download_columns", "kfx_pipeline_async", "kfx_pipeline_async_u16", "kfx_slab_mask_payload", "kfx_slab_expand", "kfx_set_icp_allreduce", "kfx_create_slab", "kfx_slab_info", "kfx_comm_get_unique_id", "kfx_comm_init",
-    "kfx_pipeline_group", "kfx_render", "kfx_volume_checksum", "kfx_extract_points", "kfx_write_ply", "kfx_save_pointcloud",
+    "kfx_pipeline_group", "kfx_slab_frame_local", "kfx_slab_frame_finish", "kfx_render", "kfx_volume_checksum", "kfx_extract_points", "kfx_write_ply", "kfx_save_pointcloud",
     "kfx_extract_mesh", "kfx_write_ply_mesh",
     "kfx_dataset_open", "kfx_dataset_info", "kfx_dataset_read", "kfx_dataset_close", "kfx_png_info",
     "kfx_png_read_bgr8", "kfx_png_read_depth", "kfx_parse_intr",
@@ -113,6 +113,8 @@ def lib():
         "kfx_comm_get_unique_id": ([P(C.c_uint8)], i),
         "kfx_comm_init": ([vp, P(C.c_uint8)], i),
         "kfx_pipeline_group": ([P(vp), i, P(C.c_uint8), P(f)], i),
+        "kfx_slab_frame_local": ([vp, P(C.c_uint8), P(f), P(C.c_uint32), P(C.c_uint32)], i),
+        "kfx_slab_frame_finish": ([vp, P(C.c_uint32)], i),
         "kfx_extract_points": ([vp, P(f), C.c_int64, P(C.c_int64)], i),
         "kfx_render": ([vp, i, P(C.c_uint8)], i),
         "kfx_volume_checksum": ([vp, P(C.c_uint64)], i),
@@ -475,6 +477,25 @@ class KinectFusion:
         a = [C.c_int() for _ in range(4)]
         _check(lib().kfx_slab_info(self._h, *[C.byref(x) for x in a]), "kfx_slab_info")
         return tuple(x.value for x in a)
+
+    def slab_frame_local(self, color: np.ndarray, depth: np.ndarray):
+        """Slab frame up to the local raycast (kfx_slab_frame_local): returns this
+        slab's (keys (n,) u32, payload (4, n) u32) for an exchange by the caller."""
+        color = np.ascontiguousarray(color, np.uint8)
+        d = np.ascontiguousarray(depth, np.float32)
+        n = self.intr.width * self.intr.height
+        keys = np.zeros(n, np.uint32)
+        pay = np.zeros((4, n), np.uint32)
+        u32p = C.POINTER(C.c_uint32)
+        _check(lib().kfx_slab_frame_local(self._h, u8ptr(color), fptr(d), keys.ctypes.data_as(u32p),
+                                          pay.ctypes.data_as(u32p)), "kfx_slab_frame_local")
+        return keys, pay
+
+    def slab_frame_finish(self, payload: np.ndarray) -> int:
+        """Finish the frame from the MAX-combined payload (kfx_slab_frame_finish)."""
+        pay = np.ascontiguousarray(payload, np.uint32)
+        rc = lib().kfx_slab_frame_finish(self._h, pay.ctypes.data_as(C.POINTER(C.c_uint32)))
+        return _check(rc, "kfx_slab_frame_finish", ok=(KFX_OK, KFX_TRACKING_LOST))
 
     def comm_init(self, uid: bytes):
         buf = (C.c_uint8 * 128).from_buffer_copy(uid)

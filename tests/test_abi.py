@@ -27,7 +27,7 @@ def test_library_exports_every_declared_symbol(kfx_lib):
     L = C.CDLL(kfx_lib.LIB_PATH)
     missing = [s for s in declared_symbols() if not hasattr(L, s)]
     assert not missing, missing
-    assert kfx_lib.lib().kfx_abi_version() == 1
+    assert kfx_lib.lib().kfx_abi_version() == 2
 
 
 def test_library_is_gfx950_code_object(kfx_lib):

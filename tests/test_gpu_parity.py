@@ -186,6 +186,41 @@ def test_integrate_512_column_spot_check(n, seq_vga):
     kf.close()
 
 
+def test_c3_pipeline_two_frames_match_oracle(seq_vga):
+    """BASELINE C3 at full size (640x480, 1024^3 @ 2 mm, 2^30 voxels on the
+    32-bit-offset path) through the whole pipeline: the bootstrap frame and one
+    tracked frame (19 ICP iterations against the 1024^3 raycast), against the
+    serial oracle's pipeline (8 GiB of host volume).  Poses, every level of the
+    raycast model maps, and 3000 sampled columns of the volume."""
+    bgr, dep, _ = seq_vga
+    intr = synth.Intrinsics.vga()
+    I = Intrinsics.from_any(intr)
+    n = 1024
+    kf, p = make(intr, dims=n)
+    pipe = O.Pipeline(I, p)
+    for k in range(2):
+        d = dep[k].astype(np.float32)
+        assert kf.pipeline(bgr[k], d) == pipe.process(bgr[k], d) == KFX_OK
+    gp, op = kf.pose_record, pipe.poses()
+    assert gp.shape == op.shape == (2, 4, 4)
+    err = np.abs(gp - op).max()
+    assert err <= 1e-6, err  # 0 measured at 128^3 / 512^3 (Rodrigues cos/sin: <= 1 ulp in double)
+    if err == 0:
+        for l in range(3):
+            _, gv, gn = kf.frame_maps(KFX_FRAME_PREV, l)
+            assert feq(gv, pipe.map(1, 1, l)), f"vmap level {l}: {mismatch(gv, pipe.map(1, 1, l))} differ"
+            assert feq(gn, pipe.map(1, 2, l)), f"nmap level {l}"
+        rng = np.random.default_rng(11)
+        cols = np.unique(np.stack([rng.integers(0, n, 3000), rng.integers(0, n, 3000)], 1).astype(np.int32), axis=0)
+        gt_, gw, gc = kf.download_columns(cols)
+        ot, ow, oc = pipe.volume()
+        idx = (cols[:, 0][:, None] + n * cols[:, 1][:, None] + n * n * np.arange(n, dtype=np.int64)[None, :])
+        assert np.array_equal(gt_, ot[idx]) and np.array_equal(gw, ow[idx])
+        assert np.array_equal(gc.reshape(-1, n, 4), oc.reshape(-1, 4)[idx])
+        assert (gw > 0).sum() > 10000
+    kf.close()
+
+
 def test_raycast_bit_exact(seq_qvga):
     bgr, dep, gt = seq_qvga
     intr = synth.Intrinsics.qvga()

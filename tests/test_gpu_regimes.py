@@ -104,10 +104,15 @@ def test_upload_rejects_weights_outside_u8():
     kf.upload_tsdf(records(t, w, c))
     gt, gw, _ = kf.volume_soa()
     assert gw[12345] == 255 and gt[12345] == -77 and (gw != 0).sum() == 1
+    t[54321] = -5  # would be written by an accepted upload
     for bad in (256, -1):
         w[999] = bad
         with pytest.raises(KfxError, match="0..255"):
             kf.upload_tsdf(records(t, w, c))
+        # refused before anything is written: the previous contents (and so
+        # the raycast skip maps built for them) are untouched
+        gt, gw, _ = kf.volume_soa()
+        assert gw[12345] == 255 and gt[12345] == -77 and (gw != 0).sum() == 1 and gt[54321] == 0
     kf.close()
 
 

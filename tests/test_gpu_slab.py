@@ -234,3 +234,77 @@ def test_c5_full_size_slabs_on_one_gpu():
         assert bits_equal(mv, gv) and bits_equal(mn, gn)
     for m in members:
         m.close()
+
+
+# ---- multi-process: one libkfx slab context per process, exchange over gloo --
+
+def _mp_rank(rank, world, port, out_dir, n_frames):
+    """One slab rank: the HIP pipeline up to its local raycast
+    (kfx_slab_frame_local: preprocess, ICP, integrate, slab raycast kernels),
+    keys all-reduced MIN and the payload MAX over torch.distributed (gloo),
+    libkfx's kfx_slab_mask_payload between them, then kfx_slab_frame_finish
+    (expand + pyramid on the device).  Writes its poses, maps and owned voxels."""
+    import os as _os
+    import sys as _sys
+    root = _os.path.dirname(_os.path.dirname(_os.path.abspath(__file__)))
+    for p in (_os.path.join(root, "slam-kinectfusion_amd"), _os.path.join(root, "oracle")):
+        if p not in _sys.path:
+            _sys.path.insert(0, p)
+    import numpy as _np
+    import torch
+    import torch.distributed as dist
+    from kfx import KFX_FRAME_PREV as PREV, KinectFusion as KF, slab_mask_payload, synth as S
+    from kfx.abi import Intrinsics as I_, default_params as dp
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    bgr, dep, _ = S.sequence(n_frames, S.Intrinsics.qvga(), noise=True, dropout=0.01)
+    p = dp(dims=64, range_m=L_VOL)
+    kf = KF(I_.from_any(S.Intrinsics.qvga()), p, slab=(rank, world))
+    st = []
+    for k in range(n_frames):
+        keys, pay = kf.slab_frame_local(bgr[k], dep[k].astype(_np.float32))
+        kt = torch.from_numpy(keys.astype(_np.int64))
+        dist.all_reduce(kt, op=dist.ReduceOp.MIN)
+        pay = slab_mask_payload(keys, kt.numpy().astype(_np.uint32), pay)
+        pt = torch.from_numpy(pay.astype(_np.int64))
+        dist.all_reduce(pt, op=dist.ReduceOp.MAX)
+        st.append(kf.slab_frame_finish(pt.numpy().astype(_np.uint32)))
+    maps = [kf.frame_maps(PREV, l)[1:] for l in range(3)]
+    t, w, c = kf.volume_soa()
+    _np.savez(_os.path.join(out_dir, f"rank{rank}.npz"), poses=kf.pose_record, status=_np.array(st),
+              slab=_np.array(kf.slab_info()), t=t, w=w, c=c,
+              **{f"v{l}": m[0] for l, m in enumerate(maps)}, **{f"n{l}": m[1] for l, m in enumerate(maps)})
+    kf.close()
+    dist.destroy_process_group()
+
+
+def test_slab_two_processes_gloo_match_single_volume(seq_qvga, tmp_path):
+    """DESIGN.md §7 across processes: two processes, each with its own libkfx
+    slab context on the GPU (HIP integrate + slab raycast per rank), exchange
+    the raycast keys and payload over gloo; both end every frame with the single
+    volume's poses and maps, and their owned voxels reassemble its volume."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    n = 6
+    mp.spawn(_mp_rank, args=(2, port, str(tmp_path), n), nprocs=2, join=True)
+    bgr, dep, _ = seq_qvga
+    p = default_params(dims=64, range_m=L_VOL)
+    single, st = _single(synth.Intrinsics.qvga(), p, bgr[:n], dep[:n])
+    t, w, c = single.volume_soa()
+    sl = 64 * 64
+    ts, ws, cs = np.zeros_like(t), np.zeros_like(w), np.zeros_like(c)
+    for r in range(2):
+        d = np.load(tmp_path / f"rank{r}.npz")
+        assert list(d["status"]) == st == [KFX_OK] * n
+        assert np.array_equal(d["poses"], single.pose_record)
+        for l in range(3):
+            _, gv, gn = single.frame_maps(KFX_FRAME_PREV, l)
+            assert bits_equal(d[f"v{l}"], gv) and bits_equal(d[f"n{l}"], gn), f"rank {r} level {l}"
+        zb, zn, o0, o1 = (int(x) for x in d["slab"])
+        ts[o0 * sl:o1 * sl], ws[o0 * sl:o1 * sl] = d["t"][o0 * sl:o1 * sl], d["w"][o0 * sl:o1 * sl]
+        cs[4 * o0 * sl:4 * o1 * sl] = d["c"][4 * o0 * sl:4 * o1 * sl]
+    assert np.array_equal(ts, t) and np.array_equal(ws, w) and np.array_equal(cs, c) and w.any()
+    single.close()

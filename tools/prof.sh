@@ -2,7 +2,7 @@
 # One profiling session on the GPU box (run from the repo root through gpurun):
 #   1. rocprofv3 --kernel-trace --stats of a short bench run  -> gpurun_out/prof/stats
 #   2. FETCH_SIZE / WRITE_SIZE calibration streams             -> gpurun_out/prof/calib
-#   3. FETCH_SIZE and WRITE_SIZE passes over the same bench    -> gpurun_out/prof/pmc
+#   3. FETCH_SIZE, WRITE_SIZE and SQ issue passes over the same bench -> gpurun_out/prof/pmc
 # Every rocprofv3 run is its own process under its own time limit; counters are
 # never combined with trace domains (MI355X_MICROARCH.md, rocprofv3 section).
 # usage: tools/prof.sh [bench args...]
@@ -35,4 +35,7 @@ if [ -x "$ROOT/tools/build/pmc_calib" ]; then
 fi
 run pmc_fetch 240 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc/FETCH_SIZE" -- python3 "$ROOT/bench.py" $PMC_ARGS
 run pmc_write 240 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc/WRITE_SIZE" -- python3 "$ROOT/bench.py" $PMC_ARGS
+# issue counters (8 SQ slots + GRBM): VALU issue fraction next to the HBM fraction
+run pmc_sq 240 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY \
+    SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc/SQ" -- python3 "$ROOT/bench.py" $PMC_ARGS
 PROF_ARGS="$ARGS" python3 "$ROOT/tools/traffic.py" "$OUT" --commit

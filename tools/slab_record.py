@@ -1,0 +1,111 @@
+#!/usr/bin/env python3
+"""Multi-GPU readiness record on ONE GPU: the Z-slab split
+of BASELINE C4 (1024^3 @ 2 mm, 640x480) or C5 (2048^3 @ 2 mm, 1280x720) over
+8 slab contexts held in one process (kfx_pipeline_group), next to the single
+volume on the same frames.  With kernel timing on, the group runs its members
+one after another, each alone on the GPU as on a GPU of its own, and every
+member reports its ICP / integrate / local raycast / combine ms (HIP events on
+its stream) and its integrate work (kfx_integrate_stats: updated voxels of the
+last frame).  The combine here is the in-process one (one reduction kernel
+over the members' buffers + mask + expand + pyramid), not RCCL.
+
+usage: python3 tools/slab_record.py c4|c5 [--world 8] [--frames 20] [--warmup 5] [--out FILE]"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "slam-kinectfusion_amd"))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("config", choices=["c4", "c5"])
+    ap.add_argument("--world", type=int, default=8)
+    ap.add_argument("--frames", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    import kfx
+    from kfx import synth
+    from kfx.abi import Intrinsics, default_params
+    from bench import CONFIGS, intrinsics
+    W, H, n, L = CONFIGS[a.config]
+    intr = intrinsics(W, H)
+    p = default_params(dims=n, range_m=L)
+    unique = 16
+    bgr, dep, _ = synth.sequence(unique, intr, L=L, noise=True, traj_seed=7, dropout=0.005)
+    dep = dep.astype(np.float32)
+    order = synth.ping_pong(unique, a.warmup + a.frames)
+    I = Intrinsics.from_any(intr)
+    rec = {"config": a.config, "width": W, "height": H, "volume_dims": n, "volume_range_m": L, "world": a.world,
+           "frames_timed": a.frames, "warmup": a.warmup, "lib_sha256": None,
+           "method": "8 slab contexts on one GPU (kfx_pipeline_group); timed members run alone, one after "
+                     "another; HIP events on each member's stream; combine = in-process reductions + expand + "
+                     "pyramid (not RCCL)"}
+    import hashlib
+    rec["lib_sha256"] = hashlib.sha256(open(kfx.LIB_PATH, "rb").read()).hexdigest()
+
+    # the single volume on the same host frames
+    single = kfx.KinectFusion(I, p)
+    for i in order[:a.warmup]:
+        single.pipeline(bgr[i], dep[i])
+    single.set_kernel_timing(1, a.frames + 2)
+    t0 = time.perf_counter()
+    for i in order[a.warmup:a.warmup + a.frames]:
+        assert single.pipeline(bgr[i], dep[i]) == kfx.KFX_OK
+    t_single = time.perf_counter() - t0
+    ks = single.kernel_timing()
+    ws = single.integrate_stats()
+    rec["single"] = {"icp_ms": ks["icp"], "integrate_ms": ks["integrate"], "raycast_ms": ks["raycast"],
+                     "integrate_updated": ws["updated"], "wall_ms_per_frame": 1e3 * t_single / a.frames}
+    sp = single.pose_record
+    single.close()
+
+    members = [kfx.KinectFusion(I, p, slab=(r, a.world)) for r in range(a.world)]
+    for i in order[:a.warmup]:
+        kfx.pipeline_group(members, bgr[i], dep[i])
+    for m in members:
+        m.set_kernel_timing(1, a.frames + 2)
+    t0 = time.perf_counter()
+    for i in order[a.warmup:a.warmup + a.frames]:
+        assert kfx.pipeline_group(members, bgr[i], dep[i]) == kfx.KFX_OK
+    t_group = time.perf_counter() - t0
+    slabs = []
+    for r, m in enumerate(members):
+        k = m.kernel_timing()
+        w = m.integrate_stats()
+        zb, zn, o0, o1 = m.slab_info()
+        slabs.append({"rank": r, "owned_slices": [o0, o1], "stored_slices": [zb, zb + zn],
+                      "icp_ms": k["icp"], "integrate_ms": k["integrate"], "raycast_local_ms": k["raycast_local"],
+                      "combine_ms": k["combine"], "integrate_updated": w["updated"], "samples": k["samples"]})
+    assert all(np.array_equal(m.pose_record, sp) for m in members), "slab poses differ from the single volume"
+    for m in members:
+        m.close()
+    it = np.array([s["integrate_ms"] for s in slabs])
+    up = np.array([s["integrate_updated"] for s in slabs], dtype=np.float64)
+    rec["slabs"] = slabs
+    rec["group_wall_ms_per_frame"] = 1e3 * t_group / a.frames
+    rec["integrate_imbalance_max_over_mean"] = float(it.max() / it.mean())
+    rec["updated_imbalance_max_over_mean"] = float(up.max() / up.mean())
+    rec["max_slab_over_single_integrate"] = float(it.max() / rec["single"]["integrate_ms"])
+    rec["ideal"] = 1.0 / a.world
+    # per-rank critical path of one frame at N GPUs (replicated ICP, RCCL not included)
+    crit = [s["icp_ms"] + s["integrate_ms"] + s["raycast_local_ms"] for s in slabs]
+    rec["max_rank_icp_integrate_raycast_ms"] = float(max(crit))
+    rec["single_icp_integrate_raycast_ms"] = float(sum(rec["single"][k] for k in ("icp_ms", "integrate_ms",
+                                                                                    "raycast_ms")))
+    out = a.out or os.path.join(ROOT, "gpurun_out", f"slabs_{a.config}.json")
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    json.dump(rec, open(out, "w"), indent=1)
+    print(json.dumps({k: rec[k] for k in ("config", "integrate_imbalance_max_over_mean",
+                                          "max_slab_over_single_integrate", "ideal")}))
+
+
+if __name__ == "__main__":
+    main()

@@ -10,9 +10,11 @@ FETCH_SIZE / WRITE_SIZE are converted to bytes with the calibration factors of
 the 2-byte streams (the width of the tsdf/weight arrays that dominate integrate
 and raycast): factor = counter value per dispatch / bytes the stream moved
 (MI355X_MICROARCH.md: only 16-B/lane streams are calibrated there, other widths
-must be calibrated on a known byte count).  Output: <dir>/traffic.json, and
-profiles/integrate_pmc.json when --commit is given (bench.py reads that file
-for roofline.traffic).
+must be calibrated on a known byte count).  The SQ pass (pmc/SQ) gives the
+issue figures of integrate and raycast (VALU issue fraction, wave-cycle split).
+Output: <dir>/traffic.json, and profiles/$PMC_RECORD (default
+r03_integrate_pmc.json) when --commit is given: bench.py attaches it as
+roofline.traffic only to a run that loaded the library it names by sha256.
 """
 import collections
 import csv
@@ -65,11 +67,13 @@ def main():
         if "read_bytes" in rec and "write_bytes" in rec:
             rec["hbm_bytes_per_launch"] = rec["read_bytes"] + rec["write_bytes"]
         out["kernels"][k] = rec
-    json.dump(out, open(f"{root}/traffic.json", "w"), indent=1)
     for k, r in out["kernels"].items():
         if k.startswith("k_"):
             print(f"{k:40s} n={r['dispatches']:5d} hbm/launch={r.get('hbm_bytes_per_launch', float('nan')) / 1e6:10.2f} MB")
-    if commit:  # profiles/r02_integrate_pmc.json: what bench.py attaches as roofline.traffic
+    sq = {k: v for k, v in per_counter(f"{root}/pmc/SQ").items()}
+    out["sq"] = sq
+    json.dump(out, open(f"{root}/traffic.json", "w"), indent=1)
+    if commit:  # profiles/<round>_integrate_pmc.json: what bench.py attaches as roofline.traffic
         integ = [r for k, r in out["kernels"].items()
                  if k.startswith("k_integrate<false") and "hbm_bytes_per_launch" in r]
         if integ:
@@ -81,23 +85,79 @@ def main():
             steps, warmup, dims = arg("--steps", 300), arg("--warmup", 20), arg("--dims", 512)
             r = max(integ, key=lambda r: r["dispatches"])
             ray = [rr for k, rr in out["kernels"].items() if k.startswith("k_raycast<true, false, false>")]
-            prof = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles")
-            json.dump({"kernel": "k_integrate", "hbm_bytes_per_launch": int(r["hbm_bytes_per_launch"]),
-                       "read_bytes": int(r["read_bytes"]), "write_bytes": int(r["write_bytes"]),
-                       "dispatches": r["dispatches"], "factor_units_per_byte": fac,
-                       "raycast_hbm_bytes_per_launch": int(ray[0]["hbm_bytes_per_launch"]) if ray and
-                       "hbm_bytes_per_launch" in ray[0] else None,
-                       "workload": [dims, 640, 480], "steps": steps, "warmup": warmup,
-                       "command": "python3 bench.py " + " ".join(args),
-                       "regime": ("mean over every dispatch of the run: %d warm-up + %d timed + 20 profiled "
-                                  "frames%s" % (warmup, steps, " (unsaturated transient: < 64 frames)"
-                                                if warmup + steps + 20 < 64 else "")),
-                       "source": "tools/prof.sh FETCH_SIZE/WRITE_SIZE passes, 2-byte stream calibration"},
-                      open(os.path.join(prof, "r02_integrate_pmc.json"), "w"), indent=1)
+            lib = os.environ.get("KFX_LIB_PATH") or os.path.join(REPO, "slam-kinectfusion_amd", "lib", "libkfx.so")
+            rec = {"kernel": "k_integrate", "hbm_bytes_per_launch": int(r["hbm_bytes_per_launch"]),
+                   "read_bytes": int(r["read_bytes"]), "write_bytes": int(r["write_bytes"]),
+                   "dispatches": r["dispatches"], "factor_units_per_byte": fac,
+                   "raycast_hbm_bytes_per_launch": int(ray[0]["hbm_bytes_per_launch"]) if ray and
+                   "hbm_bytes_per_launch" in ray[0] else None,
+                   "workload": [dims, 640, 480], "steps": steps, "warmup": warmup,
+                   "command": "python3 bench.py " + " ".join(args),
+                   "regime": ("mean over every dispatch of the run: %d warm-up + %d timed + profiled "
+                              "frames%s" % (warmup, steps, " (unsaturated transient: < 64 frames)"
+                                            if warmup + steps + 20 < 64 else "")),
+                   "source": "tools/prof.sh FETCH_SIZE/WRITE_SIZE passes, 2-byte stream calibration",
+                   # the library the counters were collected on: bench.py attaches this
+                   # record only to a run that loaded the same file
+                   "lib": os.path.relpath(lib, REPO), "lib_sha256": sha256(lib),
+                   "commit": os.environ.get("KFX_COMMIT")}
+            for k, name in (("k_integrate<false, true>", "integrate_sq"), ("k_raycast<true, false, false>", "raycast_sq")):
+                if k in sq:
+                    rec[name] = sq_issue(sq[k])
+            name = os.environ.get("PMC_RECORD", "r03_integrate_pmc.json")
+            json.dump(rec, open(os.path.join(REPO, "profiles", name), "w"), indent=1)
             # a copy beside the counters (profiles/ does not come back from the GPU box)
-            json.dump(json.load(open(os.path.join(prof, "r02_integrate_pmc.json"))),
-                      open(os.path.join(root, "r02_integrate_pmc.json"), "w"), indent=1)
+            json.dump(rec, open(os.path.join(root, name), "w"), indent=1)
 
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+N_SIMD = 1024  # 256 CUs x 4 SIMDs (MI355X_MICROARCH.md)
+
+
+def sha256(path):
+    import hashlib
+    try:
+        return hashlib.sha256(open(path, "rb").read()).hexdigest()
+    except OSError:
+        return None
+
+
+def per_counter(root):
+    """{kernel: {counter: mean per dispatch, "dispatches": n}} over a pass directory."""
+    agg = collections.defaultdict(lambda: collections.defaultdict(list))
+    for f in glob.glob(f"{root}/**/*counter_collection.csv", recursive=True):
+        for r in csv.DictReader(open(f)):
+            agg[short(r.get("Kernel_Name", "?"))][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    out = {}
+    for k, d in agg.items():
+        out[k] = {c: sum(v) / len(v) for c, v in d.items()}
+        out[k]["dispatches"] = max(len(v) for v in d.values())
+    return out
+
+
+def sq_issue(d):
+    """Issue figures of one kernel from the SQ pass (means per dispatch).
+    GRBM_GUI_ACTIVE sums the busy cycles of the 8 XCDs, so the dispatch spans
+    GRBM_GUI_ACTIVE / 8 shader cycles on each of the 1024 SIMDs; a wave64 VALU
+    instruction occupies its SIMD for 2 cycles (MI355X_MICROARCH.md, wave
+    scheduling), SQ_ACTIVE_INST_VALU counts quad-cycles summed over waves."""
+    cyc = d.get("GRBM_GUI_ACTIVE", 0.0) / 8.0
+    rec = {c: d[c] for c in sorted(d) if c != "dispatches"}
+    rec["dispatches"] = d.get("dispatches")
+    if cyc > 0:
+        rec["kernel_cycles"] = cyc
+        if "SQ_INSTS_VALU" in d:
+            rec["valu_issue_frac_2cyc"] = round(2.0 * d["SQ_INSTS_VALU"] / (N_SIMD * cyc), 4)
+        if "SQ_ACTIVE_INST_VALU" in d:
+            rec["valu_active_frac"] = round(4.0 * d["SQ_ACTIVE_INST_VALU"] / (N_SIMD * cyc), 4)
+    if d.get("SQ_WAVES"):
+        rec["valu_insts_per_wave"] = round(d.get("SQ_INSTS_VALU", 0.0) / d["SQ_WAVES"], 1)
+    if d.get("SQ_WAVE_CYCLES"):
+        w = d["SQ_WAVE_CYCLES"]
+        rec["wave_cycles_split"] = {k: round(d.get(c, 0.0) / w, 4) for k, c in
+                                    (("active_inst_any", "SQ_ACTIVE_INST_ANY"), ("wait_any", "SQ_WAIT_ANY"),
+                                     ("wait_inst_any", "SQ_WAIT_INST_ANY"))}
+    return rec
 
 if __name__ == "__main__":
     main()
