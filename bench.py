@@ -83,6 +83,8 @@ def parse():
     ap.add_argument("--replicas", type=int, default=1,
                     help="slab mode at N>1: time independent replica streams first (the fallback line)")
     ap.add_argument("--zslab-timeout", type=float, default=300.0)
+    ap.add_argument("--extract", type=int, default=1,
+                    help="N=1: time point extraction and marching cubes on the final volume (0 = skip)")
     ap.add_argument("--c3-frames", type=int, default=20,
                     help="N=1, C2: timed frames of the C3 record (1024^3 @ 2 mm, same frames; 0 = skip)")
     return ap.parse_args()
@@ -322,6 +324,29 @@ def integrate_roofline(work, ms, W, H, ms_source, traffic=None, traffic_src=None
             "achieved_ref_format": round(achieved_ref, 1), "avg_launch_ms": round(ms, 4), "launch_ms_source": ms_source}
 
 
+def extract_record(kf, n):
+    """Surface extraction off the per-frame path (C5 names the
+    marching-cubes extract): kfx_extract_points (FullScan6 zero crossings,
+    tsdf_volume.cu:307-481) and kfx_extract_mesh on the volume the timed frames
+    built; device ms of the count pass, the offset scan and the emit pass
+    (HIP events).  Roofline: each pass reads every scanned voxel's int16 tsdf +
+    u8 weight (3 B; neighbours come from cache), the emit pass also writes
+    12 B per point / 36 B per triangle."""
+    vox = n * n * (n - 1)  # z = 0 .. Z-2 (the +z neighbour must exist)
+    out = {"voxels_scanned": vox, "peak": HBM_PEAK_GBS, "unit": "GB/s"}
+    for name, fn, per in (("points", kf.extract_points, 12), ("mesh", kf.extract_mesh, 36)):
+        items = fn(cap=50_000_000)
+        ms = kf.extract_ms()
+        b = 2 * 3 * vox + per * len(items)
+        t = ms["count"] + ms["scan"] + ms["emit"]
+        out[name] = {"items": int(len(items)), "count_ms": round(ms["count"], 4), "scan_ms": round(ms["scan"], 4),
+                     "emit_ms": round(ms["emit"], 4), "algorithmic_bytes": int(b),
+                     "achieved": round(b / (t * 1e-3) / 1e9, 1) if t > 0 else None,
+                     "frac": round(b / (t * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if t > 0 else None}
+        del items
+    return out
+
+
 def round_ms(d):
     return {k: round(v, 4) if isinstance(v, float) else v for k, v in d.items()} if d else None
 
@@ -466,8 +491,12 @@ def measure_main(a, name, intr, params, frames, D, rank, world, local, mode, icp
     host_in = None
     if a.host_frames > 0 and mode == "single":
         unique = len(bgr)
-        hb = [np.ascontiguousarray(bgr[i]) for i in range(unique)]
-        hd = [np.ascontiguousarray(dep[i]) for i in range(unique)]
+        hb = np.ascontiguousarray(bgr)
+        hd = np.ascontiguousarray(dep)
+        # zero copy: the frames' host memory is page-locked once, then every
+        # frame is DMAed straight from it (no staging copy on the host)
+        kf.register_host_buffer(hb)
+        kf.register_host_buffer(hd)
         ho = synth.ping_pong(unique, a.host_frames)
         kf.synchronize()
         D.barrier()
@@ -476,12 +505,15 @@ def measure_main(a, name, intr, params, frames, D, rank, world, local, mode, icp
             kf.pipeline_async(hb[i], hd[i])
         st_h = kf.synchronize()
         dt_h = D.max(time.perf_counter() - t0)
+        kf.unregister_host_buffer(hb)
+        kf.unregister_host_buffer(hd)
         host_in = {"value": round(len(ho) * world / dt_h, 3), "unit": "frames/s",
                    "ms_per_step": round(1000.0 * dt_h / len(ho), 4), "frames": len(ho),
                    "status": "ok" if st_h == kfx.KFX_OK else "tracking lost",
                    "bytes_per_frame_h2d": W * H * 7,
-                   "path": "kfx_pipeline_async: host frame -> pinned 4-slot ring -> H2D on a copy stream "
-                           "overlapped with the previous frame; f32 depth mm + BGR8"}
+                   "path": "kfx_pipeline_async from host buffers registered with kfx_register_host_buffer: "
+                           "H2D straight from the caller's page-locked frames on a copy stream, overlapped with "
+                           "the previous frame (no host copy); f32 depth mm + BGR8"}
 
     # per-stage device ms on further frames (profiled, eager; single volume)
     stages = {k: [] for k in ("preprocess", "icp", "integrate", "raycast", "total")}
@@ -500,6 +532,7 @@ def measure_main(a, name, intr, params, frames, D, rank, world, local, mode, icp
     else:
         int_work.append(kf.integrate_stats())  # the last timed frame's integrate work
     ray_work = kf.raycast_stats() if nprof else None
+    extract = extract_record(kf, n) if (mode == "single" and a.extract) else None
     zb, zn, o0, o1 = kf.slab_info()
     kf.synchronize()
     kf.close()
@@ -574,7 +607,9 @@ def measure_main(a, name, intr, params, frames, D, rank, world, local, mode, icp
     out = base_line(a, world, value, 1000.0 * elapsed / a.steps, "strong" if mode == "slab" else "weak", {
         "workload": workload_text(name, W, H, n, L, mode, world, icp_ar),
         "width": W, "height": H, "volume_dims": n, "volume_range_m": L,
-        "frames_unique": len(bgr), "graph": not a.no_graph, "overlap": not a.no_overlap,
+        "frames_unique": len(bgr),
+        # staged frames with overlap launch eagerly on two streams; graphs only without it
+        "graph": (not a.no_graph) and a.no_overlap, "overlap": not a.no_overlap,
         "parallelism": (f"zslab x{world}" + (" + icp allreduce" if icp_ar else "") if mode == "slab" else
                         (f"replicas x{world} (independent streams)" if world > 1 else "single")),
         "tracked_frames": int(tracked),
@@ -590,6 +625,7 @@ def measure_main(a, name, intr, params, frames, D, rank, world, local, mode, icp
         "roofline_raycast": raycast_roofline(ray_work, ray_ms, W, H, ms_source, ray_traffic,
                                              traffic_src if ray_traffic else None),
         "host_input": host_in,
+        "extract": extract,
         "cpu_baseline": cpu,
         "c1_record": c1,
     })

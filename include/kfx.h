@@ -119,6 +119,14 @@ int kfx_synchronize(kfx_ctx *ctx);
  * buffers are free on return.  Tracking status: kfx_synchronize. */
 int kfx_pipeline_async(kfx_ctx *ctx, const uint8_t *bgr, const float *depth_mm);
 int kfx_pipeline_async_u16(kfx_ctx *ctx, const uint8_t *bgr, const uint16_t *depth_mm);
+/* Zero-copy host input: page-lock a caller buffer (hipHostRegister).  A frame
+ * whose depth and colour both lie in registered buffers is uploaded by
+ * kfx_pipeline_async straight from them, with no host copy and no host wait;
+ * such a buffer is then read asynchronously and must stay unchanged until
+ * kfx_synchronize returns (or kfx_unregister_host_buffer, which waits for
+ * pending uploads).  kfx_destroy unregisters what is left. */
+int kfx_register_host_buffer(kfx_ctx *ctx, void *ptr, size_t bytes);
+int kfx_unregister_host_buffer(kfx_ctx *ctx, void *ptr);
 /* Use a captured hipGraph for the per-frame launch sequence (default on). */
 int kfx_set_graph_mode(kfx_ctx *ctx, int enabled);
 /* Overlap each staged frame's preprocess with the previous frame's tracking on
@@ -255,6 +263,9 @@ int kfx_download_columns(kfx_ctx *ctx, const int32_t *cols, int n, int16_t *tsdf
                          uint32_t *rgb);
 
 /* ---- point cloud ------------------------------------------ */
+/* Device ms of the last kfx_extract_points / kfx_extract_mesh call: the count
+ * pass, the offset scan and the emit pass (0 if nothing was emitted). */
+int kfx_get_extract_ms(kfx_ctx *ctx, float out_ms[3]);
 /* TSDFVolume::fetchPointCloud buffer size (tsdf_volume.cpp:67) */
 #define KFX_DEFAULT_CLOUD_POINTS 10000000
 /* kinectfusion::getRenderMap (kinectfusion.cpp:33-47; kernel_renderPhong /

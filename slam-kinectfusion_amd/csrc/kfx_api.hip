@@ -162,8 +162,11 @@ struct kfx_ctx {
   bool ring_used[kRing]{};
   int ring_next = 0;
   bool ring_ready = false;  // every ring resource above created
+  std::vector<std::pair<uintptr_t, size_t>> host_regs;  // kfx_register_host_buffer ranges
   hipStream_t cstream = nullptr;
   ncclComm_t comm = nullptr;      // RCCL communicator over the slab ranks (one process per GPU)
+  hipEvent_t xev[5]{};            // extraction pass events (kfx_get_extract_ms)
+  float extract_ms[3]{};          // last extraction: count pass, scan, emit pass
   bool ext_open = false;          // kfx_slab_frame_local done, kfx_slab_frame_finish due
   hipEvent_t *ext_pending = nullptr;  // that frame's timing sample
 };
@@ -799,6 +802,10 @@ static int create_impl(const kfx_intrinsics *intr, const kfx_params *params, int
     std::vector<unsigned> iota(items);
     for (size_t i = 0; i < items; ++i) iota[i] = (unsigned)i;
     HIPCHK(hipMemcpy(c->vol.iperm, iota.data(), items * 4, hipMemcpyHostToDevice));
+    if (integrate_planned(c->vol)) {  // k_int_plan's per-item ranges and chunk start values
+      if ((r = dalloc(c, (void **)&c->vol.prange, items * sizeof(int2)))) return fail(r);
+      if ((r = dalloc(c, (void **)&c->vol.pckpt, items * 64 * sizeof(float4)))) return fail(r);
+    }
   }
   if ((r = dalloc(c, (void **)&c->st, sizeof(DevState)))) return fail(r);
   c->pose_cap = kInitialPoseCap;
@@ -828,6 +835,7 @@ int kfx_destroy(kfx_ctx *c) {
   if (c->cstream) (void)hipStreamSynchronize(c->cstream);
   destroy_graphs(c);
   if (c->ring_host) (void)hipHostFree(c->ring_host);
+  for (const auto &r : c->host_regs) (void)hipHostUnregister(reinterpret_cast<void *>(r.first));
   for (int k = 0; k < kfx_ctx::kRing; ++k)
     for (hipEvent_t e : {c->ring_h2d[k], c->ring_done[k]})
       if (e) (void)hipEventDestroy(e);
@@ -839,6 +847,8 @@ int kfx_destroy(kfx_ctx *c) {
   for (hipEvent_t e : {c->ev_prep, c->ev_free[0], c->ev_free[1], c->ev_icp})
     if (e) (void)hipEventDestroy(e);
   for (hipEvent_t e : c->tsets) (void)hipEventDestroy(e);
+  for (hipEvent_t e : c->xev)
+    if (e) (void)hipEventDestroy(e);
   if (c->pstream) (void)hipStreamDestroy(c->pstream);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -876,6 +886,38 @@ int kfx_pipeline_u16(kfx_ctx *c, const uint8_t *bgr, const uint16_t *depth_mm) {
   return finish_frame(c);
 }
 
+// [p, p + n) inside one buffer registered with kfx_register_host_buffer
+static bool host_registered(const kfx_ctx *c, const void *p, size_t n) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  for (const auto &r : c->host_regs)
+    if (a >= r.first && a + n <= r.first + r.second) return true;
+  return false;
+}
+
+int kfx_register_host_buffer(kfx_ctx *c, void *ptr, size_t bytes) {
+  int r = check_ctx(c);
+  if (r) return r;
+  if (!ptr || !bytes) return set_err(KFX_ERR_ARG, "null or empty buffer");
+  HIPCHK(hipHostRegister(ptr, bytes, hipHostRegisterDefault));
+  c->host_regs.emplace_back(reinterpret_cast<uintptr_t>(ptr), bytes);
+  return KFX_OK;
+}
+
+int kfx_unregister_host_buffer(kfx_ctx *c, void *ptr) {
+  int r = check_ctx(c);
+  if (r) return r;
+  const uintptr_t a = reinterpret_cast<uintptr_t>(ptr);
+  for (size_t i = 0; i < c->host_regs.size(); ++i)
+    if (c->host_regs[i].first == a) {
+      // uploads from it may still be queued
+      if (c->cstream) HIPCHK(hipStreamSynchronize(c->cstream));
+      HIPCHK(hipHostUnregister(ptr));
+      c->host_regs.erase(c->host_regs.begin() + (long)i);
+      return KFX_OK;
+    }
+  return set_err(KFX_ERR_ARG, "buffer not registered");
+}
+
 static int pipeline_async(kfx_ctx *c, const uint8_t *bgr, const void *depth, bool u16) {
   int r = check_ctx(c);
   if (r) return r;
@@ -898,14 +940,22 @@ static int pipeline_async(kfx_ctx *c, const uint8_t *bgr, const void *depth, boo
   const int k = c->ring_next;
   c->ring_next = (k + 1) % kfx_ctx::kRing;
   uint8_t *hs = c->ring_host + c->ring_slot * k, *ds = c->ring_dev + c->ring_slot * k;
-  if (c->ring_used[k]) HIPCHK(hipEventSynchronize(c->ring_h2d[k]));  // the slot's last upload is done
   const size_t dbytes = np * (u16 ? 2 : 4);
-  std::memcpy(hs, depth, dbytes);
-  std::memcpy(hs + np * 4, bgr, np * 3);
+  // zero copy: frames in buffers registered with kfx_register_host_buffer are
+  // uploaded straight from the caller's pinned pages (no host copy, no host
+  // wait); others are copied into the pinned ring slot first
+  const bool direct = host_registered(c, depth, dbytes) && host_registered(c, bgr, np * 3);
+  if (!direct) {
+    if (c->ring_used[k]) HIPCHK(hipEventSynchronize(c->ring_h2d[k]));  // the slot's last upload is done
+    std::memcpy(hs, depth, dbytes);
+    std::memcpy(hs + np * 4, bgr, np * 3);
+  }
+  const uint8_t *src_d = direct ? static_cast<const uint8_t *>(depth) : hs;
+  const uint8_t *src_c = direct ? bgr : hs + np * 4;
   // the device slot is free once the frame that read it has finished
   if (c->ring_used[k]) HIPCHK(hipStreamWaitEvent(c->cstream, c->ring_done[k], 0));
-  HIPCHK(hipMemcpyAsync(ds, hs, dbytes, hipMemcpyHostToDevice, c->cstream));
-  HIPCHK(hipMemcpyAsync(ds + np * 4, hs + np * 4, np * 3, hipMemcpyHostToDevice, c->cstream));
+  HIPCHK(hipMemcpyAsync(ds, src_d, dbytes, hipMemcpyHostToDevice, c->cstream));
+  HIPCHK(hipMemcpyAsync(ds + np * 4, src_c, np * 3, hipMemcpyHostToDevice, c->cstream));
   HIPCHK(hipEventRecord(c->ring_h2d[k], c->cstream));
   c->ring_used[k] = true;
   FrameInput in{u16 ? c->raw[0] : (const float *)ds, u16 ? (const uint16_t *)ds : nullptr, ds + np * 4};
@@ -988,6 +1038,8 @@ int kfx_set_kernel_timing(kfx_ctx *c, int every, int max_samples) {
   if (every < 0 || max_samples < 0) return set_err(KFX_ERR_ARG, "negative timing argument");
   HIPCHK(hipStreamSynchronize(c->stream));
   for (hipEvent_t e : c->tsets) (void)hipEventDestroy(e);
+  for (hipEvent_t e : c->xev)
+    if (e) (void)hipEventDestroy(e);
   c->tsets.clear();
   c->tnext = 0;
   c->frame_seq = 0;
@@ -1557,6 +1609,21 @@ int kfx_render(kfx_ctx *c, int type, uint8_t *out) {
 
 // ---- point cloud / PLY -----------------------------------------------------
 
+// timing events of the extraction passes (created on first use)
+static int extract_events(kfx_ctx *c) {
+  for (hipEvent_t &e : c->xev)
+    if (!e) HIPCHK(hipEventCreate(&e));
+  return KFX_OK;
+}
+
+int kfx_get_extract_ms(kfx_ctx *c, float out_ms[3]) {
+  int r = check_ctx(c);
+  if (r) return r;
+  if (!out_ms) return set_err(KFX_ERR_ARG, "null out");
+  for (int i = 0; i < 3; ++i) out_ms[i] = c->extract_ms[i];
+  return KFX_OK;
+}
+
 int kfx_extract_points(kfx_ctx *c, float *xyz, int64_t cap, int64_t *n_points) {
   int r = check_ctx(c);
   if (r) return r;
@@ -1576,24 +1643,34 @@ int kfx_extract_points(kfx_ctx *c, float *xyz, int64_t cap, int64_t *n_points) {
     unsigned long long *bsum = offsets + waves;
     unsigned long long *dtot = bsum + nb;
     const DevPose vp = to_dev(c->p.volu_pose);
+    if ((r = extract_events(c))) return r;
+    HIPCHK(hipEventRecord(c->xev[0], c->stream));
     launch_extract(c->stream, c->vol, vp, zlo, zhi, counts, nullptr, nullptr, 0);
+    HIPCHK(hipEventRecord(c->xev[1], c->stream));
     launch_scan(c->stream, counts, offsets, bsum, waves, dtot);
+    HIPCHK(hipEventRecord(c->xev[2], c->stream));
     unsigned long long ht = 0;
     hipError_t e = hipMemcpyAsync(&ht, dtot, 8, hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     total = (int64_t)ht;
     const int64_t n = std::min<int64_t>(total, cap);
     float *dout = nullptr;
+    c->extract_ms[2] = 0.f;
     if (e == hipSuccess && n > 0) {
       e = hipMalloc(&dout, (size_t)n * 12);
       if (e == hipSuccess) {
+        (void)hipEventRecord(c->xev[3], c->stream);
         launch_extract(c->stream, c->vol, vp, zlo, zhi, counts, offsets, dout,
                        (unsigned long long)n);
+        (void)hipEventRecord(c->xev[4], c->stream);
         e = hipMemcpyAsync(xyz, dout, (size_t)n * 12, hipMemcpyDeviceToHost, c->stream);
         if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        if (e == hipSuccess) (void)hipEventElapsedTime(&c->extract_ms[2], c->xev[3], c->xev[4]);
         (void)hipFree(dout);
       }
     }
+    (void)hipEventElapsedTime(&c->extract_ms[0], c->xev[0], c->xev[1]);
+    (void)hipEventElapsedTime(&c->extract_ms[1], c->xev[1], c->xev[2]);
     (void)hipFree(ws);
     if (e != hipSuccess) return set_err(KFX_ERR_HIP, std::string("extract_points: ") + hipGetErrorString(e));
   }
@@ -1690,23 +1767,33 @@ int kfx_extract_mesh(kfx_ctx *c, float *tri_xyz, int64_t cap, int64_t *n_tris) {
     unsigned long long *bsum = offsets + waves;
     unsigned long long *dtot = bsum + nb;
     const DevPose vp = to_dev(c->p.volu_pose);
+    if ((r = extract_events(c))) return r;
+    HIPCHK(hipEventRecord(c->xev[0], c->stream));
     launch_mesh(c->stream, c->vol, vp, zlo, zhi, c->mc_tab, counts, nullptr, nullptr, 0);
+    HIPCHK(hipEventRecord(c->xev[1], c->stream));
     launch_scan(c->stream, counts, offsets, bsum, waves, dtot);
+    HIPCHK(hipEventRecord(c->xev[2], c->stream));
     unsigned long long ht = 0;
     hipError_t e = hipMemcpyAsync(&ht, dtot, 8, hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     total = (int64_t)ht;
     const int64_t n = std::min<int64_t>(total, cap);
     float *dout = nullptr;
+    c->extract_ms[2] = 0.f;
     if (e == hipSuccess && n > 0) {
       e = hipMalloc(&dout, (size_t)n * 36);
       if (e == hipSuccess) {
+        (void)hipEventRecord(c->xev[3], c->stream);
         launch_mesh(c->stream, c->vol, vp, zlo, zhi, c->mc_tab, counts, offsets, dout, (unsigned long long)n);
+        (void)hipEventRecord(c->xev[4], c->stream);
         e = hipMemcpyAsync(tri_xyz, dout, (size_t)n * 36, hipMemcpyDeviceToHost, c->stream);
         if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        if (e == hipSuccess) (void)hipEventElapsedTime(&c->extract_ms[2], c->xev[3], c->xev[4]);
         (void)hipFree(dout);
       }
     }
+    (void)hipEventElapsedTime(&c->extract_ms[0], c->xev[0], c->xev[1]);
+    (void)hipEventElapsedTime(&c->extract_ms[1], c->xev[1], c->xev[2]);
     (void)hipFree(ws);
     if (e != hipSuccess) return set_err(KFX_ERR_HIP, std::string("extract_mesh: ") + hipGetErrorString(e));
   }

@@ -53,8 +53,14 @@
 #ifndef KFX_INT_MAXCHUNK
 #define KFX_INT_MAXCHUNK 8  // integrate: most z-chunks per column tile
 #endif
-#ifndef KFX_INT_FREE
-#define KFX_INT_FREE 1  // integrate: free-space updates at the tsdf fixed points without divisions
+#ifndef KFX_INT_PLAN
+#define KFX_INT_PLAN 0  // integrate: chunk start values from one sweep per tile (k_int_plan) instead of per-chunk replays (measured: the plan kernel costs what the replays cost)
+#endif
+#ifndef KFX_INT_PWAVES
+#define KFX_INT_PWAVES 16384  // planned integrate: target wave count (C2: 4 equal chunks of 4096 tiles)
+#endif
+#ifndef KFX_INT_PCHUNKR
+#define KFX_INT_PCHUNKR 100  // planned integrate: chunk weights (100: equal chunks)
 #endif
 #ifndef KFX_INT_WAVES
 #define KFX_INT_WAVES 12288  // integrate: target wave count (z-chunks per column tile; C2: 3 chunks of 4096 tiles)
@@ -1260,13 +1266,159 @@ struct RayMem<false> {
   }
 };
 
+// Integrate's vol2cam pose of this frame (tsdf_volume.cpp:50) and the frame
+// kind (2: reset); stage seams pass an explicit pose.
+__device__ __forceinline__ int int_frame_pose(const DevState *st, const DevPose *log, const DevPose &vpose,
+                                              const float *xpose, DevPose &P, DevPose &gp) {
+  gp = pose_identity();
+  if (xpose) {
+    for (int i = 0; i < 9; ++i) P.R[i] = xpose[i];
+    for (int i = 0; i < 3; ++i) P.t[i] = xpose[9 + i];
+    return 1;
+  }
+  const int kind = frame_kind(st);
+  if (kind != 2) {
+    gp = frame_pose(st, log, kind);
+    P = pose_mul(pose_inv(gp), vpose);
+  }
+  return kind;
+}
+
+// A column's vc at z = 0 and its per-z step (tsdf_volume.cu:53-55), and its
+// conservative interval [zl, zh] of z where any check can pass (empty: zl > zh).
+__device__ __forceinline__ void int_column(const VolView &v, const LevelGeom &g, const float2 *dl, const DevPose &P,
+                                           int x, int y, f3 &vc, f3 &zs, int &zl, int &zh) {
+  const f3 vx = {(float)x * v.vs[0], (float)y * v.vs[1], 0.f * v.vs[2]};
+  vc = add(rmul(P.R, vx), {P.t[0], P.t[1], P.t[2]});
+  zs = {P.R[2] * v.vs[0], P.R[5] * v.vs[0], P.R[8] * v.vs[0]};
+  unsigned dm = 0u;  // the frame's max depth (k_preprocess_maps' shards)
+  const unsigned *dmx = dmax_shards(dl, g);
+#pragma unroll
+  for (int i = 0; i < kDmaxShards; ++i) dm = max(dm, dmx[i]);
+  const float dmax = __uint_as_float(dm);
+  // global z = 1..Z-1 (tsdf_volume.cu:53), restricted to the stored slab
+  // (the linear model vc0 + z zs of the accumulated vc, with 2 pixels and 2
+  // slices of margin: the float accumulation drifts < 0.1 voxel over a column)
+  const int lo0 = max(1, v.zb), hi0 = min(v.Z - 1, v.zb + v.zn - 1);
+  float lo = (float)lo0, hi = (float)hi0;  // lo only grows, hi only shrinks: finite unless emptied
+  {
+    const float ax = vc.x, ay = vc.y, az = vc.z, sx = zs.x, sy = zs.y, sz = zs.z;
+    const float M = 2.f;  // pixels
+    clip_lin(az + 1e-3f, sz, lo, hi);  // vc.z > 0
+    const float cxl = g.cx + 0.5f + M, cxh = (float)g.w - 0.5f + M - g.cx;
+    const float cyl = g.cy + 0.5f + M, cyh = (float)g.h - 0.5f + M - g.cy;
+    clip_lin(g.fx * ax + cxl * az, g.fx * sx + cxl * sz, lo, hi);
+    clip_lin(cxh * az - g.fx * ax, cxh * sz - g.fx * sx, lo, hi);
+    clip_lin(g.fy * ay + cyl * az, g.fy * sy + cyl * sz, lo, hi);
+    clip_lin(cyh * az - g.fy * ay, cyh * sz - g.fy * sy, lo, hi);
+    const float zfar = (dmax + v.trunc) * 1.02f + 0.01f;
+    clip_lin(zfar - az, -sz, lo, hi);
+  }
+  zl = INT_MAX, zh = INT_MIN;
+  if (hi >= lo) {
+    zl = max(lo0, (int)floorf(lo) - 2);
+    zh = min(hi0, (int)ceilf(hi) + 2);
+    if (zh < zl) zl = INT_MAX, zh = INT_MIN;
+  }
+}
+
+// Chunk `chunk` of the wave-uniform union interval [wl, wh] (wl <= wh):
+// [za, zb], or false when this item has no chunk (length-capped mode).
+__device__ __forceinline__ bool int_chunk(const VolView &v, int chunkr, int chunk, int nchunk, int wl, int wh,
+                                          int &za, int &zb) {
+  const int len = wh - wl + 1;
+  if (v.iadapt == 1) {
+    // length-capped: chunks of about zn / nchunk slices (a short interval
+    // takes fewer; the surplus items, ordered last, exit)
+    const int ct = min(nchunk, max(1, (int)(((long long)len * nchunk + v.zn - 1) / v.zn)));
+    if (chunk >= ct) return false;
+    za = wl + (int)((long long)len * chunk / ct);
+    zb = wl + (int)((long long)len * (chunk + 1) / ct) - 1;
+    return true;
+  }
+  if (chunkr >= 100) {  // equal chunks
+    za = wl + (int)((long long)len * chunk / nchunk);
+    zb = wl + (int)((long long)len * (chunk + 1) / nchunk) - 1;
+    return true;
+  }
+  // chunk c gets weight r^c: the chunks dispatched last (highest item
+  // index) are the shortest, so the kernel's tail waves are short
+  const float r = (float)chunkr * 0.01f;
+  const float den = 1.f - __powf(r, (float)nchunk);
+  za = wl + (int)((float)len * ((1.f - __powf(r, (float)chunk)) / den));
+  zb = chunk + 1 == nchunk ? wh : wl + (int)((float)len * ((1.f - __powf(r, (float)(chunk + 1))) / den)) - 1;
+  return true;
+}
+
+// Integrate plan (volumes with several z-chunks per tile): one wave per
+// column tile computes its lanes' intervals and the union once, splits it
+// into the chunks, and sweeps vc from z = 1 through the chunk starts with the
+// reference's float adds, storing every chunk's start value: the chunk waves
+// of k_integrate then begin at their first slice instead of each replaying
+// the column from z = 1 (the replays of 3 chunks cost ~7 % of integrate at
+// C2; the sweep here is shared by all chunks of a tile).  Per item
+// (chunk * tiles + tile): prange = {za, zb} ({1, 0}: nothing to do),
+// pckpt[item * 64 + lane] = {vc(za - 1) x, y, z, bits zl | zh << 16}.
+__global__ __launch_bounds__(64) void k_int_plan(VolView v, LevelGeom g, const float2 *__restrict__ dl,
+                                                 const DevState *__restrict__ st, const DevPose *log,
+                                                 DevPose vpose, const float *xpose, int write_work) {
+  __shared__ DevPose s_pose;
+  __shared__ int s_kind;
+  if (threadIdx.x == 0) {
+#if KFX_PLAN_EXP == 2  // timing experiment only (wrong values): no pose loads
+    s_pose = vpose;
+    s_kind = 1;
+#else
+    DevPose gp;
+    s_kind = int_frame_pose(st, log, vpose, xpose, s_pose, gp);
+#endif
+  }
+  __syncthreads();
+  const int tiles = v.tiles_x * v.tiles_y, nchunk = v.inchunk;
+  const int tile = blockIdx.x, lane = threadIdx.x;
+  int2 *rg = v.prange + tile;
+  if (s_kind == 2) return;  // reset frame: integrate zeroes the volume, no plan read
+  const int x = (tile % v.tiles_x) * 8 + (lane & 7);
+  const int y = (tile / v.tiles_x) * 8 + (lane >> 3);
+  f3 vc, zs;
+  int zl, zh;
+  int_column(v, g, dl, s_pose, x, y, vc, zs, zl, zh);
+  int wl = zl, wh = zh;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    wl = min(wl, __shfl_xor(wl, off));
+    wh = max(wh, __shfl_xor(wh, off));
+  }
+  // the next frame's dispatch order (k_int_order) from this interval length
+  if (write_work && lane == 0 && v.iwork) v.iwork[tile] = wh >= wl ? (unsigned)(wh - wl + 1) : 0u;
+  const unsigned zbits = zl <= zh ? ((unsigned)zl | ((unsigned)zh << 16)) : 0xFFFFu;
+  int z = 1;
+  for (int c = 0; c < nchunk; ++c) {
+    int za = 1, zb = 0;
+    if (wl > wh || !int_chunk(v, KFX_INT_PCHUNKR, c, nchunk, wl, wh, za, zb) ||
+        __all(!(max(za, zl) <= min(zb, zh)))) {
+      if (lane == 0) rg[(size_t)c * tiles] = make_int2(1, 0);
+      continue;
+    }
+#if KFX_PLAN_EXP == 1  // timing experiment only (wrong values): no sweep
+    if (za > z) vc = add(vc, scl(zs, (float)(za - z)));
+    z = max(z, za);
+#else
+#pragma unroll 8
+    for (; z < za; ++z) vc = add(vc, zs);
+#endif
+    v.pckpt[((size_t)c * tiles + tile) * 64 + lane] = make_float4(vc.x, vc.y, vc.z, __uint_as_float(zbits));
+    if (lane == 0) rg[(size_t)c * tiles] = make_int2(za, zb);
+  }
+}
+
 // Work split: a wave owns an 8x8 tile of columns and one of gridDim.y z-chunks
 // of every column's in-range interval (more waves per SIMD to hide latency);
 // each lane replays the vc adds up to its chunk start, so every voxel's vc is
 // the reference's bit for bit.
 // kCount: count-only variant (no voxel traffic) giving N_upd / N_col, the
 // algorithmic-byte inputs of the roofline.
-template <bool kCount, bool kIdx32>
+template <bool kCount, bool kIdx32, bool kPlan>
 __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(KFX_INT_OCC, KFX_INT_OCC))) void k_integrate(VolView v, LevelGeom g,
                                                    const float2 *__restrict__ dl,
                                                    const uint8_t *__restrict__ bgr,
@@ -1279,7 +1431,7 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
   __shared__ DevPose s_pose;
   __shared__ int s_kind;
   for (int i = threadIdx.x; i < 257; i += KFX_INT_BLOCK) rtab[i] = 1.f / (float)max(1, i);
-  if (threadIdx.x == 0) {
+  if (threadIdx.x == 0) {  // (inline rather than int_frame_pose: that form spills in the unplanned loop)
     if (xpose) {  // stage seam: explicit vol2cam
       s_kind = 1;
       for (int i = 0; i < 9; ++i) s_pose.R[i] = xpose[i];
@@ -1327,77 +1479,41 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
     return;
   }
   const DevPose P = s_pose;
-  const f3 vx = {(float)x * v.vs[0], (float)y * v.vs[1], 0.f * v.vs[2]};
-  f3 vc = add(rmul(P.R, vx), {P.t[0], P.t[1], P.t[2]});
-  const f3 zs = {P.R[2] * v.vs[0], P.R[5] * v.vs[0], P.R[8] * v.vs[0]};
-
-  // conservative interval [zlo, zhi] of z where any check can pass
-  unsigned dm = 0u;
-  const unsigned *dmx = dmax_shards(dl, g);
+  f3 vc, zs;
+  int zl, zh, za, zb, z;
+  if (kPlan) {  // planned (k_int_plan): this chunk's range, lane intervals and start vc
+    const int2 r = v.prange[item];
+    za = r.x, zb = r.y;
+    if (za > zb) return;  // wave-uniform
+    const float4 ck = v.pckpt[(size_t)item * 64 + lane];
+    const unsigned zbits = __float_as_uint(ck.w);
+    zl = (int)(zbits & 0xFFFFu), zh = (int)(zbits >> 16);
+    vc = {ck.x, ck.y, ck.z};
+    zs = {P.R[2] * v.vs[0], P.R[5] * v.vs[0], P.R[8] * v.vs[0]};
+    z = za;
+  } else {
+    int_column(v, g, dl, P, x, y, vc, zs, zl, zh);
+    // The wave takes a chunk of the UNION of its lanes' intervals, so all 64
+    // lanes step the same z and each voxel load / store of the wave is one
+    // 128-B line (per-lane intervals put the lanes on different slices: one
+    // line per lane); a lane only updates voxels inside its own interval.
+    int wl = zl, wh = zh;
 #pragma unroll
-  for (int i = 0; i < kDmaxShards; ++i) dm = max(dm, dmx[i]);
-  const float dmax = __uint_as_float(dm);
-  // global z = 1..Z-1 (tsdf_volume.cu:53), restricted to the stored slab
-  // (the linear model vc0 + z zs of the accumulated vc, with 2 pixels and 2
-  // slices of margin: the float accumulation drifts < 0.1 voxel over a column)
-  const int lo0 = max(1, v.zb), hi0 = min(v.Z - 1, v.zb + v.zn - 1);
-  float lo = (float)lo0, hi = (float)hi0;  // lo only grows, hi only shrinks: finite unless emptied
-  {
-    const float ax = vc.x, ay = vc.y, az = vc.z, sx = zs.x, sy = zs.y, sz = zs.z;
-    const float M = 2.f;  // pixels
-    clip_lin(az + 1e-3f, sz, lo, hi);  // vc.z > 0
-    const float cxl = g.cx + 0.5f + M, cxh = (float)g.w - 0.5f + M - g.cx;
-    const float cyl = g.cy + 0.5f + M, cyh = (float)g.h - 0.5f + M - g.cy;
-    clip_lin(g.fx * ax + cxl * az, g.fx * sx + cxl * sz, lo, hi);
-    clip_lin(cxh * az - g.fx * ax, cxh * sz - g.fx * sx, lo, hi);
-    clip_lin(g.fy * ay + cyl * az, g.fy * sy + cyl * sz, lo, hi);
-    clip_lin(cyh * az - g.fy * ay, cyh * sz - g.fy * sy, lo, hi);
-    const float zfar = (dmax + v.trunc) * 1.02f + 0.01f;
-    clip_lin(zfar - az, -sz, lo, hi);
-  }
-  // this lane's candidate interval [zl, zh] (empty: zl > zh)
-  int zl = INT_MAX, zh = INT_MIN;
-  if (hi >= lo) {
-    zl = max(lo0, (int)floorf(lo) - 2);
-    zh = min(hi0, (int)ceilf(hi) + 2);
-    if (zh < zl) zl = INT_MAX, zh = INT_MIN;
-  }
-  // The wave takes a chunk of the UNION of its lanes' intervals, so all 64
-  // lanes step the same z and each voxel load / store of the wave is one
-  // 128-B line (per-lane intervals put the lanes on different slices: one
-  // line per lane); a lane only updates voxels inside its own interval.
-  int wl = zl, wh = zh;
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    wl = min(wl, __shfl_xor(wl, off));
-    wh = max(wh, __shfl_xor(wh, off));
-  }
-  // the next frame's dispatch order (k_int_order) from this interval length
-  if (!kCount && chunk == 0 && lane == 0 && v.iwork) v.iwork[tile] = wh >= wl ? (unsigned)(wh - wl + 1) : 0u;
-  if (wh < wl) return;  // wave-uniform
-  int za, zb;
-  {
-    const int len = wh - wl + 1;
-    if (v.iadapt == 1) {
-      // length-capped: chunks of about zn / nchunk slices (a short interval
-      // takes fewer; the surplus items, ordered last, exit here)
-      const int ct = min(nchunk, max(1, (int)(((long long)len * nchunk + v.zn - 1) / v.zn)));
-      if (chunk >= ct) return;  // wave-uniform
-      za = wl + (int)((long long)len * chunk / ct);
-      zb = wl + (int)((long long)len * (chunk + 1) / ct) - 1;
-    } else {
-#if KFX_INT_CHUNKR == 100
-    za = wl + (int)((long long)len * chunk / nchunk);
-    zb = wl + (int)((long long)len * (chunk + 1) / nchunk) - 1;
-#else
-    // chunk c gets weight r^c: the chunks dispatched last (highest
-    // blockIdx.y) are the shortest, so the kernel's tail waves are short
-    const float r = (float)KFX_INT_CHUNKR * 0.01f;
-    const float den = 1.f - __powf(r, (float)nchunk);
-    za = wl + (int)((float)len * ((1.f - __powf(r, (float)chunk)) / den));
-    zb = chunk + 1 == nchunk ? wh : wl + (int)((float)len * ((1.f - __powf(r, (float)(chunk + 1))) / den)) - 1;
-#endif
+    for (int off = 32; off > 0; off >>= 1) {
+      wl = min(wl, __shfl_xor(wl, off));
+      wh = max(wh, __shfl_xor(wh, off));
     }
+    // the next frame's dispatch order (k_int_order) from this interval length
+    if (!kCount && chunk == 0 && lane == 0 && v.iwork) v.iwork[tile] = wh >= wl ? (unsigned)(wh - wl + 1) : 0u;
+    if (wh < wl || !int_chunk(v, KFX_INT_CHUNKR, chunk, nchunk, wl, wh, za, zb)) return;  // wave-uniform
+    z = 1;
+#if KFX_INT_EXP == 5  // timing experiment only (wrong values): no per-chunk replay
+    if (za > z) vc = add(vc, scl(zs, (float)(za - z)));
+    z = max(z, za);
+#else
+#pragma unroll 8
+    for (; z < za; ++z) vc = add(vc, zs);
+#endif
   }
   const int la = max(za, zl), lb = min(zb, zh);  // this lane's voxels of the chunk
   const bool live = lb >= la;
@@ -1411,9 +1527,6 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
   const int gbs = za >> 3;
   unsigned long long nbm = 0ull;
   int nlo = INT_MAX, nhi = -1;
-  int z = 1;
-#pragma unroll 8
-  for (; z < za; ++z) vc = add(vc, zs);
   using Mem = VoxMem<kIdx32>;
   using Idx = typename Mem::Idx;
   const Mem mem(v);
@@ -1537,24 +1650,7 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
       // saturated free space (w = 64 at the tsdf fixed point T* of a ts = 1
       // update, sdf >= trunc so ts = 1 and no colour band): the update is
       // the identity — skip it (same stores skipped as below)
-      if (!ok[j]) continue;
-#if KFX_INT_FREE
-      // free space (sdf >= trunc, so ts = 1 exactly) at the fixed points of
-      // such updates: the reference's average gives 32767 from weight 0 and
-      // 32766 from t0 in {32766, 32767} at weights 1..64 (every weight it
-      // writes; exhaustive check against the oracle's update,
-      // tests/test_oracle_kat.py) — no divisions, no colour band, q > 0.
-      // Saturated free space (t0 = 32766, w = 64) stores nothing.
-      if (sdf[j] >= trunc && (w0[j] == 0 || (t0[j] >= kShortMax - 1 && w0[j] <= kMaxWeight))) {
-        const int q = w0[j] == 0 ? kShortMax : kShortMax - 1;
-        const int nw = min(w0[j] + 1, kMaxWeight);
-        if (q != t0[j]) mem.st_t(vi[j], (int16_t)q);
-        if (nw != w0[j]) mem.st_w(vi[j], (int16_t)nw);
-        continue;
-      }
-#else
-      if (w0[j] == kMaxWeight && t0[j] == v.tsat && sdf[j] >= trunc) continue;
-#endif
+      if (!ok[j] || (w0[j] == kMaxWeight && t0[j] == v.tsat && sdf[j] >= trunc)) continue;
       const Idx i = vi[j];
       const int pre_w = w0[j];
       const float ts = fminf(1.f, div_rn(sdf[j], trunc, v.inv_trunc));
@@ -3024,8 +3120,12 @@ int integrate_chunks(const VolView &v) {
   const int tiles = v.tiles_x * v.tiles_y;
   if (integrate_mode(v) == 1) return std::max(1, std::min(KFX_INT_NC, v.zn / 32));  // chunks of >= 32 slices
   // z-chunks so that >= KFX_INT_WAVES waves exist (12 per SIMD on 1024 SIMDs)
-  return std::max(1, std::min(KFX_INT_MAXCHUNK, (KFX_INT_WAVES + tiles - 1) / tiles));
+  const int waves = KFX_INT_PLAN ? KFX_INT_PWAVES : KFX_INT_WAVES;
+  return std::max(1, std::min(KFX_INT_MAXCHUNK, (waves + tiles - 1) / tiles));
 }
+
+// k_int_plan is used where a tile has several chunks (the per-chunk replay it removes)
+bool integrate_planned(const VolView &v) { return KFX_INT_PLAN && integrate_chunks(v) > 1 && v.Z < 65535; }
 
 // Longest-first dispatch order of k_integrate's (tile, chunk) items for the
 // next frame (VolView::iadapt): item c of tile t is one of ct(len_t) capped
@@ -3077,6 +3177,13 @@ void launch_integrate(hipStream_t s, VolView v, LevelGeom g0, const float2 *dl0,
   v.iadapt = integrate_mode(v);
   if (!v.iadapt) v.iperm = nullptr, v.iwork = nullptr;  // geometric chunks in block order
   if (counters) v.iwork = nullptr;  // the count-only pass leaves the order alone
+  const bool planned = integrate_planned(v) && v.prange && v.pckpt;
+  if (planned) {
+    hipLaunchKernelGGL(k_int_plan, dim3(tiles), dim3(64), 0, s, v, g0, dl0, st, log, vpose, xpose,
+                       v.iwork ? 1 : 0);
+  } else {
+    v.prange = nullptr, v.pckpt = nullptr;
+  }
   dim3 grd(tiles * nchunk);  // one wave (block) per (tile, chunk) item
   const bool idx32 = v.local_voxels() < (1ull << 31);  // 32-bit tsdf/weight byte offsets
 #ifdef KFX_INT_TRACE
@@ -3088,20 +3195,29 @@ void launch_integrate(hipStream_t s, VolView v, LevelGeom g0, const float2 *dl0,
   g_int_trace_waves = (int)grd.x;
   (void)hipMemsetAsync(trace_buf, 0, sizeof(unsigned long long) * 4 * g_int_trace_waves, s);  // waves that exit early write none
   if (!counters) {
-    hipLaunchKernelGGL((k_integrate<false, true>), grd, dim3(KFX_INT_BLOCK), 0, s, v, g0, dl0, bgr, st, log,
-                       vpose, xpose, trace_buf);
+    if (planned)
+      hipLaunchKernelGGL((k_integrate<false, true, true>), grd, dim3(KFX_INT_BLOCK), 0, s, v, g0, dl0, bgr, st,
+                         log, vpose, xpose, trace_buf);
+    else
+      hipLaunchKernelGGL((k_integrate<false, true, false>), grd, dim3(KFX_INT_BLOCK), 0, s, v, g0, dl0, bgr, st,
+                         log, vpose, xpose, trace_buf);
     return;
   }
 #endif
-  if (counters)
-    hipLaunchKernelGGL((k_integrate<true, false>), grd, dim3(KFX_INT_BLOCK), 0, s, v, g0, dl0, bgr, st, log,
-                       vpose, xpose, counters);
-  else if (idx32)
-    hipLaunchKernelGGL((k_integrate<false, true>), grd, dim3(KFX_INT_BLOCK), 0, s, v, g0, dl0, bgr, st, log,
-                       vpose, xpose, counters);
-  else
-    hipLaunchKernelGGL((k_integrate<false, false>), grd, dim3(KFX_INT_BLOCK), 0, s, v, g0, dl0, bgr, st, log,
-                       vpose, xpose, counters);
+#define KFX_LAUNCH_INT(C, I, P)                                                                             \
+  hipLaunchKernelGGL((k_integrate<C, I, P>), grd, dim3(KFX_INT_BLOCK), 0, s, v, g0, dl0, bgr, st, log, vpose, xpose, \
+                     counters)
+  if (counters) {
+    if (planned) KFX_LAUNCH_INT(true, false, true);
+    else KFX_LAUNCH_INT(true, false, false);
+  } else if (idx32) {
+    if (planned) KFX_LAUNCH_INT(false, true, true);
+    else KFX_LAUNCH_INT(false, true, false);
+  } else {
+    if (planned) KFX_LAUNCH_INT(false, false, true);
+    else KFX_LAUNCH_INT(false, false, false);
+  }
+#undef KFX_LAUNCH_INT
   if (!counters && v.iwork && v.iperm)
     hipLaunchKernelGGL(k_int_order, dim3(1), dim3(1024), 0, s, v.iwork, v.iperm, tiles, nchunk, v.zn);
 }

@@ -33,9 +33,9 @@ EXPORTS = [
     "kfx_write_poses_txt", "kfx_get_frame_maps", "kfx_set_frame_maps", "kfx_download_tsdf",
     "kfx_upload_tsdf", "kfx_download_volume_soa", "kfx_stage_preprocess", "kfx_stage_icp_accumulate",
     "kfx_stage_icp", "kfx_stage_integrate", "kfx_stage_raycast", "kfx_set_profiling", "kfx_get_stage_ms",
-    "kfx_integrate_counts", "kfx_integrate_stats", "kfx_raycast_stats", "kfx_download_columns", "kfx_pipeline_async", "kfx_pipeline_async_u16", "kfx_slab_mask_payload", "kfx_slab_expand", "kfx_set_icp_allreduce", "kfx_create_slab", "kfx_slab_info", "kfx_comm_get_unique_id", "kfx_comm_init",
+    "kfx_integrate_counts", "kfx_integrate_stats", "kfx_raycast_stats", "kfx_download_columns", "kfx_pipeline_async", "kfx_pipeline_async_u16", "kfx_register_host_buffer", "kfx_unregister_host_buffer", "kfx_slab_mask_payload", "kfx_slab_expand", "kfx_set_icp_allreduce", "kfx_create_slab", "kfx_slab_info", "kfx_comm_get_unique_id", "kfx_comm_init",
     "kfx_pipeline_group", "kfx_slab_frame_local", "kfx_slab_frame_finish", "kfx_render", "kfx_volume_checksum", "kfx_extract_points", "kfx_write_ply", "kfx_save_pointcloud",
-    "kfx_extract_mesh", "kfx_write_ply_mesh",
+    "kfx_extract_mesh", "kfx_write_ply_mesh", "kfx_get_extract_ms",
     "kfx_dataset_open", "kfx_dataset_info", "kfx_dataset_read", "kfx_dataset_close", "kfx_png_info",
     "kfx_png_read_bgr8", "kfx_png_read_depth", "kfx_parse_intr",
 ]
@@ -107,6 +107,8 @@ def lib():
         "kfx_set_icp_allreduce": ([vp, i], i),
         "kfx_slab_expand": ([P(C.c_uint32), P(Intrinsics), P(Pose), P(f), P(f), P(f)], i),
         "kfx_pipeline_async_u16": ([vp, P(C.c_uint8), P(C.c_uint16)], i),
+        "kfx_register_host_buffer": ([vp, vp, C.c_size_t], i),
+        "kfx_unregister_host_buffer": ([vp, vp], i),
         "kfx_download_columns": ([vp, P(C.c_int32), i, P(C.c_int16), P(C.c_int16), P(C.c_uint32)], i),
         "kfx_create_slab": ([P(Intrinsics), P(Params), i, i, i, P(vp)], i),
         "kfx_slab_info": ([vp, P(i), P(i), P(i), P(i)], i),
@@ -121,6 +123,7 @@ def lib():
         "kfx_write_ply": ([C.c_char_p, P(f), C.c_int64], i),
         "kfx_save_pointcloud": ([vp, C.c_char_p, C.c_int64], i),
         "kfx_extract_mesh": ([vp, P(f), C.c_int64, P(C.c_int64)], i),
+        "kfx_get_extract_ms": ([vp, P(f)], i),
         "kfx_write_ply_mesh": ([C.c_char_p, P(f), C.c_int64], i),
         "kfx_dataset_open": ([C.c_char_p, P(vp)], i),
         "kfx_dataset_info": ([vp, P(Intrinsics), P(i), P(i)], i),
@@ -132,7 +135,10 @@ def lib():
         "kfx_parse_intr": ([C.c_char_p, P(f)], i),
     }
     for name, (args, res) in sig.items():
-        fn = getattr(L, name)
+        try:
+            fn = getattr(L, name)
+        except AttributeError:  # an older build (A/B timing runs); calling it raises then
+            continue
         fn.argtypes = args
         fn.restype = res
     _lib = L
@@ -360,6 +366,15 @@ class KinectFusion:
             d = np.ascontiguousarray(depth_mm, np.float32)
             _check(lib().kfx_pipeline_async(self._h, u8ptr(color), fptr(d)), "kfx_pipeline_async")
 
+    def register_host_buffer(self, arr: np.ndarray):
+        """Page-lock a C-contiguous array: pipeline_async then uploads frames in
+        it without a host copy (keep it unchanged until synchronize())."""
+        assert arr.flags["C_CONTIGUOUS"]
+        _check(lib().kfx_register_host_buffer(self._h, arr.ctypes.data, arr.nbytes), "kfx_register_host_buffer")
+
+    def unregister_host_buffer(self, arr: np.ndarray):
+        _check(lib().kfx_unregister_host_buffer(self._h, arr.ctypes.data), "kfx_unregister_host_buffer")
+
     def synchronize(self) -> int:
         """Wait for queued frames; KFX_OK, or KFX_TRACKING_LOST if one of the
         frames completed since the last status check was dropped (reset)."""
@@ -467,6 +482,12 @@ class KinectFusion:
         if m:
             _check(lib().kfx_extract_points(self._h, fptr(out), m, C.byref(n)), "kfx_extract_points")
         return out
+
+    def extract_ms(self) -> dict:
+        """Device ms of the last extract_points / extract_mesh: count pass, scan, emit pass."""
+        a = (C.c_float * 3)()
+        _check(lib().kfx_get_extract_ms(self._h, a), "kfx_get_extract_ms")
+        return {"count": a[0], "scan": a[1], "emit": a[2]}
 
     def save_pointcloud(self, path: str, cap: int = 0):
         _check(lib().kfx_save_pointcloud(self._h, path.encode(), cap), "kfx_save_pointcloud")

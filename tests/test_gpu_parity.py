@@ -422,15 +422,28 @@ def test_async_host_input_matches_staged(u16, seq_qvga):
         kf.pipeline_async(bgr[k], frames[k])
     assert kf.synchronize() == KFX_TRACKING_LOST
     assert kf.synchronize() == KFX_OK
+    # zero copy: the same frames uploaded straight from registered host buffers
+    zc, _ = make(intr, dims=64)
+    hb = np.ascontiguousarray(bgr)
+    zc.register_host_buffer(hb)
+    zc.register_host_buffer(frames)
+    for k in range(len(frames)):
+        zc.pipeline_async(hb[k], frames[k])
+    assert zc.synchronize() == KFX_TRACKING_LOST
+    zc.unregister_host_buffer(hb)
+    with pytest.raises(KfxError):
+        zc.unregister_host_buffer(hb)
     ref, _ = make(intr, dims=64)
     ref.stage_frames(bgr, frames.astype(np.float32))
     for k in range(len(frames)):
         ref.pipeline_staged(k)
     assert ref.synchronize() == KFX_TRACKING_LOST
     assert np.array_equal(kf.pose_record, ref.pose_record) and kf.frame_count == ref.frame_count
-    for a, b in zip(kf.volume_soa(), ref.volume_soa()):
-        assert np.array_equal(a, b)
+    assert np.array_equal(zc.pose_record, ref.pose_record) and zc.frame_count == ref.frame_count
+    for a, b, z in zip(kf.volume_soa(), ref.volume_soa(), zc.volume_soa()):
+        assert np.array_equal(a, b) and np.array_equal(z, b)
     kf.close()
+    zc.close()
     ref.close()
 
 

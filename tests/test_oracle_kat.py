@@ -427,19 +427,17 @@ def test_rodrigues_sincos_within_an_ulp_of_libm(oracle_lib):
     assert oracle_lib.sincos(0.7) == (math.sin(0.7), math.cos(0.7))  # libm above the polynomial range
 
 
-def test_free_space_update_shortcut_exhaustive():
-    """k_integrate's free-space shortcut (KFX_INT_FREE): a voxel with sdf >=
-    trunc (so ts = 1 exactly) and w0 = 0, or t0 in {32766, 32767} and
-    w0 <= 64 (MAX_WEIGHT: every weight the reference writes), gets tsdf 32767
-    (w0 = 0) / 32766 (w0 >= 1) and weight min(w0 + 1, 64), which is what the
-    reference's update (tsdf_volume.cu:72-81, restated by the oracle)
-    computes.  Uploaded weights 65..255 take the general path: there the
-    shortcut would be wrong (e.g. t0 = 32766, w0 = 97 -> 32765)."""
+def test_saturated_free_space_fixed_point():
+    """k_integrate skips the update of saturated free space (w0 = MAX_WEIGHT =
+    64, t0 = T*, sdf >= trunc so ts = 1 exactly): the reference's running
+    average (tsdf_volume.cu:72-81, restated by the oracle) leaves such a voxel
+    unchanged, and T* = 32766 is where free space settles (32767 after the
+    first update, 32766 from the second on)."""
     import oracle as O
     for trunc in (0.0084, 2.1 * 2.048 / 1024, 2.1 * 4.096 / 2048, 2.1 * 3.0 / 512):
-        for sdf in (trunc, np.nextafter(np.float32(trunc), np.float32(1)), 2 * trunc, 0.5, 7.0):
-            for w0 in range(65):
-                for t0 in ((32766, 32767) if w0 else (-32767, -1, 0, 1, 12345, 32766, 32767)):
-                    q, w = O.tsdf_update(t0, w0, float(sdf), float(np.float32(trunc)))
-                    assert (q, w) == (32767 if w0 == 0 else 32766, min(w0 + 1, 64)), (trunc, sdf, t0, w0, q)
-    assert O.tsdf_update(32766, 97, 0.0084, 0.0084)[0] == 32765
+        for sdf in (trunc, float(np.nextafter(np.float32(trunc), np.float32(1))), 2 * trunc, 0.5, 7.0):
+            assert O.tsdf_update(32766, 64, sdf, float(np.float32(trunc))) == (32766, 64)
+            t = 0
+            for w in range(64):  # a voxel seen as free space from its first update on
+                t, w1 = O.tsdf_update(t, w, sdf, float(np.float32(trunc)))
+                assert (t, w1) == ((32767 if w == 0 else 32766), w + 1)

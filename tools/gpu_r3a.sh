@@ -9,5 +9,5 @@ echo "== tests (var_free)"
 KFX_LIB_PATH=$PWD/slam-kinectfusion_amd/lib/var_free/libkfx.so timeout -k 10 1200 python3 -u -m pytest tests -m gpu -x -v \
   --timeout 300 --timeout-method thread > gpurun_out/tests_r3a.log 2>&1; rc=$?
 tail -3 gpurun_out/tests_r3a.log; [ $rc -eq 0 ] || exit $rc
-echo "== profile (base)"
-KFX_COMMIT=aa0686e PMC_RECORD=r03_head_pmc.json bash tools/prof.sh --steps 20 --warmup 5
+echo "== profile (var_free)"
+KFX_LIB_PATH=$PWD/slam-kinectfusion_amd/lib/var_free/libkfx.so KFX_COMMIT=4dc4658+ PMC_RECORD=r03_free_pmc.json bash tools/prof.sh --steps 20 --warmup 5

@@ -54,6 +54,12 @@ for k in range(20):
     t = span * (k + 0.5) / 20
     print(f"  t={t / 1e3:6.1f} us resident {((st <= t) & (en > t)).sum() / 8192:5.2f}")
 print(f"wave-time / (span x 8192 slots) = {dur.sum() / (span * 8192):.3f}")
+chunk = a[:, 3] >> 32
+for c in np.unique(chunk):
+    m = chunk == c
+    print(f"  chunk {c}: waves {m.sum():5d} start med {np.median(st[m]) / 1e3:6.1f} dur med {np.median(dur[m]) / 1e3:6.1f} "
+          f"p90 {np.percentile(dur[m], 90) / 1e3:6.1f} max {dur[m].max() / 1e3:6.1f} us; ends after 90% of span: "
+          f"{(m & (en > 0.9 * span)).sum()}")
 if len(sys.argv) > 1 and sys.argv[1] != "-":
     np.save(sys.argv[1], a)
 kf.close()
