@@ -83,6 +83,8 @@ def parse():
     ap.add_argument("--replicas", type=int, default=1,
                     help="slab mode at N>1: time independent replica streams first (the fallback line)")
     ap.add_argument("--zslab-timeout", type=float, default=300.0)
+    ap.add_argument("--cuts", choices=["balanced", "equal"], default="balanced",
+                    help="slab mode: Z-slab cuts balanced on the first frame's per-slice work, or equal slice ranges")
     ap.add_argument("--extract", type=int, default=1,
                     help="N=1: time point extraction and marching cubes on the final volume (0 = skip)")
     ap.add_argument("--c3-frames", type=int, default=20,
@@ -267,7 +269,8 @@ def workload_text(name, W, H, n, L, mode, world, icp_ar):
     t = (f"{name.upper()}: synthetic {W}x{H} depth+BGR, {n}^3 TSDF @ {1000 * L / n:.1f} mm, "
          f"3-level ICP {{10,5,4}}, full pipeline per frame")
     if mode == "slab":
-        t += (f"; one stream, volume Z-slab sharded over {world} GPUs, raycast combined per frame by RCCL "
+        t += (f"; one stream, volume Z-slab sharded over {world} GPUs (cuts balanced on the first frame's "
+              f"per-slice integrate work), raycast combined per frame by RCCL "
               f"(MIN keys + MAX {{Ts, normal}} payload), ICP " + ("sharded (27 int64 partials all-reduced per "
                                                                    "iteration)" if icp_ar else "replicated"))
     elif mode == "replicas":
@@ -281,7 +284,10 @@ def run_stream(a, intr, params, frames, D, local, slab=None, icp_ar=False, timin
     import kfx
     from kfx.abi import Intrinsics
     bgr, dep, order = frames
-    kf = kfx.KinectFusion(Intrinsics.from_any(intr), params, device=local, slab=slab)
+    cuts = None
+    if slab is not None and a.cuts == "balanced":
+        cuts = balanced_cuts(intr, params, bgr[order[0]], dep[order[0]], local, slab[1])
+    kf = kfx.KinectFusion(Intrinsics.from_any(intr), params, device=local, slab=slab, cuts=cuts)
     if slab is not None:
         kf.comm_init(D.bcast_bytes(kfx.comm_unique_id() if slab[0] == 0 else None))
         kf.set_icp_allreduce(icp_ar)
@@ -305,6 +311,19 @@ def run_stream(a, intr, params, frames, D, local, slab=None, icp_ar=False, timin
     if ktime is not None and not ktime["samples"]:
         ktime = None
     return kf, {"elapsed": elapsed, "ktime": ktime, "tracked": tracked}
+
+
+def balanced_cuts(intr, params, bgr0, dep0, local, world):
+    """Work-balanced Z-slab cuts from the first frame (kfx_slice_work on a
+    throw-away 16-slice slab context, kfx_slab_balance): every rank computes
+    the same cuts from the same frame."""
+    import kfx
+    from kfx.abi import Intrinsics
+    Z = int(params.volu_dims[2])
+    probe = kfx.KinectFusion(Intrinsics.from_any(intr), params, device=local, slab=(0, Z // 16))
+    work = probe.slice_work(bgr0, dep0)
+    probe.close()
+    return kfx.slab_balance(work, world)
 
 
 def integrate_roofline(work, ms, W, H, ms_source, traffic=None, traffic_src=None):

@@ -346,6 +346,17 @@ int kfx_parse_intr(const char *path, float out5[5]);
  * single-GPU kfx_create context, bit for bit. */
 int kfx_create_slab(const kfx_intrinsics *intr, const kfx_params *params, int device,
                     int rank, int world, kfx_ctx **out);
+/* Work-balanced slabs: slab r owns [cuts[r], cuts[r+1]) (cuts[0] = 0,
+ * cuts[world] = Z, multiples of 8, >= 8 slices each; every rank passes the
+ * same cuts).  kfx_slice_work gives, per global slice, the voxels a frame's
+ * integrate would update at the first frame's pose (any context, slab or not;
+ * an estimate from the frame's filtered depth); kfx_slab_balance turns such a
+ * histogram into cuts minimising the largest slab's stored-range work (halos
+ * included).  Results stay bit-identical to the single volume for any cuts. */
+int kfx_create_slab_cuts(const kfx_intrinsics *intr, const kfx_params *params, int device,
+                         int rank, int world, const int *cuts, kfx_ctx **out);
+int kfx_slice_work(kfx_ctx *ctx, const uint8_t *bgr, const float *depth_mm, int64_t *work);
+int kfx_slab_balance(const int64_t *slice_work, int Z, int world, int *cuts);
 /* stored slices [zb, zb+zn), owned slices [own0, own1) */
 int kfx_slab_info(kfx_ctx *ctx, int *zb, int *zn, int *own0, int *own1);
 /* One process per GPU: rank 0 creates the id, every rank passes it to

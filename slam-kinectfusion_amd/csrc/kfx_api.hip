@@ -81,6 +81,10 @@ constexpr int kInitialPoseCap = 1 << 16;
 
 }  // namespace
 
+// per-frame stage events: [0] start, [1] preprocess done, [2] ICP done,
+// [3] integrate done, [4] frame done, [5] local raycast done, [6] combine starts
+constexpr int kStageEvents = 7;
+
 struct kfx_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -113,7 +117,7 @@ struct kfx_ctx {
   // pipelined frame records its stage events into the next unused set
   int timing_every = 0;
   unsigned long long frame_seq = 0;
-  std::vector<hipEvent_t> tsets;  // 5 per sample
+  std::vector<hipEvent_t> tsets;  // kStageEvents per sample
   size_t tnext = 0;
   VolView vol{};
   DevState *st = nullptr;
@@ -140,7 +144,7 @@ struct kfx_ctx {
   hipGraphExec_t graph[2] = {nullptr, nullptr};  // [u16 input], inputs in raw[0]/bgr
   std::vector<hipGraphExec_t> staged_graph;       // one per staged frame (reads it in place)
   const uint8_t *last_bgr = nullptr;              // colour the last frame integrated
-  hipEvent_t ev[6]{};  // stage events; [5]: local raycast done (slab, before the combine)
+  hipEvent_t ev[kStageEvents]{};  // stage events; [5]: local raycast done, [6]: combine starts (slabs)
   float stage_ms[5]{};
   int pending = 0;      // frames enqueued since the last host sync
   int known_poses = 1;  // n_poses at the last sync
@@ -242,6 +246,7 @@ int enqueue_frame(kfx_ctx *c, FrameInput in, hipEvent_t *ev) {
   enqueue_pre(c, in, ev);
   int r = enqueue_track(c, in, ev, false);
   if (ev) (void)hipEventRecord(ev[5], c->stream);
+  if (ev) (void)hipEventRecord(ev[6], c->stream);
   if (!r && c->slab) r = enqueue_combine(c);
   if (ev) (void)hipEventRecord(ev[4], c->stream);
   return r;
@@ -399,6 +404,7 @@ int enqueue_frame_overlap(kfx_ctx *c, FrameInput in, hipEvent_t *ev) {
   if (ev) HIPCHK(hipEventRecord(ev[1], c->stream));
   int r = enqueue_track(c, in, ev, true);
   if (ev) HIPCHK(hipEventRecord(ev[5], c->stream));
+  if (ev) HIPCHK(hipEventRecord(ev[6], c->stream));
   if (!r && c->slab) r = enqueue_combine(c);
   if (ev) HIPCHK(hipEventRecord(ev[4], c->stream));
   HIPCHK(hipEventRecord(c->ev_free[p], c->stream));
@@ -482,8 +488,8 @@ int ensure_graph(kfx_ctx *c, FrameInput in, hipGraphExec_t *graph) {
 // or null when the frame is not sampled.
 hipEvent_t *timing_sample(kfx_ctx *c) {
   if (c->timing_every > 0 && !c->profiling && c->frame_seq++ % c->timing_every == 0 &&
-      6 * (c->tnext + 1) <= c->tsets.size())
-    return &c->tsets[6 * c->tnext++];
+      kStageEvents * (c->tnext + 1) <= c->tsets.size())
+    return &c->tsets[kStageEvents * c->tnext++];
   return nullptr;
 }
 
@@ -556,14 +562,18 @@ int finish_frame(kfx_ctx *c) {
 
 // Slab `rank` of `world` owns global slices [Z*rank/world, Z*(rank+1)/world)
 // and stores kSlabHalo more on each side (clipped to the volume).
-VolView make_vol(const kfx_params &p, int rank, int world) {
+VolView make_vol(const kfx_params &p, int rank, int world, const int *cuts = nullptr) {
   VolView v{};
   v.X = p.volu_dims[0];
   v.Y = p.volu_dims[1];
   v.Z = p.volu_dims[2];
   // slab boundaries on multiples of 8 slices (the point-extraction chunk), so
-  // slab clouds concatenate to the single-volume cloud
-  auto cut = [&](int r) { return r >= world ? v.Z : (int)((long long)v.Z * r / world) / 8 * 8; };
+  // slab clouds concatenate to the single-volume cloud; equal slice ranges
+  // unless explicit cuts are given (kfx_create_slab_cuts)
+  auto cut = [&](int r) {
+    if (cuts) return cuts[r];
+    return r >= world ? v.Z : (int)((long long)v.Z * r / world) / 8 * 8;
+  };
   v.own0 = cut(rank);
   v.own1 = cut(rank + 1);
   if (world > 1) {
@@ -687,7 +697,7 @@ int kfx_default_params(kfx_params *p) {
 }
 
 static int create_impl(const kfx_intrinsics *intr, const kfx_params *params, int device,
-                       int rank, int world, bool slab, kfx_ctx **out);
+                       int rank, int world, bool slab, kfx_ctx **out, const int *cuts = nullptr);
 
 int kfx_create(const kfx_intrinsics *intr, const kfx_params *params, int device, kfx_ctx **out) {
   return create_impl(intr, params, device, 0, 1, false, out);
@@ -701,8 +711,64 @@ int kfx_create_slab(const kfx_intrinsics *intr, const kfx_params *params, int de
   return create_impl(intr, params, device, rank, world, true, out);
 }
 
+int kfx_create_slab_cuts(const kfx_intrinsics *intr, const kfx_params *params, int device, int rank,
+                         int world, const int *cuts, kfx_ctx **out) {
+  if (world < 1 || rank < 0 || rank >= world || !cuts || !params) return set_err(KFX_ERR_ARG, "bad argument");
+  const int Z = params->volu_dims[2];
+  if (cuts[0] != 0 || cuts[world] != Z) return set_err(KFX_ERR_ARG, "cuts must run from 0 to Z");
+  for (int r = 0; r < world; ++r)
+    if (cuts[r + 1] - cuts[r] < 8 || (r > 0 && cuts[r] % 8))
+      return set_err(KFX_ERR_ARG, "cuts must be multiples of 8 with >= 8 slices per slab");
+  return create_impl(intr, params, device, rank, world, true, out, cuts);
+}
+
+int kfx_slab_balance(const int64_t *slice_work, int Z, int world, int *cuts) {
+  if (!slice_work || !cuts || world < 1 || Z < 8 * world) return set_err(KFX_ERR_ARG, "bad argument");
+  // a slab integrates its stored slices (owned + kSlabHalo on each side):
+  // choose cuts on multiples of 8 minimising the largest stored-range work
+  // (binary search on the bound, greedy longest-prefix feasibility)
+  std::vector<int64_t> pre(Z + 1, 0);
+  for (int z = 0; z < Z; ++z) pre[z + 1] = pre[z] + std::max<int64_t>(0, slice_work[z]);
+  auto load = [&](int a, int b) {  // work of the slab owning [a, b)
+    const int lo = world > 1 ? std::max(0, a - kSlabHalo) : 0, hi = world > 1 ? std::min(Z, b + kSlabHalo) : Z;
+    return pre[hi] - pre[lo];
+  };
+  auto plan = [&](int64_t bound, std::vector<int> &c) {  // greedy; true if world slabs suffice
+    c.assign(1, 0);
+    int a = 0;
+    for (int r = 0; r < world; ++r) {
+      if (r == world - 1) {
+        c.push_back(Z);
+        return load(a, Z) <= bound && Z - a >= 8;
+      }
+      // longest end b (multiple of 8, leaving >= 8 slices per later slab) within the bound
+      const int bmax = Z - 8 * (world - 1 - r);
+      int b = a + 8;
+      if (load(a, b) > bound) return false;
+      while (b + 8 <= bmax && load(a, b + 8) <= bound) b += 8;
+      c.push_back(b);
+      a = b;
+    }
+    return false;
+  };
+  int64_t lo = 0, hi = pre[Z] + 1;
+  std::vector<int> best, c;
+  while (lo < hi) {
+    const int64_t mid = lo + (hi - lo) / 2;
+    if (plan(mid, c)) {
+      hi = mid;
+      best = c;
+    } else {
+      lo = mid + 1;
+    }
+  }
+  if (best.empty() && !plan(lo, best)) return set_err(KFX_ERR_STATE, "no feasible cuts");
+  for (int r = 0; r <= world; ++r) cuts[r] = best[r];
+  return KFX_OK;
+}
+
 static int create_impl(const kfx_intrinsics *intr, const kfx_params *params, int device,
-                       int rank, int world, bool slab, kfx_ctx **out) {
+                       int rank, int world, bool slab, kfx_ctx **out, const int *cuts) {
   if (!intr || !params || !out) return set_err(KFX_ERR_ARG, "null argument");
   *out = nullptr;
   const kfx_params &p = *params;
@@ -781,7 +847,7 @@ static int create_impl(const kfx_intrinsics *intr, const kfx_params *params, int
   if ((r = dalloc(c, (void **)&c->inv_lambda, np0 * 4))) return fail(r);
   for (float2 *&d : c->dl0b)
     if ((r = dalloc(c, (void **)&d, np0 * 8 + 64))) return fail(r);
-  c->vol = make_vol(p, rank, world);
+  c->vol = make_vol(p, rank, world, cuts);
   const size_t n = nvox(c);
   {
     // tsdf and weight in ONE allocation, weight (u8) at a fixed offset (2 MiB-
@@ -1045,7 +1111,7 @@ int kfx_set_kernel_timing(kfx_ctx *c, int every, int max_samples) {
   c->frame_seq = 0;
   c->timing_every = every;
   if (every == 0) return KFX_OK;
-  c->tsets.assign(6 * (size_t)max_samples, nullptr);
+  c->tsets.assign(kStageEvents * (size_t)max_samples, nullptr);
   // timing-only events: no system-scope fence on record (a fence per event
   // cost ~6 us of GPU time each)
   for (hipEvent_t &e : c->tsets) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
@@ -1058,13 +1124,14 @@ int kfx_get_kernel_timing_ex(kfx_ctx *c, float out_ms[4], int *n_samples) {
   if (!out_ms) return set_err(KFX_ERR_ARG, "null out");
   HIPCHK(hipStreamSynchronize(c->stream));
   // sample events: [2] ICP done, [3] integrate done, [5] local raycast done,
+  // [6] combine starts (group members: after the other members' local phases),
   // [4] frame done; [1] the frame's tracking starts
-  static const int kFrom[4] = {1, 2, 3, 5}, kTo[4] = {2, 3, 5, 4};
+  static const int kFrom[4] = {1, 2, 3, 6}, kTo[4] = {2, 3, 5, 4};
   double acc[4] = {0, 0, 0, 0};
   for (size_t k = 0; k < c->tnext; ++k) {
     for (int i = 0; i < 4; ++i) {
       float ms = 0.f;
-      HIPCHK(hipEventElapsedTime(&ms, c->tsets[6 * k + kFrom[i]], c->tsets[6 * k + kTo[i]]));
+      HIPCHK(hipEventElapsedTime(&ms, c->tsets[kStageEvents * k + kFrom[i]], c->tsets[kStageEvents * k + kTo[i]]));
       acc[i] += ms;
     }
   }
@@ -1843,6 +1910,35 @@ int kfx_save_pointcloud(kfx_ctx *c, const char *path, int64_t cap) {
 
 // ---- Z-slab sharding -------------------------------------------------------
 
+int kfx_slice_work(kfx_ctx *c, const uint8_t *bgr, const float *depth_mm, int64_t *work) {
+  int r = check_ctx(c);
+  if (r) return r;
+  if (!bgr || !depth_mm || !work) return set_err(KFX_ERR_ARG, "null argument");
+  HIPCHK(hipStreamSynchronize(c->pstream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  set_par(c, 0);
+  const size_t np = (size_t)c->intr.width * c->intr.height;
+  HIPCHK(hipMemcpyAsync(c->raw[0], depth_mm, np * 4, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(c->bgr, bgr, np * 3, hipMemcpyHostToDevice, c->stream));
+  enqueue_pre(c, {c->raw[0], nullptr, c->bgr}, nullptr);  // the frame's {depth, 1/lambda} table
+  const int Z = c->vol.Z;
+  unsigned long long *hist = nullptr;
+  HIPCHK(hipMalloc(&hist, sizeof(unsigned long long) * (size_t)Z));
+  hipError_t e = hipMemsetAsync(hist, 0, sizeof(unsigned long long) * (size_t)Z, c->stream);
+  if (e == hipSuccess) {
+    // the first frame integrates at the identity camera pose: vol2cam = volume pose
+    launch_slice_work(c->stream, c->vol, to_dev(c->p.volu_pose), c->g[0], c->dl0, hist);
+    e = hipGetLastError();
+  }
+  std::vector<unsigned long long> h(Z);
+  if (e == hipSuccess) e = hipMemcpyAsync(h.data(), hist, sizeof(unsigned long long) * (size_t)Z, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  (void)hipFree(hist);
+  if (e != hipSuccess) return set_err(KFX_ERR_HIP, std::string("slice_work: ") + hipGetErrorString(e));
+  for (int z = 0; z < Z; ++z) work[z] = (int64_t)h[z];
+  return KFX_OK;
+}
+
 int kfx_slab_info(kfx_ctx *c, int *zb, int *zn, int *own0, int *own1) {
   if (!c) return set_err(KFX_ERR_ARG, "null context");
   if (zb) *zb = c->vol.zb;
@@ -1910,7 +2006,7 @@ int kfx_pipeline_group(kfx_ctx **cs, int n, const uint8_t *bgr, const float *dep
       tev[k] = timing_sample(c);
       enqueue_local(c, {c->raw[0], nullptr, c->bgr}, tev[k]);
       if (tev[k]) {  // timed: this member runs alone, as on a GPU of its own
-        HIPCHK(hipEventRecord(tev[k][5], c->stream));
+        HIPCHK(hipEventRecord(tev[k][5], c->stream));  // [6] is recorded when the combine starts
         HIPCHK(hipStreamSynchronize(c->stream));
       }
     }
@@ -1958,6 +2054,8 @@ int kfx_pipeline_group(kfx_ctx **cs, int n, const uint8_t *bgr, const float *dep
   }
   kfx_ctx *c0 = cs[0];
   if ((r = check_ctx(c0))) return r;
+  for (int k = 0; k < n; ++k)  // every member's combine starts with the shared reductions
+    if (tev[k]) HIPCHK(hipEventRecord(tev[k][6], c0->stream));
   launch_group_reduce(c0->stream, kin, n, kout, n, np, false);
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(c0->stream));
@@ -2004,6 +2102,7 @@ int kfx_slab_frame_local(kfx_ctx *c, const uint8_t *bgr, const float *depth_mm, 
   hipEvent_t *tev = timing_sample(c);
   enqueue_local(c, {c->raw[0], nullptr, c->bgr}, tev);
   if (tev) HIPCHK(hipEventRecord(tev[5], c->stream));
+  if (tev) HIPCHK(hipEventRecord(tev[6], c->stream));  // re-recorded when the combine starts
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(keys, c->key_local, np * 4, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipMemcpyAsync(payload, c->key_local + np, 4 * np * 4, hipMemcpyDeviceToHost, c->stream));
@@ -2021,6 +2120,7 @@ int kfx_slab_frame_finish(kfx_ctx *c, const uint32_t *payload) {
   c->ext_open = false;
   const size_t np = (size_t)c->intr.width * c->intr.height;
   uint32_t *pay = c->key_local + np;
+  if (c->ext_pending) HIPCHK(hipEventRecord(c->ext_pending[6], c->stream));
   HIPCHK(hipMemcpyAsync(pay, payload, 4 * np * 4, hipMemcpyHostToDevice, c->stream));
   launch_slab_expand(c->stream, c->g[0], pay, c->cur, c->prev, c->st, c->pose_log, to_dev(c->p.volu_pose));
   launch_resize(c->stream, c->L, c->g, c->cur, c->prev, c->st, nullptr);

@@ -280,6 +280,9 @@ void launch_export_soa(hipStream_t s, VolView v, int z0, int nz, int16_t *t, int
 void launch_occ_rebuild(hipStream_t s, VolView v);
 // z-chunks per column tile of k_integrate (the iperm item count is tiles x this)
 int integrate_chunks(const VolView &v);
+// per global slice: voxels passing integrate's depth test at vol2cam (an estimate, slab balancing)
+void launch_slice_work(hipStream_t s, const VolView &v, DevPose vol2cam, LevelGeom g0, const float2 *dl0,
+                       unsigned long long *hist);
 bool integrate_planned(const VolView &v);
 // owned-slice records of n (x, y) columns (device cols), column-major outputs
 void launch_gather_columns(hipStream_t s, VolView v, const int32_t *cols, int n, int16_t *t, int16_t *w,

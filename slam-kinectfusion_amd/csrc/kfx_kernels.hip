@@ -23,6 +23,9 @@
 #ifndef KFX_RAY_OCC
 #define KFX_RAY_OCC 5  // raycast: waves per SIMD the register budget must allow (4800 waves at VGA: one round at 5)
 #endif
+#ifndef KFX_RAY_SREPLAY
+#define KFX_RAY_SREPLAY 0  // raycast skip replay as four scalar add chains (A/B)
+#endif
 #ifndef KFX_RAY_KR
 #define KFX_RAY_KR 14  // raycast: samples per batch (loads in flight per lane)
 #endif
@@ -1266,6 +1269,33 @@ struct RayMem<false> {
   }
 };
 
+// One step of a long add chain (integrate's vc replay): the IEEE adds of the
+// reference, kept as three scalar v_add_f32 chains — the compiler otherwise
+// packs {x, y} into v_pk_add_f32, whose dependent latency makes such chains
+// several times slower (tools/chain_bench.hip).
+#ifndef KFX_SREPLAY
+#define KFX_SREPLAY 1
+#endif
+__device__ __forceinline__ f3 replay_add(f3 a, f3 b) {
+#if KFX_SREPLAY
+  asm volatile("v_add_f32 %0, %0, %1" : "+v"(a.x) : "v"(b.x));
+  asm volatile("v_add_f32 %0, %0, %1" : "+v"(a.y) : "v"(b.y));
+  asm volatile("v_add_f32 %0, %0, %1" : "+v"(a.z) : "v"(b.z));
+  return a;
+#else
+  return add(a, b);
+#endif
+}
+// a advanced from slice z to slice za (za - z adds when za > z), 8 per trip
+__device__ __forceinline__ f3 replay(f3 a, f3 b, int z, int za) {
+  for (; z + 8 <= za; z += 8) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) a = replay_add(a, b);
+  }
+  for (; z < za; ++z) a = replay_add(a, b);
+  return a;
+}
+
 // Integrate's vol2cam pose of this frame (tsdf_volume.cpp:50) and the frame
 // kind (2: reset); stage seams pass an explicit pose.
 __device__ __forceinline__ int int_frame_pose(const DevState *st, const DevPose *log, const DevPose &vpose,
@@ -1404,8 +1434,8 @@ __global__ __launch_bounds__(64) void k_int_plan(VolView v, LevelGeom g, const f
     if (za > z) vc = add(vc, scl(zs, (float)(za - z)));
     z = max(z, za);
 #else
-#pragma unroll 8
-    for (; z < za; ++z) vc = add(vc, zs);
+    vc = replay(vc, zs, z, za);
+    z = max(z, za);
 #endif
     v.pckpt[((size_t)c * tiles + tile) * 64 + lane] = make_float4(vc.x, vc.y, vc.z, __uint_as_float(zbits));
     if (lane == 0) rg[(size_t)c * tiles] = make_int2(za, zb);
@@ -1511,8 +1541,8 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
     if (za > z) vc = add(vc, scl(zs, (float)(za - z)));
     z = max(z, za);
 #else
-#pragma unroll 8
-    for (; z < za; ++z) vc = add(vc, zs);
+    vc = replay(vc, zs, z, za);
+    z = max(z, za);
 #endif
   }
   const int la = max(za, zl), lb = min(zb, zh);  // this lane's voxels of the chunk
@@ -2062,6 +2092,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KFX_RAY_OCC
           const int nf = min(n, max(0, (int)((tfar - ray_len) * rstep) - 2));
 #endif
           int i = 0;
+#if KFX_RAY_SREPLAY  // four scalar add chains (see replay_add)
+          {
+            float px = pxy.x, py = pxy.y, pz = pzr.x, pr = pzr.y;
+            for (; i + 8 <= nf; i += 8) {
+#pragma unroll
+              for (int u = 0; u < 8; ++u) {
+                asm volatile("v_add_f32 %0, %0, %1" : "+v"(px) : "v"(sxy.x));
+                asm volatile("v_add_f32 %0, %0, %1" : "+v"(py) : "v"(sxy.y));
+                asm volatile("v_add_f32 %0, %0, %1" : "+v"(pz) : "v"(szr.x));
+                asm volatile("v_add_f32 %0, %0, %1" : "+v"(pr) : "v"(szr.y));
+              }
+            }
+            pxy = {px, py};
+            pzr = {pz, pr};
+          }
+#else
           for (; i + 8 <= nf; i += 8) {
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
@@ -2069,6 +2115,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KFX_RAY_OCC
               pzr = pzr + szr;
             }
           }
+#endif
           for (; i < nf; ++i) {
             pxy = pxy + sxy;
             pzr = pzr + szr;
@@ -3385,6 +3432,47 @@ void launch_scan(hipStream_t s, const unsigned *counts, unsigned long long *offs
   hipLaunchKernelGGL(k_scan_local, dim3((unsigned)nb), dim3(1024), 0, s, counts, offsets, bsum, n);
   hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, s, bsum, (int)nb, total);
   hipLaunchKernelGGL(k_scan_add, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, offsets, bsum, n);
+}
+
+// Per-slice integrate work of one frame (Z-slab balancing):
+// for every global slice z, the voxels whose depth test passes (sdf >=
+// -trunc, tsdf_volume.cu:56-71) at pose P, counted from the level-0 {depth,
+// 1/lambda} table.  An estimate for choosing slab cuts — vc is computed
+// directly, not accumulated — so it is not bit-exact with integrate.
+// One thread per (x, y) column; per-block LDS histogram, flushed once.
+__global__ __launch_bounds__(256) void k_slice_work(int X, int Y, int Z, float vs, float trunc, DevPose P,
+                                                    LevelGeom g, const float2 *__restrict__ dl,
+                                                    unsigned long long *hist) {
+  extern __shared__ unsigned lh[];
+  for (int i = threadIdx.x; i < Z; i += blockDim.x) lh[i] = 0u;
+  __syncthreads();
+  const int col = blockIdx.x * blockDim.x + threadIdx.x;
+  if (col < X * Y) {
+    const int x = col % X, y = col / X;
+    const f3 vx = {(float)x * vs, (float)y * vs, 0.f};
+    const f3 c0 = add(rmul(P.R, vx), {P.t[0], P.t[1], P.t[2]});
+    const f3 zs = {P.R[2] * vs, P.R[5] * vs, P.R[8] * vs};
+    for (int z = 1; z < Z; ++z) {
+      const f3 vc = add(c0, scl(zs, (float)z));
+      if (!(vc.z > 0.f)) continue;
+      const float iz = 1.f / vc.z;
+      const int u = (int)rintf(vc.x * iz * g.fx + g.cx), w = (int)rintf(vc.y * iz * g.fy + g.cy);
+      if (u < 0 || u >= g.w || w < 0 || w >= g.h) continue;
+      const float2 d = dl[(size_t)w * g.w + u];
+      if (!(d.x > 0.f)) continue;
+      if (d.x - d.y * sqrtf(dot(vc, vc)) >= -trunc) atomicAdd(&lh[z], 1u);
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < Z; i += blockDim.x)
+    if (lh[i]) atomicAdd(&hist[i], (unsigned long long)lh[i]);
+}
+
+void launch_slice_work(hipStream_t s, const VolView &v, DevPose vol2cam, LevelGeom g0, const float2 *dl0,
+                       unsigned long long *hist) {
+  const int cols = v.X * v.Y;
+  hipLaunchKernelGGL(k_slice_work, dim3((cols + 255) / 256), dim3(256), (size_t)v.Z * 4, s, v.X, v.Y, v.Z, v.vs[0],
+                     v.trunc, vol2cam, g0, dl0, hist);
 }
 
 void launch_inv_lambda(hipStream_t s, LevelGeom g0, float *inv_lambda) {

@@ -19,7 +19,7 @@ from .abi import (KFX_FRAME_CUR, KFX_FRAME_PREV, KFX_OK, KFX_TRACKING_LOST, Intr
                   default_params, fptr, i16ptr, i64ptr, u8ptr, u16ptr)
 
 __all__ = ["KinectFusion", "KfxError", "Dataset", "png_info", "png_read_bgr8", "png_read_depth", "parse_intr",
-           "comm_unique_id", "pipeline_group", "write_ply", "lib", "build", "LIB_PATH", "Intrinsics", "Params", "Pose",
+           "comm_unique_id", "pipeline_group", "slab_balance", "write_ply", "lib", "build", "LIB_PATH", "Intrinsics", "Params", "Pose",
            "default_params", "KFX_FRAME_CUR", "KFX_FRAME_PREV", "KFX_OK", "KFX_TRACKING_LOST", "EXPORTS"]
 
 _PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -33,7 +33,7 @@ EXPORTS = [
     "kfx_write_poses_txt", "kfx_get_frame_maps", "kfx_set_frame_maps", "kfx_download_tsdf",
     "kfx_upload_tsdf", "kfx_download_volume_soa", "kfx_stage_preprocess", "kfx_stage_icp_accumulate",
     "kfx_stage_icp", "kfx_stage_integrate", "kfx_stage_raycast", "kfx_set_profiling", "kfx_get_stage_ms",
-    "kfx_integrate_counts", "kfx_integrate_stats", "kfx_raycast_stats", "kfx_download_columns", "kfx_pipeline_async", "kfx_pipeline_async_u16", "kfx_register_host_buffer", "kfx_unregister_host_buffer", "kfx_slab_mask_payload", "kfx_slab_expand", "kfx_set_icp_allreduce", "kfx_create_slab", "kfx_slab_info", "kfx_comm_get_unique_id", "kfx_comm_init",
+    "kfx_integrate_counts", "kfx_integrate_stats", "kfx_raycast_stats", "kfx_download_columns", "kfx_pipeline_async", "kfx_pipeline_async_u16", "kfx_register_host_buffer", "kfx_unregister_host_buffer", "kfx_slab_mask_payload", "kfx_slab_expand", "kfx_set_icp_allreduce", "kfx_create_slab", "kfx_create_slab_cuts", "kfx_slice_work", "kfx_slab_balance", "kfx_slab_info", "kfx_comm_get_unique_id", "kfx_comm_init",
     "kfx_pipeline_group", "kfx_slab_frame_local", "kfx_slab_frame_finish", "kfx_render", "kfx_volume_checksum", "kfx_extract_points", "kfx_write_ply", "kfx_save_pointcloud",
     "kfx_extract_mesh", "kfx_write_ply_mesh", "kfx_get_extract_ms",
     "kfx_dataset_open", "kfx_dataset_info", "kfx_dataset_read", "kfx_dataset_close", "kfx_png_info",
@@ -111,6 +111,9 @@ def lib():
         "kfx_unregister_host_buffer": ([vp, vp], i),
         "kfx_download_columns": ([vp, P(C.c_int32), i, P(C.c_int16), P(C.c_int16), P(C.c_uint32)], i),
         "kfx_create_slab": ([P(Intrinsics), P(Params), i, i, i, P(vp)], i),
+        "kfx_create_slab_cuts": ([P(Intrinsics), P(Params), i, i, i, P(i), P(vp)], i),
+        "kfx_slice_work": ([vp, P(C.c_uint8), P(f), P(C.c_int64)], i),
+        "kfx_slab_balance": ([P(C.c_int64), i, i, P(i)], i),
         "kfx_slab_info": ([vp, P(i), P(i), P(i), P(i)], i),
         "kfx_comm_get_unique_id": ([P(C.c_uint8)], i),
         "kfx_comm_init": ([vp, P(C.c_uint8)], i),
@@ -261,6 +264,15 @@ def comm_unique_id() -> bytes:
     return bytes(buf)
 
 
+def slab_balance(slice_work, world: int) -> list:
+    """kfx_slab_balance: world + 1 slab cuts (multiples of 8) minimising the
+    largest slab's stored-range work for a per-slice work histogram."""
+    w = np.ascontiguousarray(slice_work, np.int64)
+    cu = (C.c_int * (world + 1))()
+    _check(lib().kfx_slab_balance(i64ptr(w), int(w.size), int(world), cu), "kfx_slab_balance")
+    return list(cu)
+
+
 def pipeline_group(members, color: np.ndarray, depth: np.ndarray) -> int:
     """One pipeline() frame over all Z-slabs held in this process
     (members[k] = slab k of len(members))."""
@@ -275,10 +287,11 @@ class KinectFusion:
     """kf::kinectfusion over the C-ABI.  Images: depth (H,W) float32/uint16 mm,
     colour (H,W,3) uint8 BGR."""
 
-    def __init__(self, intr, params: Params | None = None, device: int = 0, slab=None):
+    def __init__(self, intr, params: Params | None = None, device: int = 0, slab=None, cuts=None):
         """slab=(rank, world): this instance owns Z-slab `rank` of `world`
-        (kfx_create_slab); combine through comm_init (one process per GPU) or
-        pipeline_group (all slabs in this process)."""
+        (kfx_create_slab; with cuts, world + 1 slice boundaries:
+        kfx_create_slab_cuts); combine through comm_init (one process per GPU)
+        or pipeline_group (all slabs in this process)."""
         self.intr = Intrinsics.from_any(intr)
         self.params = params if params is not None else default_params()
         h = C.c_void_p()
@@ -286,8 +299,13 @@ class KinectFusion:
             _check(lib().kfx_create(C.byref(self.intr), C.byref(self.params), device, C.byref(h)), "kfx_create")
         else:
             rank, world = slab
-            _check(lib().kfx_create_slab(C.byref(self.intr), C.byref(self.params), device, int(rank), int(world),
-                                         C.byref(h)), "kfx_create_slab")
+            if cuts is None:
+                _check(lib().kfx_create_slab(C.byref(self.intr), C.byref(self.params), device, int(rank), int(world),
+                                             C.byref(h)), "kfx_create_slab")
+            else:
+                cu = (C.c_int * (world + 1))(*[int(x) for x in cuts])
+                _check(lib().kfx_create_slab_cuts(C.byref(self.intr), C.byref(self.params), device, int(rank),
+                                                  int(world), cu, C.byref(h)), "kfx_create_slab_cuts")
         self._h = h
         self.slab = slab
         X, Y, Z = (int(d) for d in self.params.volu_dims)
@@ -517,6 +535,15 @@ class KinectFusion:
         pay = np.ascontiguousarray(payload, np.uint32)
         rc = lib().kfx_slab_frame_finish(self._h, pay.ctypes.data_as(C.POINTER(C.c_uint32)))
         return _check(rc, "kfx_slab_frame_finish", ok=(KFX_OK, KFX_TRACKING_LOST))
+
+    def slice_work(self, color: np.ndarray, depth: np.ndarray) -> np.ndarray:
+        """(Z,) int64: per global slice, the voxels this frame's integrate would
+        update at the first frame's pose (kfx_slice_work; slab balancing)."""
+        color = np.ascontiguousarray(color, np.uint8)
+        d = np.ascontiguousarray(depth, np.float32)
+        out = np.zeros(self.dims[2], np.int64)
+        _check(lib().kfx_slice_work(self._h, u8ptr(color), fptr(d), i64ptr(out)), "kfx_slice_work")
+        return out
 
     def comm_init(self, uid: bytes):
         buf = (C.c_uint8 * 128).from_buffer_copy(uid)

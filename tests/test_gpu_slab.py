@@ -308,3 +308,35 @@ def test_slab_two_processes_gloo_match_single_volume(seq_qvga, tmp_path):
         cs[4 * o0 * sl:4 * o1 * sl] = d["c"][4 * o0 * sl:4 * o1 * sl]
     assert np.array_equal(ts, t) and np.array_equal(ws, w) and np.array_equal(cs, c) and w.any()
     single.close()
+
+
+def test_balanced_cuts_group_matches_single_volume(seq_qvga):
+    """Work-balanced slabs (kfx_slice_work -> kfx_slab_balance ->
+    kfx_create_slab_cuts) reproduce the single volume bit for bit, and the
+    slice-work estimate matches the first frame's counted integrate work."""
+    from kfx import slab_balance
+    bgr, dep, _ = seq_qvga
+    intr = synth.Intrinsics.qvga()
+    I = Intrinsics.from_any(intr)
+    p = default_params(dims=64, range_m=L_VOL)
+    single, st = _single(intr, p, bgr, dep)
+    probe = KinectFusion(I, p, slab=(0, 4))  # any context: only its frame buffers are used
+    work = probe.slice_work(bgr[0], dep[0].astype(np.float32))
+    probe.close()
+    first = KinectFusion(I, p)
+    first.pipeline(bgr[0], dep[0].astype(np.float32))
+    upd = first.integrate_stats()["updated"]
+    first.close()
+    assert work[0] == 0 and abs(int(work.sum()) - upd) <= 0.01 * upd, (int(work.sum()), upd)
+    world = 3
+    cuts = slab_balance(work, world)
+    assert cuts[0] == 0 and cuts[-1] == 64 and all(b - a >= 8 for a, b in zip(cuts, cuts[1:]))
+    members = [KinectFusion(I, p, slab=(r, world), cuts=cuts) for r in range(world)]
+    for r, m in enumerate(members):
+        assert m.slab_info()[2:] == (cuts[r], cuts[r + 1])
+    gst = [pipeline_group(members, bgr[k], dep[k].astype(np.float32)) for k in range(len(dep))]
+    assert gst == st == [KFX_OK] * len(dep)
+    _compare(single, members)
+    for m in members:
+        m.close()
+    single.close()

@@ -67,44 +67,53 @@ def main():
     sp = single.pose_record
     single.close()
 
-    members = [kfx.KinectFusion(I, p, slab=(r, a.world)) for r in range(a.world)]
-    for i in order[:a.warmup]:
-        kfx.pipeline_group(members, bgr[i], dep[i])
-    for m in members:
-        m.set_kernel_timing(1, a.frames + 2)
-    t0 = time.perf_counter()
-    for i in order[a.warmup:a.warmup + a.frames]:
-        assert kfx.pipeline_group(members, bgr[i], dep[i]) == kfx.KFX_OK
-    t_group = time.perf_counter() - t0
-    slabs = []
-    for r, m in enumerate(members):
-        k = m.kernel_timing()
-        w = m.integrate_stats()
-        zb, zn, o0, o1 = m.slab_info()
-        slabs.append({"rank": r, "owned_slices": [o0, o1], "stored_slices": [zb, zb + zn],
-                      "icp_ms": k["icp"], "integrate_ms": k["integrate"], "raycast_local_ms": k["raycast_local"],
-                      "combine_ms": k["combine"], "integrate_updated": w["updated"], "samples": k["samples"]})
-    assert all(np.array_equal(m.pose_record, sp) for m in members), "slab poses differ from the single volume"
-    for m in members:
-        m.close()
-    it = np.array([s["integrate_ms"] for s in slabs])
-    up = np.array([s["integrate_updated"] for s in slabs], dtype=np.float64)
-    rec["slabs"] = slabs
-    rec["group_wall_ms_per_frame"] = 1e3 * t_group / a.frames
-    rec["integrate_imbalance_max_over_mean"] = float(it.max() / it.mean())
-    rec["updated_imbalance_max_over_mean"] = float(up.max() / up.mean())
-    rec["max_slab_over_single_integrate"] = float(it.max() / rec["single"]["integrate_ms"])
+    def group(cuts):
+        members = [kfx.KinectFusion(I, p, slab=(r, a.world), cuts=cuts) for r in range(a.world)]
+        for i in order[:a.warmup]:
+            kfx.pipeline_group(members, bgr[i], dep[i])
+        for m in members:
+            m.set_kernel_timing(1, a.frames + 2)
+        t0 = time.perf_counter()
+        for i in order[a.warmup:a.warmup + a.frames]:
+            assert kfx.pipeline_group(members, bgr[i], dep[i]) == kfx.KFX_OK
+        t_group = time.perf_counter() - t0
+        slabs = []
+        for r, m in enumerate(members):
+            k = m.kernel_timing()
+            w = m.integrate_stats()
+            zb, zn, o0, o1 = m.slab_info()
+            slabs.append({"rank": r, "owned_slices": [o0, o1], "stored_slices": [zb, zb + zn],
+                          "icp_ms": k["icp"], "integrate_ms": k["integrate"], "raycast_local_ms": k["raycast_local"],
+                          "combine_ms": k["combine"], "integrate_updated": w["updated"], "samples": k["samples"]})
+        assert all(np.array_equal(m.pose_record, sp) for m in members), "slab poses differ from the single volume"
+        for m in members:
+            m.close()
+        it = np.array([s["integrate_ms"] for s in slabs])
+        up = np.array([s["integrate_updated"] for s in slabs], dtype=np.float64)
+        # per-rank critical path of one frame at N GPUs (replicated ICP, RCCL not included)
+        crit = [s["icp_ms"] + s["integrate_ms"] + s["raycast_local_ms"] for s in slabs]
+        return {"cuts": cuts, "slabs": slabs, "group_wall_ms_per_frame": 1e3 * t_group / a.frames,
+                "integrate_imbalance_max_over_mean": float(it.max() / it.mean()),
+                "updated_imbalance_max_over_mean": float(up.max() / up.mean()),
+                "max_slab_over_single_integrate": float(it.max() / rec["single"]["integrate_ms"]),
+                "max_rank_icp_integrate_raycast_ms": float(max(crit))}
+
     rec["ideal"] = 1.0 / a.world
-    # per-rank critical path of one frame at N GPUs (replicated ICP, RCCL not included)
-    crit = [s["icp_ms"] + s["integrate_ms"] + s["raycast_local_ms"] for s in slabs]
-    rec["max_rank_icp_integrate_raycast_ms"] = float(max(crit))
     rec["single_icp_integrate_raycast_ms"] = float(sum(rec["single"][k] for k in ("icp_ms", "integrate_ms",
                                                                                     "raycast_ms")))
+    rec["equal_cuts"] = group(None)
+    # work-balanced cuts from the first frame's per-slice work (what bench.py uses at N > 1)
+    probe = kfx.KinectFusion(I, p, slab=(0, n // 16))
+    work = probe.slice_work(bgr[order[0]], dep[order[0]])
+    probe.close()
+    rec["slice_work_first_frame"] = [int(x) for x in work]
+    rec["balanced_cuts"] = group(kfx.slab_balance(work, a.world))
     out = a.out or os.path.join(ROOT, "gpurun_out", f"slabs_{a.config}.json")
     os.makedirs(os.path.dirname(out), exist_ok=True)
     json.dump(rec, open(out, "w"), indent=1)
-    print(json.dumps({k: rec[k] for k in ("config", "integrate_imbalance_max_over_mean",
-                                          "max_slab_over_single_integrate", "ideal")}))
+    print(json.dumps({"config": rec["config"], "ideal": rec["ideal"],
+                      **{f"{k}:{q}": rec[k][q] for k in ("equal_cuts", "balanced_cuts")
+                         for q in ("integrate_imbalance_max_over_mean", "max_slab_over_single_integrate")}}))
 
 
 if __name__ == "__main__":
