@@ -348,14 +348,20 @@ int kfx_create_slab(const kfx_intrinsics *intr, const kfx_params *params, int de
                     int rank, int world, kfx_ctx **out);
 /* Work-balanced slabs: slab r owns [cuts[r], cuts[r+1]) (cuts[0] = 0,
  * cuts[world] = Z, multiples of 8, >= 8 slices each; every rank passes the
- * same cuts).  kfx_slice_work gives, per global slice, the voxels a frame's
- * integrate would update at the first frame's pose (any context, slab or not;
- * an estimate from the frame's filtered depth); kfx_slab_balance turns such a
+ * same cuts).  kfx_slice_work gives, per global slice, an estimate of a
+ * frame's integrate cost at the first frame's pose (any context, slab or not;
+ * from the frame's filtered depth: voxel slots visited, updated voxels
+ * weighted more); kfx_slab_balance turns such a
  * histogram into cuts minimising the largest slab's stored-range work (halos
  * included).  Results stay bit-identical to the single volume for any cuts. */
 int kfx_create_slab_cuts(const kfx_intrinsics *intr, const kfx_params *params, int device,
                          int rank, int world, const int *cuts, kfx_ctx **out);
 int kfx_slice_work(kfx_ctx *ctx, const uint8_t *bgr, const float *depth_mm, int64_t *work);
+/* The two parts kfx_slice_work weighs, per global slice: cover = the voxel
+ * slots integrate's waves step through (64 per column tile whose z interval
+ * holds the slice), updated = the voxels whose depth test passes. */
+int kfx_slice_work_parts(kfx_ctx *ctx, const uint8_t *bgr, const float *depth_mm, int64_t *cover,
+                         int64_t *updated);
 int kfx_slab_balance(const int64_t *slice_work, int Z, int world, int *cuts);
 /* stored slices [zb, zb+zn), owned slices [own0, own1) */
 int kfx_slab_info(kfx_ctx *ctx, int *zb, int *zn, int *own0, int *own1);

@@ -112,6 +112,7 @@ struct kfx_ctx {
   hipStream_t pstream = nullptr;
   hipEvent_t ev_prep = nullptr, ev_free[2]{};
   hipEvent_t ev_icp = nullptr;  // after the last overlapped frame's ICP (the next preprocess starts there)
+  bool group_chain = false;     // kfx_pipeline_group member: record ev_icp after every ICP
 
   // sampled kernel timing (kfx_set_kernel_timing): every `timing_every`-th
   // pipelined frame records its stage events into the next unused set
@@ -194,6 +195,9 @@ int dalloc(kfx_ctx *c, void **p, size_t bytes) {
 
 #ifndef KFX_PREP_AFTER_ICP
 #define KFX_PREP_AFTER_ICP 1  // overlapped frames: next preprocess waits for this frame's ICP
+#endif
+#ifndef KFX_UPDATED_COST
+#define KFX_UPDATED_COST 2  // slab balancing: cost of an updated voxel over a visited slot (slice_cost)
 #endif
 #ifndef KFX_VOL_PAD
 #define KFX_VOL_PAD 4096  // weight offset past the 2 MiB-rounded tsdf (bytes)
@@ -362,7 +366,9 @@ int enqueue_track(kfx_ctx *c, FrameInput in, hipEvent_t *ev, bool begin) {
     }
   }
   if (ev) (void)hipEventRecord(ev[2], s);
-  if (begin) (void)hipEventRecord(c->ev_icp, s);  // overlapped frames: the next preprocess waits here
+  // overlapped frames: the next preprocess waits here; a group: the next
+  // member's ICP on this device waits here
+  if (begin || c->group_chain) (void)hipEventRecord(c->ev_icp, s);
   enqueue_map(c, in, ev);
   return r;
 }
@@ -721,6 +727,13 @@ int kfx_create_slab_cuts(const kfx_intrinsics *intr, const kfx_params *params, i
       return set_err(KFX_ERR_ARG, "cuts must be multiples of 8 with >= 8 slices per slab");
   return create_impl(intr, params, device, rank, world, true, out, cuts);
 }
+
+// Integrate cost of one slice from kfx_slice_work_parts, in voxel-slot units:
+// every slot a wave steps through, plus kUpdatedCost more per updated voxel
+// (its tsdf / weight / colour read-modify-write).  Fitted to per-slab
+// integrate times (tools/slab_record.py).
+constexpr int64_t kUpdatedCost = KFX_UPDATED_COST;
+static int64_t slice_cost(int64_t cover, int64_t updated) { return cover + kUpdatedCost * updated; }
 
 int kfx_slab_balance(const int64_t *slice_work, int Z, int world, int *cuts) {
   if (!slice_work || !cuts || world < 1 || Z < 8 * world) return set_err(KFX_ERR_ARG, "bad argument");
@@ -1910,32 +1923,47 @@ int kfx_save_pointcloud(kfx_ctx *c, const char *path, int64_t cap) {
 
 // ---- Z-slab sharding -------------------------------------------------------
 
-int kfx_slice_work(kfx_ctx *c, const uint8_t *bgr, const float *depth_mm, int64_t *work) {
+int kfx_slice_work_parts(kfx_ctx *c, const uint8_t *bgr, const float *depth_mm, int64_t *cover, int64_t *updated) {
   int r = check_ctx(c);
   if (r) return r;
-  if (!bgr || !depth_mm || !work) return set_err(KFX_ERR_ARG, "null argument");
+  if (!bgr || !depth_mm || !cover || !updated) return set_err(KFX_ERR_ARG, "null argument");
   HIPCHK(hipStreamSynchronize(c->pstream));
   HIPCHK(hipStreamSynchronize(c->stream));
   set_par(c, 0);
   const size_t np = (size_t)c->intr.width * c->intr.height;
   HIPCHK(hipMemcpyAsync(c->raw[0], depth_mm, np * 4, hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipMemcpyAsync(c->bgr, bgr, np * 3, hipMemcpyHostToDevice, c->stream));
-  enqueue_pre(c, {c->raw[0], nullptr, c->bgr}, nullptr);  // the frame's {depth, 1/lambda} table
+  enqueue_pre(c, {c->raw[0], nullptr, c->bgr}, nullptr);  // the frame's {depth, 1/lambda} table and max depth
   const int Z = c->vol.Z;
+  const size_t n = 2 * (size_t)Z + 1;
   unsigned long long *hist = nullptr;
-  HIPCHK(hipMalloc(&hist, sizeof(unsigned long long) * (size_t)Z));
-  hipError_t e = hipMemsetAsync(hist, 0, sizeof(unsigned long long) * (size_t)Z, c->stream);
+  HIPCHK(hipMalloc(&hist, sizeof(unsigned long long) * n));
+  hipError_t e = hipMemsetAsync(hist, 0, sizeof(unsigned long long) * n, c->stream);
   if (e == hipSuccess) {
     // the first frame integrates at the identity camera pose: vol2cam = volume pose
     launch_slice_work(c->stream, c->vol, to_dev(c->p.volu_pose), c->g[0], c->dl0, hist);
     e = hipGetLastError();
   }
-  std::vector<unsigned long long> h(Z);
-  if (e == hipSuccess) e = hipMemcpyAsync(h.data(), hist, sizeof(unsigned long long) * (size_t)Z, hipMemcpyDeviceToHost, c->stream);
+  std::vector<unsigned long long> h(n);
+  if (e == hipSuccess) e = hipMemcpyAsync(h.data(), hist, sizeof(unsigned long long) * n, hipMemcpyDeviceToHost, c->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   (void)hipFree(hist);
   if (e != hipSuccess) return set_err(KFX_ERR_HIP, std::string("slice_work: ") + hipGetErrorString(e));
-  for (int z = 0; z < Z; ++z) work[z] = (int64_t)h[z];
+  int64_t run = 0;
+  for (int z = 0; z < Z; ++z) {
+    run += (int64_t)h[z];  // prefix sum of the cover differences
+    cover[z] = run;
+    updated[z] = (int64_t)h[Z + 1 + z];
+  }
+  return KFX_OK;
+}
+
+int kfx_slice_work(kfx_ctx *c, const uint8_t *bgr, const float *depth_mm, int64_t *work) {
+  if (!c || !work) return set_err(KFX_ERR_ARG, "null argument");
+  std::vector<int64_t> cover(c->vol.Z), upd(c->vol.Z);
+  const int r = kfx_slice_work_parts(c, bgr, depth_mm, cover.data(), upd.data());
+  if (r) return r;
+  for (int z = 0; z < c->vol.Z; ++z) work[z] = slice_cost(cover[z], upd[z]);
   return KFX_OK;
 }
 
@@ -2003,6 +2031,12 @@ int kfx_pipeline_group(kfx_ctx **cs, int n, const uint8_t *bgr, const float *dep
     if (sharded) {
       enqueue_pre(c, {c->raw[0], nullptr, c->bgr}, nullptr);
     } else {
+      // Two persistent ICP grids spinning on one device at once can each hold
+      // CUs the other's grid barrier waits for (the watchdog then fires): a
+      // member's ICP starts after the previous same-device member's ICP.
+      // Integrates and raycasts still overlap the next member's work.
+      c->group_chain = true;
+      if (k > 0 && cs[k - 1]->device == c->device) HIPCHK(hipStreamWaitEvent(c->stream, cs[k - 1]->ev_icp, 0));
       tev[k] = timing_sample(c);
       enqueue_local(c, {c->raw[0], nullptr, c->bgr}, tev[k]);
       if (tev[k]) {  // timed: this member runs alone, as on a GPU of its own

@@ -1,0 +1,81 @@
+// Exact fast-forward of a repeated float addition (integrate's vc replay).
+//
+// The reference accumulates a column's camera-space position by n float adds,
+// x <- RN(x + s) (tsdf_volume.cu:53-55); a z-chunk or a Z-slab that starts at
+// slice n must reproduce that value bit for bit.  Inside one binade of |x|,
+// [2^E, 2^(E+1)), every float is an integer multiple X of u = 2^(E-23), so
+// while the exact sum x + s stays in the binade, RN(x + s) = (X + R) u with
+// R = the integer nearest to s / u: the sequence is an arithmetic progression
+// in integers, and m steps of it are (X + m R) u.  Steps that leave the
+// binade, ties (s / u a half-integer: the rounding then depends on X's last
+// bit), values near zero and extreme or non-finite values take plain float
+// adds.  Integer and float arithmetic only (a handful of registers: the loop
+// runs in integrate's prologue).  Checked against the plain loop on millions
+// of cases (tests/test_ffadd.py) and bit for bit inside the GPU parity tests.
+// Host and device share this code.
+#pragma once
+#include <cstdint>
+#include <cstring>
+
+#if defined(__HIPCC__)
+#define KFX_HD __host__ __device__
+#else
+#define KFX_HD
+#endif
+
+namespace kfx {
+
+KFX_HD inline uint32_t ff_f_bits(float f) {
+  uint32_t b;
+  std::memcpy(&b, &f, 4);
+  return b;
+}
+KFX_HD inline float ff_pow2f(int e) {  // 2^e as a float, -126 <= e <= 127
+  const uint32_t b = (uint32_t)(e + 127) << 23;
+  float f;
+  std::memcpy(&f, &b, 4);
+  return f;
+}
+
+// n repeated x <- RN(x + s) (binary32, round to nearest even), exactly.
+KFX_HD inline float ff_add(float x, float s, int n) {
+  const float as = s < 0.f ? -s : s;
+  while (n > 0) {
+    const float ax = x < 0.f ? -x : x;
+    // plain step: |x| within four steps of zero (tiny binades: one add each
+    // is cheaper), extreme or non-finite values, s == 0
+    if (!(ax >= 4.f * as) || !(ax >= 0x1p-90f) || !(ax < 0x1p90f) || !(as >= 0x1p-90f)) {
+      x = x + s;
+      --n;
+      continue;
+    }
+    const uint32_t bx = ff_f_bits(ax);
+    const int E = (int)((bx >> 23) & 0xffu) - 127;              // |x| in [2^E, 2^(E+1))
+    const int X = (int)((bx & 0x7fffffu) | 0x800000u);          // |x| / u in [2^23, 2^24)
+    const float su = (x < 0.f ? -s : s) * ff_pow2f(23 - E);     // s / u toward |x|: exact, |su| <= 2^22
+    const float rf = __builtin_rintf(su);
+    const float f = su - rf;                                    // exact
+    const int R = (int)rf;
+    // the sum X + R + f must stay in [2^23, 2^24): X + R in [lb, ub]
+    const int lb = 0x800000 + (f < 0.f ? 1 : 0), ub = 0x1000000 - (f < 0.f ? 0 : 1);
+    if (f == 0.5f || f == -0.5f || X + R < lb || X + R > ub) {  // tie, or the step leaves the binade
+      x = x + s;
+      --n;
+      continue;
+    }
+    if (R == 0) return x;  // |s| < u/2: x is a fixed point while in the binade
+    // the most steps with X + m R in [lb, ub]: D / |R| (D < 2^24, exact in
+    // float) from a reciprocal estimate, then corrected
+    const int D = R > 0 ? ub - X : X - lb, aR = R > 0 ? R : -R;
+    int m = (int)((float)D * (1.f / (float)aR));
+    while (m > 0 && m * aR > D) --m;
+    while ((m + 1) * aR <= D) ++m;
+    if (m > n) m = n;
+    const float xn = (float)(X + m * R) * ff_pow2f(E - 23);  // exact
+    x = x < 0.f ? -xn : xn;
+    n -= m;
+  }
+  return x;
+}
+
+}  // namespace kfx

@@ -13,6 +13,7 @@
 #include <type_traits>
 
 #include "kfx_internal.h"
+#include "kfx_ffadd.h"
 
 #ifndef KFX_INT_ICHECK
 #define KFX_INT_ICHECK 1  // integrate fast path: integer image-range tests
@@ -55,6 +56,15 @@
 #endif
 #ifndef KFX_INT_MAXCHUNK
 #define KFX_INT_MAXCHUNK 8  // integrate: most z-chunks per column tile
+#endif
+#ifndef KFX_FFADD
+#define KFX_FFADD 1  // integrate's vc replay by the exact fast-forward (kfx_ffadd.h)
+#endif
+#ifndef KFX_FF_MIN
+#define KFX_FF_MIN 768  // fast-forward replays of at least this many adds (shorter ones: the adds; A/B r3m: 384 costs C2 +8 %)
+#endif
+#ifndef KFX_INT_LPT
+#define KFX_INT_LPT 0  // integrate: longest-first dispatch order in every chunk mode (A/B)
 #endif
 #ifndef KFX_INT_PLAN
 #define KFX_INT_PLAN 0  // integrate: chunk start values from one sweep per tile (k_int_plan) instead of per-chunk replays (measured: the plan kernel costs what the replays cost)
@@ -1286,8 +1296,18 @@ __device__ __forceinline__ f3 replay_add(f3 a, f3 b) {
   return add(a, b);
 #endif
 }
-// a advanced from slice z to slice za (za - z adds when za > z), 8 per trip
+// a advanced from slice z to slice za (za - z adds when za > z): the exact
+// fast-forward of kfx_ffadd.h for long replays, the adds themselves (8 per
+// trip) for short ones
 __device__ __forceinline__ f3 replay(f3 a, f3 b, int z, int za) {
+#if KFX_FFADD
+  if (za - z >= KFX_FF_MIN) {
+    a.x = ff_add(a.x, b.x, za - z);
+    a.y = ff_add(a.y, b.y, za - z);
+    a.z = ff_add(a.z, b.z, za - z);
+    return a;
+  }
+#endif
   for (; z + 8 <= za; z += 8) {
 #pragma unroll
     for (int u = 0; u < 8; ++u) a = replay_add(a, b);
@@ -3182,19 +3202,31 @@ bool integrate_planned(const VolView &v) { return KFX_INT_PLAN && integrate_chun
 // permutation integrates the same volume.
 constexpr int kOrderBuckets = 1024;
 __global__ __launch_bounds__(1024) void k_int_order(const unsigned *__restrict__ work, unsigned *__restrict__ perm,
-                                                    int tiles, int nchunk, int zn) {
+                                                    int tiles, int nchunk, int zn, int capped, int chunkr) {
   __shared__ unsigned hist[kOrderBuckets];
   __shared__ unsigned wsum[16];
   const int t = threadIdx.x;
   hist[t] = 0u;
   __syncthreads();
   const int n = tiles * nchunk;
-  const float scale = (float)(kOrderBuckets - 2) / ((float)zn / (float)nchunk + 2.f);
+  const float scale = (float)(kOrderBuckets - 2) / ((float)zn + 2.f);
   auto bucket = [&](int item) {
     const unsigned len = work[item % tiles];
-    const int ct = min(nchunk, max(1, (int)(((long long)len * nchunk + zn - 1) / zn)));
-    if (len == 0u || item / tiles >= ct) return kOrderBuckets - 1;
-    return kOrderBuckets - 2 - min(kOrderBuckets - 2, (int)((float)len / (float)ct * scale));
+    const int c = item / tiles;
+    if (len == 0u) return kOrderBuckets - 1;
+    int clen;
+    if (capped) {
+      const int ct = min(nchunk, max(1, (int)(((long long)len * nchunk + zn - 1) / zn)));
+      if (c >= ct) return kOrderBuckets - 1;
+      clen = (int)len / ct;
+    } else {  // the chunk's length under the split k_integrate uses (geometric / equal)
+      VolView q{};
+      q.iadapt = 0;
+      int za, zb;
+      int_chunk(q, chunkr, c, nchunk, 0, (int)len - 1, za, zb);
+      clen = zb - za + 1;
+    }
+    return kOrderBuckets - 2 - min(kOrderBuckets - 2, (int)((float)max(clen, 0) * scale));
   };
   for (int i = t; i < n; i += 1024) atomicAdd(&hist[bucket(i)], 1u);
   __syncthreads();
@@ -3222,8 +3254,14 @@ void launch_integrate(hipStream_t s, VolView v, LevelGeom g0, const float2 *dl0,
   const int nchunk = integrate_chunks(v);
   v.inchunk = nchunk;
   v.iadapt = integrate_mode(v);
+#if !KFX_INT_LPT
   if (!v.iadapt) v.iperm = nullptr, v.iwork = nullptr;  // geometric chunks in block order
+#endif
   if (counters) v.iwork = nullptr;  // the count-only pass leaves the order alone
+#if KFX_INT_LPT
+  // every mode dispatches its items longest first (by the last frame's intervals)
+  if (counters) v.iperm = nullptr;  // the count-only pass keeps block order
+#endif
   const bool planned = integrate_planned(v) && v.prange && v.pckpt;
   if (planned) {
     hipLaunchKernelGGL(k_int_plan, dim3(tiles), dim3(64), 0, s, v, g0, dl0, st, log, vpose, xpose,
@@ -3266,7 +3304,8 @@ void launch_integrate(hipStream_t s, VolView v, LevelGeom g0, const float2 *dl0,
   }
 #undef KFX_LAUNCH_INT
   if (!counters && v.iwork && v.iperm)
-    hipLaunchKernelGGL(k_int_order, dim3(1), dim3(1024), 0, s, v.iwork, v.iperm, tiles, nchunk, v.zn);
+    hipLaunchKernelGGL(k_int_order, dim3(1), dim3(1024), 0, s, v.iwork, v.iperm, tiles, nchunk, v.zn, v.iadapt,
+                       planned ? KFX_INT_PCHUNKR : KFX_INT_CHUNKR);
 }
 
 #ifdef KFX_RAY_TRACE
@@ -3434,45 +3473,72 @@ void launch_scan(hipStream_t s, const unsigned *counts, unsigned long long *offs
   hipLaunchKernelGGL(k_scan_add, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, offsets, bsum, n);
 }
 
-// Per-slice integrate work of one frame (Z-slab balancing):
-// for every global slice z, the voxels whose depth test passes (sdf >=
-// -trunc, tsdf_volume.cu:56-71) at pose P, counted from the level-0 {depth,
-// 1/lambda} table.  An estimate for choosing slab cuts — vc is computed
-// directly, not accumulated — so it is not bit-exact with integrate.
-// One thread per (x, y) column; per-block LDS histogram, flushed once.
-__global__ __launch_bounds__(256) void k_slice_work(int X, int Y, int Z, float vs, float trunc, DevPose P,
-                                                    LevelGeom g, const float2 *__restrict__ dl,
-                                                    unsigned long long *hist) {
-  extern __shared__ unsigned lh[];
-  for (int i = threadIdx.x; i < Z; i += blockDim.x) lh[i] = 0u;
+// Per-slice integrate work of one frame (Z-slab balancing), in
+// two parts per global slice z:
+//   cover[z]   = 64 x the column tiles whose union interval (integrate's
+//                wave-uniform z range, int_column) contains z: the voxel slots
+//                integrate's waves step through, updated or not;
+//   updated[z] = the voxels of those intervals whose depth test passes
+//                (sdf >= -trunc, tsdf_volume.cu:56-71).
+// At pose P, from the level-0 {depth, 1/lambda} table.  An estimate for
+// choosing slab cuts (vc is computed directly, not accumulated), not bit-exact
+// with integrate.  One wave per 8x8 column tile; per-block LDS histograms
+// (cover as a difference array), flushed once.  hist: 2Z + 1 counters.
+__global__ __launch_bounds__(256) void k_slice_work(VolView v, LevelGeom g, const float2 *__restrict__ dl,
+                                                    DevPose P, unsigned long long *hist) {
+  extern __shared__ int lh[];  // [0, Z]: cover differences; [Z + 1, 2Z + 1): updated
+  const int Z = v.Z;
+  for (int i = threadIdx.x; i < 2 * Z + 1; i += blockDim.x) lh[i] = 0;
   __syncthreads();
-  const int col = blockIdx.x * blockDim.x + threadIdx.x;
-  if (col < X * Y) {
-    const int x = col % X, y = col / X;
-    const f3 vx = {(float)x * vs, (float)y * vs, 0.f};
-    const f3 c0 = add(rmul(P.R, vx), {P.t[0], P.t[1], P.t[2]});
-    const f3 zs = {P.R[2] * vs, P.R[5] * vs, P.R[8] * vs};
-    for (int z = 1; z < Z; ++z) {
-      const f3 vc = add(c0, scl(zs, (float)z));
-      if (!(vc.z > 0.f)) continue;
-      const float iz = 1.f / vc.z;
-      const int u = (int)rintf(vc.x * iz * g.fx + g.cx), w = (int)rintf(vc.y * iz * g.fy + g.cy);
-      if (u < 0 || u >= g.w || w < 0 || w >= g.h) continue;
-      const float2 d = dl[(size_t)w * g.w + u];
-      if (!(d.x > 0.f)) continue;
-      if (d.x - d.y * sqrtf(dot(vc, vc)) >= -trunc) atomicAdd(&lh[z], 1u);
+  const int lane = threadIdx.x & 63;
+  const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (tile < v.tiles_x * v.tiles_y) {  // wave-uniform
+    const int x = (tile % v.tiles_x) * 8 + (lane & 7), y = (tile / v.tiles_x) * 8 + (lane >> 3);
+    f3 c0, zs;
+    int zl, zh;
+    int_column(v, g, dl, P, x, y, c0, zs, zl, zh);
+    int wl = zl, wh = zh;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      wl = min(wl, __shfl_xor(wl, off));
+      wh = max(wh, __shfl_xor(wh, off));
+    }
+    if (wl <= wh) {
+      if (lane == 0) {
+        atomicAdd(&lh[wl], 64);
+        atomicSub(&lh[wh + 1], 64);
+      }
+      for (int z = wl; z <= wh; ++z) {
+        bool pass = false;
+        if (z >= zl && z <= zh) {
+          const f3 vc = add(c0, scl(zs, (float)z));
+          if (vc.z > 0.f) {
+            const float iz = 1.f / vc.z;
+            const int u = (int)rintf(vc.x * iz * g.fx + g.cx), w = (int)rintf(vc.y * iz * g.fy + g.cy);
+            if (u >= 0 && u < g.w && w >= 0 && w < g.h) {
+              const float2 d = dl[(size_t)w * g.w + u];
+              pass = d.x > 0.f && d.x - d.y * sqrtf(dot(vc, vc)) >= -v.trunc;
+            }
+          }
+        }
+        const int n = __popcll(__ballot(pass));
+        if (lane == 0 && n) atomicAdd(&lh[Z + 1 + z], n);
+      }
     }
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < Z; i += blockDim.x)
-    if (lh[i]) atomicAdd(&hist[i], (unsigned long long)lh[i]);
+  for (int i = threadIdx.x; i < 2 * Z + 1; i += blockDim.x)
+    if (lh[i]) atomicAdd(&hist[i], (unsigned long long)(long long)lh[i]);  // (two's complement sums)
 }
 
 void launch_slice_work(hipStream_t s, const VolView &v, DevPose vol2cam, LevelGeom g0, const float2 *dl0,
                        unsigned long long *hist) {
-  const int cols = v.X * v.Y;
-  hipLaunchKernelGGL(k_slice_work, dim3((cols + 255) / 256), dim3(256), (size_t)v.Z * 4, s, v.X, v.Y, v.Z, v.vs[0],
-                     v.trunc, vol2cam, g0, dl0, hist);
+  VolView gv = v;  // the whole volume's slices, whatever this context stores
+  gv.zb = 0;
+  gv.zn = v.Z;
+  const int tiles = v.tiles_x * v.tiles_y;
+  hipLaunchKernelGGL(k_slice_work, dim3((tiles + 3) / 4), dim3(256), (size_t)(2 * v.Z + 1) * 4, s, gv, g0, dl0,
+                     vol2cam, hist);
 }
 
 void launch_inv_lambda(hipStream_t s, LevelGeom g0, float *inv_lambda) {

@@ -322,12 +322,21 @@ def test_balanced_cuts_group_matches_single_volume(seq_qvga):
     single, st = _single(intr, p, bgr, dep)
     probe = KinectFusion(I, p, slab=(0, 4))  # any context: only its frame buffers are used
     work = probe.slice_work(bgr[0], dep[0].astype(np.float32))
+    cover, updated = probe.slice_work_parts(bgr[0], dep[0].astype(np.float32))
     probe.close()
     first = KinectFusion(I, p)
     first.pipeline(bgr[0], dep[0].astype(np.float32))
-    upd = first.integrate_stats()["updated"]
+    ws = first.integrate_stats()
     first.close()
-    assert work[0] == 0 and abs(int(work.sum()) - upd) <= 0.01 * upd, (int(work.sum()), upd)
+    # the parts: updated voxels as integrate counts them (the estimate's vc is
+    # direct, not accumulated: 1 %), wave slots as its batches of 4 slices
+    # (each of a tile's <= 8 z-chunks rounds up to a whole batch); the cost
+    # weighs both
+    upd, slots, tiles = ws["updated"], ws["wave_batches"] * 4 * 64, (64 // 8) ** 2
+    assert work[0] == 0 and cover[0] == 0 and np.all(cover >= updated)
+    assert abs(int(updated.sum()) - upd) <= 0.01 * upd, (int(updated.sum()), upd)
+    assert cover.sum() <= slots <= cover.sum() + 8 * tiles * 4 * 64, (int(cover.sum()), slots)
+    assert np.array_equal(work, cover + 2 * updated)
     world = 3
     cuts = slab_balance(work, world)
     assert cuts[0] == 0 and cuts[-1] == 64 and all(b - a >= 8 for a, b in zip(cuts, cuts[1:]))

@@ -1,0 +1,11 @@
+#!/bin/bash
+# slab tests, slab records with the cover/updated cost fit
+set -o pipefail
+cd ${GRAFT_REPO_ROOT:-.}
+mkdir -p gpurun_out
+timeout -k 10 600 python3 -u -m pytest tests/test_gpu_slab.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/tests_r3m.log 2>&1; rc=$?
+tail -3 gpurun_out/tests_r3m.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python3 tools/slab_record.py c4 --out gpurun_out/r03_c4_slabs.json || exit 1
+timeout -k 10 500 python3 tools/slab_record.py c5 --frames 10 --warmup 3 --out gpurun_out/r03_c5_slabs.json || exit 1
+bash tools/ab_quick.sh 2 base noff ff768 ff1 2>&1 | tee gpurun_out/ab_r3m.log || exit 1
+KFX_LIB_PATH=$PWD/slam-kinectfusion_amd/lib/var_noff/libkfx.so timeout -k 10 300 python3 tools/slab_record.py c4 --frames 10 --out gpurun_out/r03_c4_slabs_noff.json || exit 1

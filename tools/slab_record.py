@@ -101,19 +101,40 @@ def main():
     rec["ideal"] = 1.0 / a.world
     rec["single_icp_integrate_raycast_ms"] = float(sum(rec["single"][k] for k in ("icp_ms", "integrate_ms",
                                                                                     "raycast_ms")))
-    rec["equal_cuts"] = group(None)
-    # work-balanced cuts from the first frame's per-slice work (what bench.py uses at N > 1)
+    # per-slice work of the first frame (what bench.py balances on at N > 1)
     probe = kfx.KinectFusion(I, p, slab=(0, n // 16))
     work = probe.slice_work(bgr[order[0]], dep[order[0]])
+    cover, upd = probe.slice_work_parts(bgr[order[0]], dep[order[0]])
     probe.close()
     rec["slice_work_first_frame"] = [int(x) for x in work]
+    rec["slice_cover_first_frame"] = [int(x) for x in cover]
+    rec["slice_updated_first_frame"] = [int(x) for x in upd]
+    rec["equal_cuts"] = group(None)
     rec["balanced_cuts"] = group(kfx.slab_balance(work, a.world))
+    # integrate ms of a slab against its stored slices' estimated parts:
+    # ms ~ a * cover + b * updated + c (least squares over both cut sets)
+    rows, ys = [], []
+    for k in ("equal_cuts", "balanced_cuts"):
+        for sl in rec[k]["slabs"]:
+            z0, z1 = sl["stored_slices"]
+            sl["est_cover"] = int(cover[z0:z1].sum())
+            sl["est_updated"] = int(upd[z0:z1].sum())
+            rows.append([sl["est_cover"], sl["est_updated"], 1.0])
+            ys.append(sl["integrate_ms"])
+    A = np.array(rows, np.float64)
+    coef, *_ = np.linalg.lstsq(A / A.max(axis=0), np.array(ys), rcond=None)
+    coef = coef / A.max(axis=0)
+    pred = A @ coef
+    rec["cost_fit"] = {"ms_per_cover": float(coef[0]), "ms_per_updated": float(coef[1]), "ms_const": float(coef[2]),
+                       "updated_over_cover": float(coef[1] / coef[0]) if coef[0] else None,
+                       "max_rel_err": float(np.max(np.abs(pred - ys) / np.array(ys)))}
     out = a.out or os.path.join(ROOT, "gpurun_out", f"slabs_{a.config}.json")
     os.makedirs(os.path.dirname(out), exist_ok=True)
     json.dump(rec, open(out, "w"), indent=1)
     print(json.dumps({"config": rec["config"], "ideal": rec["ideal"],
                       **{f"{k}:{q}": rec[k][q] for k in ("equal_cuts", "balanced_cuts")
-                         for q in ("integrate_imbalance_max_over_mean", "max_slab_over_single_integrate")}}))
+                         for q in ("integrate_imbalance_max_over_mean", "max_slab_over_single_integrate")},
+                      "cost_fit": rec["cost_fit"]}))
 
 
 if __name__ == "__main__":
