@@ -75,6 +75,9 @@
 #ifndef KFX_INT_PCHUNKR
 #define KFX_INT_PCHUNKR 100  // planned integrate: chunk weights (100: equal chunks)
 #endif
+#ifndef KFX_INT_DEDUP
+#define KFX_INT_DEDUP 0  // integrate: a voxel projecting to the previous voxel's pixel reuses its gather (A/B)
+#endif
 #ifndef KFX_INT_WAVES
 #define KFX_INT_WAVES 12288  // integrate: target wave count (z-chunks per column tile; C2: 3 chunks of 4096 tiles)
 #endif
@@ -1638,6 +1641,21 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
       }
     }
     float2 d[kB];
+#if KFX_INT_DEDUP
+    // consecutive voxels of a column often project to the same pixel: such a
+    // voxel reuses the previous one's {depth, 1/lambda} instead of gathering
+    // it (its lane issues no cache request: kOob), cutting L1/L2 gather lines
+    unsigned gpix[kB];
+    gpix[0] = pix[0];
+#pragma unroll
+    for (int j = 1; j < kB; ++j) gpix[j] = pix[j] == pix[j - 1] ? kOob : pix[j];
+#pragma unroll
+    for (int j = 0; j < kB; ++j)
+      d[j] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rdl, gpix[j], 0, 0));
+#pragma unroll
+    for (int j = 1; j < kB; ++j)
+      if (pix[j] == pix[j - 1]) d[j] = d[j - 1];
+#else
 #pragma unroll
     for (int j = 0; j < kB; ++j)
 #if KFX_INT_EXP == 4  // timing experiment only (wrong values): no depth gathers
@@ -1646,6 +1664,7 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
       d[j] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rdl, pix[j] == kOob ? kOob : 8u * (unsigned)lane + 4096u * (unsigned)j, 0, 0));
 #else
       d[j] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rdl, pix[j], 0, 0));
+#endif
 #endif
     // sdf and the depth test (tsdf_volume.cu:67-71)
     if (fast) {
