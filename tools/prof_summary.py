@@ -25,7 +25,7 @@ def main():
         d = np.array(d)
         e = {"dispatches": len(d), "mean_us_all": round(float(d.mean()), 2),
              "median_us_all": round(float(np.median(d)), 2)}
-        if name in ("k_icp_track", "k_integrate<false, true>", "k_raycast<true, false, false>") and len(d) >= warmup + steps:
+        if (name in ("k_icp_track", "k_raycast<true, false, false>") or name.startswith("k_integrate<false, true")) and len(d) >= warmup + steps:
             t = d[warmup:warmup + steps]
             e["mean_us_timed_region"] = round(float(t.mean()), 2)
         out[name] = e

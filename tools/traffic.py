@@ -101,9 +101,10 @@ def main():
                    # record only to a run that loaded the same file
                    "lib": os.path.relpath(lib, REPO), "lib_sha256": sha256(lib),
                    "commit": os.environ.get("KFX_COMMIT")}
-            for k, name in (("k_integrate<false, true>", "integrate_sq"), ("k_raycast<true, false, false>", "raycast_sq")):
-                if k in sq:
-                    rec[name] = sq_issue(sq[k])
+            for pre, name in (("k_integrate<false, true", "integrate_sq"), ("k_raycast<true, false, false>", "raycast_sq")):
+                ks = [k for k in sq if k.startswith(pre)]
+                if ks:
+                    rec[name] = sq_issue(sq[ks[0]])
             name = os.environ.get("PMC_RECORD", "r03_integrate_pmc.json")
             json.dump(rec, open(os.path.join(REPO, "profiles", name), "w"), indent=1)
             # a copy beside the counters (profiles/ does not come back from the GPU box)
