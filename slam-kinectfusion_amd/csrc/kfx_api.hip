@@ -162,12 +162,18 @@ struct kfx_ctx {
   // the copy stream while earlier frames run (slot reuse ordered by events)
   static constexpr int kRing = 4;
   uint8_t *ring_host = nullptr, *ring_dev = nullptr;
+  uint8_t *ring_host_dev = nullptr;  // ring_host as mapped into the device address space
   size_t ring_slot = 0;  // bytes per slot: f32 depth + BGR8
   hipEvent_t ring_h2d[kRing]{}, ring_done[kRing]{};
   bool ring_used[kRing]{};
   int ring_next = 0;
   bool ring_ready = false;  // every ring resource above created
-  std::vector<std::pair<uintptr_t, size_t>> host_regs;  // kfx_register_host_buffer ranges
+  struct HostReg {
+    uintptr_t host;
+    size_t bytes;
+    uint8_t *dev;  // the same pages mapped into the device address space
+  };
+  std::vector<HostReg> host_regs;  // kfx_register_host_buffer ranges
   hipStream_t cstream = nullptr;
   ncclComm_t comm = nullptr;      // RCCL communicator over the slab ranks (one process per GPU)
   hipEvent_t xev[5]{};            // extraction pass events (kfx_get_extract_ms)
@@ -858,8 +864,11 @@ static int create_impl(const kfx_intrinsics *intr, const kfx_params *params, int
   if ((r = dalloc(c, (void **)&c->raw0_u16, np0 * 2))) return fail(r);
   if ((r = dalloc(c, (void **)&c->bgr, np0 * 3))) return fail(r);
   if ((r = dalloc(c, (void **)&c->inv_lambda, np0 * 4))) return fail(r);
+  // {depth, 1/lambda} per pixel + 16 max-depth shards + the min-depth pyramid
+  // (levels 1..4, < np0 / 3 + W + H + 4 floats; kfx_kernels.hip dmin_level)
+  const size_t pyr = np0 / 3 + (size_t)intr->width + (size_t)intr->height + 64;
   for (float2 *&d : c->dl0b)
-    if ((r = dalloc(c, (void **)&d, np0 * 8 + 64))) return fail(r);
+    if ((r = dalloc(c, (void **)&d, np0 * 8 + 64 + pyr * 4))) return fail(r);
   c->vol = make_vol(p, rank, world, cuts);
   const size_t n = nvox(c);
   {
@@ -914,7 +923,7 @@ int kfx_destroy(kfx_ctx *c) {
   if (c->cstream) (void)hipStreamSynchronize(c->cstream);
   destroy_graphs(c);
   if (c->ring_host) (void)hipHostFree(c->ring_host);
-  for (const auto &r : c->host_regs) (void)hipHostUnregister(reinterpret_cast<void *>(r.first));
+  for (const auto &r : c->host_regs) (void)hipHostUnregister(reinterpret_cast<void *>(r.host));
   for (int k = 0; k < kfx_ctx::kRing; ++k)
     for (hipEvent_t e : {c->ring_h2d[k], c->ring_done[k]})
       if (e) (void)hipEventDestroy(e);
@@ -931,6 +940,9 @@ int kfx_destroy(kfx_ctx *c) {
   if (c->pstream) (void)hipStreamDestroy(c->pstream);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
+  // the teardown's errors (e.g. a buffer another context unregistered first)
+  // must not surface in a later call's hipGetLastError check
+  (void)hipGetLastError();
   return KFX_OK;
 }
 
@@ -965,20 +977,27 @@ int kfx_pipeline_u16(kfx_ctx *c, const uint8_t *bgr, const uint16_t *depth_mm) {
   return finish_frame(c);
 }
 
-// [p, p + n) inside one buffer registered with kfx_register_host_buffer
-static bool host_registered(const kfx_ctx *c, const void *p, size_t n) {
+// The device address of [p, p + n) when it lies inside one buffer registered
+// with kfx_register_host_buffer, else null
+static const uint8_t *host_mapped(const kfx_ctx *c, const void *p, size_t n) {
   const uintptr_t a = reinterpret_cast<uintptr_t>(p);
   for (const auto &r : c->host_regs)
-    if (a >= r.first && a + n <= r.first + r.second) return true;
-  return false;
+    if (a >= r.host && a + n <= r.host + r.bytes) return r.dev + (a - r.host);
+  return nullptr;
 }
 
 int kfx_register_host_buffer(kfx_ctx *c, void *ptr, size_t bytes) {
   int r = check_ctx(c);
   if (r) return r;
   if (!ptr || !bytes) return set_err(KFX_ERR_ARG, "null or empty buffer");
-  HIPCHK(hipHostRegister(ptr, bytes, hipHostRegisterDefault));
-  c->host_regs.emplace_back(reinterpret_cast<uintptr_t>(ptr), bytes);
+  HIPCHK(hipHostRegister(ptr, bytes, hipHostRegisterMapped));
+  void *dev = nullptr;
+  const hipError_t e = hipHostGetDevicePointer(&dev, ptr, 0);
+  if (e != hipSuccess || !dev) {
+    (void)hipHostUnregister(ptr);
+    return set_err(KFX_ERR_HIP, std::string("hipHostGetDevicePointer: ") + hipGetErrorString(e));
+  }
+  c->host_regs.push_back({reinterpret_cast<uintptr_t>(ptr), bytes, static_cast<uint8_t *>(dev)});
   return KFX_OK;
 }
 
@@ -987,7 +1006,7 @@ int kfx_unregister_host_buffer(kfx_ctx *c, void *ptr) {
   if (r) return r;
   const uintptr_t a = reinterpret_cast<uintptr_t>(ptr);
   for (size_t i = 0; i < c->host_regs.size(); ++i)
-    if (c->host_regs[i].first == a) {
+    if (c->host_regs[i].host == a) {
       // uploads from it may still be queued
       if (c->cstream) HIPCHK(hipStreamSynchronize(c->cstream));
       HIPCHK(hipHostUnregister(ptr));
@@ -1007,7 +1026,8 @@ static int pipeline_async(kfx_ctx *c, const uint8_t *bgr, const void *depth, boo
     // the next call creates only what is still missing)
     c->ring_slot = (np * 4 + np * 3 + 255) & ~(size_t)255;
     if (!c->ring_host)
-      HIPCHK(hipHostMalloc((void **)&c->ring_host, c->ring_slot * kfx_ctx::kRing, hipHostMallocDefault));
+      HIPCHK(hipHostMalloc((void **)&c->ring_host, c->ring_slot * kfx_ctx::kRing, hipHostMallocMapped));
+    if (!c->ring_host_dev) HIPCHK(hipHostGetDevicePointer((void **)&c->ring_host_dev, c->ring_host, 0));
     if (!c->ring_dev && (r = dalloc(c, (void **)&c->ring_dev, c->ring_slot * kfx_ctx::kRing))) return r;
     if (!c->cstream) HIPCHK(hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
     for (int k = 0; k < kfx_ctx::kRing; ++k) {
@@ -1021,20 +1041,24 @@ static int pipeline_async(kfx_ctx *c, const uint8_t *bgr, const void *depth, boo
   uint8_t *hs = c->ring_host + c->ring_slot * k, *ds = c->ring_dev + c->ring_slot * k;
   const size_t dbytes = np * (u16 ? 2 : 4);
   // zero copy: frames in buffers registered with kfx_register_host_buffer are
-  // uploaded straight from the caller's pinned pages (no host copy, no host
-  // wait); others are copied into the pinned ring slot first
-  const bool direct = host_registered(c, depth, dbytes) && host_registered(c, bgr, np * 3);
+  // read by the GPU straight from the caller's pinned pages (no host copy, no
+  // host wait); others are copied into the pinned ring slot first.  Either way
+  // the upload is a kernel on the copy stream reading mapped host memory
+  // (k_host_fetch), not hipMemcpyAsync, whose host-side cost per call was the
+  // bottleneck of this path
+  const uint8_t *map_d = host_mapped(c, depth, dbytes), *map_c = host_mapped(c, bgr, np * 3);
+  const bool direct = map_d && map_c;
   if (!direct) {
     if (c->ring_used[k]) HIPCHK(hipEventSynchronize(c->ring_h2d[k]));  // the slot's last upload is done
     std::memcpy(hs, depth, dbytes);
     std::memcpy(hs + np * 4, bgr, np * 3);
+    map_d = c->ring_host_dev + c->ring_slot * k;
+    map_c = map_d + np * 4;
   }
-  const uint8_t *src_d = direct ? static_cast<const uint8_t *>(depth) : hs;
-  const uint8_t *src_c = direct ? bgr : hs + np * 4;
   // the device slot is free once the frame that read it has finished
   if (c->ring_used[k]) HIPCHK(hipStreamWaitEvent(c->cstream, c->ring_done[k], 0));
-  HIPCHK(hipMemcpyAsync(ds, src_d, dbytes, hipMemcpyHostToDevice, c->cstream));
-  HIPCHK(hipMemcpyAsync(ds + np * 4, src_c, np * 3, hipMemcpyHostToDevice, c->cstream));
+  launch_host_fetch(c->cstream, map_d, ds, dbytes, map_c, ds + np * 4, np * 3);
+  HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(c->ring_h2d[k], c->cstream));
   c->ring_used[k] = true;
   FrameInput in{u16 ? c->raw[0] : (const float *)ds, u16 ? (const uint16_t *)ds : nullptr, ds + np * 4};
@@ -1545,8 +1569,9 @@ int kfx_stage_icp(kfx_ctx *c, kfx_pose *out) {
   return failed ? KFX_TRACKING_LOST : KFX_OK;
 }
 
-// out: {updated, coloured, visited, gathered, wave batches, 0, 0, 0} of the
-// last frame's integrate
+// out: {updated, coloured, visited, gathered, wave batches, updated in
+// certified free-space groups, certified wave batches, 0} of the last frame's
+// integrate
 static int integrate_stats_impl(kfx_ctx *c, int64_t out[8], const float *xpose) {
   HIPCHK(hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * 128, c->stream));
   launch_integrate(c->stream, c->vol, c->g[0], c->dl0, c->last_bgr ? c->last_bgr : c->bgr, c->st,

@@ -258,6 +258,9 @@ constexpr int kMaxGroup = 16;
 void launch_group_reduce(hipStream_t s, uint32_t *const *in, int n_in, uint32_t *const *out,
                          int n_out, size_t count, bool is_max);
 void launch_inv_lambda(hipStream_t s, LevelGeom g0, float *inv_lambda);
+// device reads of mapped page-locked host memory into device buffers (two segments)
+void launch_host_fetch(hipStream_t s, const void *src0, void *dst0, size_t n0, const void *src1, void *dst1,
+                       size_t n1);
 // point extraction (FullScan6) over global slices [zlo, zhi): offsets == null
 // counts points per wave, else writes them (float3) at offsets (< cap)
 size_t extract_waves(const VolView &v, int zlo, int zhi);

@@ -75,6 +75,9 @@
 #ifndef KFX_INT_PCHUNKR
 #define KFX_INT_PCHUNKR 100  // planned integrate: chunk weights (100: equal chunks)
 #endif
+#ifndef KFX_INT_CERT
+#define KFX_INT_CERT 0  // integrate: certified free-space groups skip projection, gather and sdf (measured slower)
+#endif
 #ifndef KFX_INT_DEDUP
 #define KFX_INT_DEDUP 0  // integrate: a voxel projecting to the previous voxel's pixel reuses its gather (A/B)
 #endif
@@ -236,6 +239,19 @@ __device__ __forceinline__ void frame_begin(DevState *st) {
 // the frame's max-depth shards live after the level-0 dl table (one per cur buffer)
 __device__ __forceinline__ unsigned *dmax_shards(const float2 *dl0, const LevelGeom &g0) {
   return (unsigned *)(const_cast<float2 *>(dl0) + (size_t)g0.w * g0.h);
+}
+
+// Min-depth pyramid of the level-0 filtered depth, after the max-depth shards:
+// level k = 1..kPyrLevels holds the minimum over each 2^k x 2^k pixel cell
+// (cells clipped at the image edge; 0 where any pixel of the cell has no depth),
+// ceil(W / 2^k) x ceil(H / 2^k) floats, levels back to back.  Written by
+// k_preprocess_maps (level 0 blocks are 16x16 tiles = one level-4 cell);
+// read by integrate's free-space certification.
+[[maybe_unused]] constexpr int kPyrLevels = 4;
+__device__ __forceinline__ const float *dmin_level(const float2 *dl0, const LevelGeom &g0, int k) {
+  const float *p = reinterpret_cast<const float *>(dl0 + (size_t)g0.w * g0.h) + kDmaxShards;
+  for (int i = 1; i < k; ++i) p += (size_t)((g0.w + (1 << i) - 1) >> i) * ((g0.h + (1 << i) - 1) >> i);
+  return p;
 }
 
 // z is the global slice; the view stores slices [zb, zb+zn) (tile-column
@@ -517,6 +533,38 @@ __global__ __launch_bounds__(256) void k_preprocess_maps(BilatArgs a) {
     }
     st3(a.n[l], o, n);
   }
+#if KFX_INT_CERT
+  if (l == 0) {  // block-uniform: the min-depth pyramid (dmin_level) of this 16x16 tile
+    // lanes: threadIdx = cy * 16 + cx, a wave = 4 rows; levels 1 and 2 within
+    // the wave (partners differ in lane bits 0/4, 1/5), levels 3 and 4 in LDS
+    float mn = in ? dval : __builtin_huge_valf();  // outside the image: neutral
+    mn = fminf(mn, __shfl_xor(mn, 1));
+    mn = fminf(mn, __shfl_xor(mn, 16));
+    float *p1 = const_cast<float *>(dmin_level(a.dl0, g, 1));
+    const int w1 = (g.w + 1) >> 1;
+    if (in && !(cx & 1) && !(cy & 1)) p1[(size_t)(y >> 1) * w1 + (x >> 1)] = mn;
+    mn = fminf(mn, __shfl_xor(mn, 2));
+    mn = fminf(mn, __shfl_xor(mn, 32));
+    float *p2 = const_cast<float *>(dmin_level(a.dl0, g, 2));
+    const int w2 = (g.w + 3) >> 2;
+    if (in && !(cx & 3) && !(cy & 3)) p2[(size_t)(y >> 2) * w2 + (x >> 2)] = mn;
+    __shared__ float q4[16];  // the 4x4 level-2 cells of the tile
+    if (!(cx & 3) && !(cy & 3)) q4[(cy >> 2) * 4 + (cx >> 2)] = mn;
+    __syncthreads();
+    if (threadIdx.x < 4) {  // level 3: 2x2 cells of 8x8 pixels
+      const int qx = (threadIdx.x & 1) * 2, qy = (threadIdx.x >> 1) * 2;
+      const float m3 = fminf(fminf(q4[qy * 4 + qx], q4[qy * 4 + qx + 1]), fminf(q4[(qy + 1) * 4 + qx], q4[(qy + 1) * 4 + qx + 1]));
+      const int x3 = (X0 >> 3) + (threadIdx.x & 1), y3 = (Y0 >> 3) + (threadIdx.x >> 1);
+      const int w3 = (g.w + 7) >> 3, h3 = (g.h + 7) >> 3;
+      if (x3 < w3 && y3 < h3) const_cast<float *>(dmin_level(a.dl0, g, 3))[(size_t)y3 * w3 + x3] = m3;
+    }
+    if (threadIdx.x == 0) {  // level 4: the tile
+      float m4 = q4[0];
+      for (int i = 1; i < 16; ++i) m4 = fminf(m4, q4[i]);
+      const_cast<float *>(dmin_level(a.dl0, g, 4))[(size_t)(Y0 >> 4) * ((g.w + 15) >> 4) + (X0 >> 4)] = m4;
+    }
+  }
+#endif
   if (l == 0) {  // block-uniform
     unsigned m = (in && dval > 0.f) ? __float_as_uint(dval) : 0u;
     for (int off = 32; off > 0; off >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, off));
@@ -1465,6 +1513,48 @@ __global__ __launch_bounds__(64) void k_int_plan(VolView v, LevelGeom g, const f
   }
 }
 
+#ifndef KFX_CERT_G
+#define KFX_CERT_G 16  // integrate: slices per certification group (a multiple of KFX_INT_KB)
+#endif
+// Does the group of KFX_CERT_G voxels after vc (the next one is vc + zs) lie in
+// certified free space?  Every voxel of the group projects (rounded, as the
+// exact path computes it) into the pixel box [ilo, ihi] x [jlo, jhi]: along a
+// column u = (a + z b) / (c + z d) fx + cx is monotonic while vc.z > 0, so the
+// box of the two end voxels (approximate quotients, 0.01 px of margin: the
+// rcp / fma errors and the accumulated adds' deviation from the linear model
+// over KFX_CERT_G adds stay below 1e-3 px) holds every rounded projection.
+// If that box is inside the image, the minimum depth over a min-depth pyramid
+// cell cover of it (dmin_level) is the least depth any voxel reads; with vc.z
+// at most zhi (monotonic too), sdf = d - RN(il * |vc|) >= dmin - zhi * bfac >=
+// trunc, evaluated with 1e-5 m of margin for the float evaluation here.
+#if KFX_INT_CERT
+__device__ __forceinline__ bool cert_free(f3 vc, f3 zs, const LevelGeom &g, const float2 *dl, float bfac,
+                                          float need) {
+  const f3 pa = add(vc, zs);
+  const float G = (float)KFX_CERT_G;
+  const f3 pb = {fmaf(G, zs.x, vc.x), fmaf(G, zs.y, vc.y), fmaf(G, zs.z, vc.z)};
+  const float zlo = fminf(pa.z, pb.z), zhi = fmaxf(pa.z, pb.z);
+  if (!(zlo > 1e-3f)) return false;  // (NaN-safe)
+  const float ra = __builtin_amdgcn_rcpf(pa.z), rb = __builtin_amdgcn_rcpf(pb.z);
+  const float ua = fmaf(pa.x * ra, g.fx, g.cx), ub = fmaf(pb.x * rb, g.fx, g.cx);
+  const float va = fmaf(pa.y * ra, g.fy, g.cy), vb = fmaf(pb.y * rb, g.fy, g.cy);
+  const float ulo = fminf(ua, ub) - 0.51f, uhi = fmaxf(ua, ub) + 0.51f;
+  const float vlo = fminf(va, vb) - 0.51f, vhi = fmaxf(va, vb) + 0.51f;
+  if (!(ulo > -1.f && vlo > -1.f && uhi < (float)g.w && vhi < (float)g.h)) return false;
+  const int ilo = (int)ceilf(ulo), ihi = (int)floorf(uhi), jlo = (int)ceilf(vlo), jhi = (int)floorf(vhi);
+  if (ilo < 0 || jlo < 0 || ihi > g.w - 1 || jhi > g.h - 1) return false;
+  const int span = max(ihi - ilo, jhi - jlo) + 1;
+  const int k = span <= 2 ? 1 : (span <= 4 ? 2 : (span <= 8 ? 3 : (span <= 16 ? 4 : 0)));
+  static_assert(kPyrLevels == 4, "the level choice above covers spans up to 16 px");
+  if (!k) return false;
+  const float *lv = dmin_level(dl, g, k);
+  const int wk = (g.w + (1 << k) - 1) >> k;
+  const int x0 = ilo >> k, x1 = ihi >> k, y0 = jlo >> k, y1 = jhi >> k;
+  const float dmin = fminf(fminf(lv[y0 * wk + x0], lv[y0 * wk + x1]), fminf(lv[y1 * wk + x0], lv[y1 * wk + x1]));
+  return dmin - zhi * bfac >= need;
+}
+#endif
+
 // Work split: a wave owns an 8x8 tile of columns and one of gridDim.y z-chunks
 // of every column's in-range interval (more waves per SIMD to hide latency);
 // each lane replays the vc adds up to its chunk start, so every voxel's vc is
@@ -1575,7 +1665,7 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
   const float trunc = v.trunc;
   const float thres_color = trunc / 2;
   // kCount: updated, coloured, visited, gathered voxels; wave batches
-  unsigned cu = 0, cc = 0, cv = 0, cg = 0, cb = 0;
+  unsigned cu = 0, cc = 0, cv = 0, cg = 0, cb = 0, cfu = 0, cfb = 0;  // + certified updates / batches
   // negative tsdf this lane wrote: bricks gbs .. gbs+61 as bits, beyond as a z range
   const int gbs = za >> 3;
   unsigned long long nbm = 0ull;
@@ -1593,18 +1683,60 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
   // (memory-level parallelism); each voxel's arithmetic is exactly the
   // reference's (tsdf_volume.cu:56-98).
   constexpr int kB = KFX_INT_KB;
+#if KFX_INT_DEDUP == 2
+  unsigned dd_pix = kOob;  // the previous batch's last voxel: pixel and gathered value
+  float2 dd_d = make_float2(0.f, 0.f);
+#endif
+#if KFX_INT_CERT
+  // Free-space certification: bfac bounds RN(1/lambda * |vc|) /
+  // vc.z for any voxel whose rounded projection lies in the image (the voxel's
+  // ray and its pixel's centre ray differ by <= 0.51 px: lambda_v^2 -
+  // lambda_p^2 <= ex (2 tx + ex) + ey (2 ty + ey), lambda_p >= 1), with 1e-5 of
+  // relative margin for the roundings of the table, sqrt_rn and the product
+  const float cex = 0.51f / g.fx, cey = 0.51f / g.fy;
+  const float ctx = (fmaxf(g.cx, fw - 1.f - g.cx) + 0.51f) / g.fx;
+  const float cty = (fmaxf(g.cy, fh - 1.f - g.cy) + 0.51f) / g.fy;
+  const float cbfac = sqrtf(1.f + cex * (2.f * ctx + cex) + cey * (2.f * cty + cey)) * 1.00001f;
+  const float cneed = trunc + 1e-5f;
+  int cert_left = 0;  // wave-uniform: batches left in the certified group
+#endif
   for (; z <= zb; z += kB) {
+    float sdf[kB];
+    unsigned pix[kB];
+    bool ok[kB];
+#if KFX_INT_CERT
+    if (cert_left == 0) {
+      // the next KFX_CERT_G slices of every lane that updates any of them are
+      // certified free space: in the image, in front of the camera, depth > 0
+      // and sdf >= trunc for every voxel (so ts = 1, no colour band)
+      const bool any = max(z, la) <= min(z + KFX_CERT_G - 1, lb);
+      if (__all(!any || cert_free(vc, zs, g, dl, cbfac, cneed))) cert_left = KFX_CERT_G / kB;
+    }
+    const bool fastg = cert_left > 0;
+    if (fastg) --cert_left;
+#else
+    constexpr bool fastg = false;
+#endif
     f3 p[kB];
-    float n2[kB];
 #pragma unroll
     for (int j = 0; j < kB; ++j) {
       vc = add(vc, zs);
       p[j] = vc;
-      n2[j] = dot(vc, vc);
     }
-    float sdf[kB];
-    unsigned pix[kB];
-    bool ok[kB];
+    if (fastg) {  // certified free space: no projection, gather or sdf
+#pragma unroll
+      for (int j = 0; j < kB; ++j) {
+        ok[j] = (z + j >= la) & (z + j <= lb);
+        sdf[j] = 2.f * trunc;  // any value >= trunc gives ts = 1 and no colour band
+        pix[j] = ok[j] ? 0u : kOob;
+      }
+#if KFX_INT_DEDUP == 2
+      dd_pix = kOob;
+#endif
+    } else {
+    float n2[kB];
+#pragma unroll
+    for (int j = 0; j < kB; ++j) n2[j] = dot(p[j], p[j]);
     // projection: ok = in the image in front of the camera (tsdf_volume.cu:56-66)
     if (fast) {  // the cheap exact sequences, two voxels per packed-FP32 op
       static_assert(kB % 2 == 0, "voxel pairs");
@@ -1646,15 +1778,26 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
     // voxel reuses the previous one's {depth, 1/lambda} instead of gathering
     // it (its lane issues no cache request: kOob), cutting L1/L2 gather lines
     unsigned gpix[kB];
+#if KFX_INT_DEDUP == 2  // also against the previous batch's last voxel
+    gpix[0] = pix[0] == dd_pix ? kOob : pix[0];
+#else
     gpix[0] = pix[0];
+#endif
 #pragma unroll
     for (int j = 1; j < kB; ++j) gpix[j] = pix[j] == pix[j - 1] ? kOob : pix[j];
 #pragma unroll
     for (int j = 0; j < kB; ++j)
       d[j] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rdl, gpix[j], 0, 0));
+#if KFX_INT_DEDUP == 2
+    if (pix[0] == dd_pix) d[0] = dd_d;
+#endif
 #pragma unroll
     for (int j = 1; j < kB; ++j)
       if (pix[j] == pix[j - 1]) d[j] = d[j - 1];
+#if KFX_INT_DEDUP == 2
+    dd_pix = pix[kB - 1];
+    dd_d = d[kB - 1];
+#endif
 #else
 #pragma unroll
     for (int j = 0; j < kB; ++j)
@@ -1680,9 +1823,15 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
     }
 #pragma unroll
     for (int j = 0; j < kB; ++j) ok[j] = ok[j] & (d[j].x > 0) & (sdf[j] >= -trunc);
+    }
     if (kCount) {
       iz += (Idx)kB * slice;
       ++cb;
+      if (fastg) {
+        ++cfb;
+#pragma unroll
+        for (int j = 0; j < kB; ++j) cfu += ok[j];
+      }
 #pragma unroll
       for (int j = 0; j < kB; ++j) {
         cv += (z + j >= la) & (z + j <= lb);
@@ -1784,8 +1933,10 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
     atomicAdd(&counters[2 * sh + 1], (unsigned long long)cc);
     atomicAdd(&counters[32 + sh], (unsigned long long)cv);
     atomicAdd(&counters[48 + sh], (unsigned long long)cg);
+    atomicAdd(&counters[80 + sh], (unsigned long long)cfu);
     if (lane == 0) {  // per-wave counts (wave-uniform)
       atomicAdd(&counters[64 + sh], (unsigned long long)cb);
+      atomicAdd(&counters[96 + sh], (unsigned long long)cfb);
     }
   }
 }
@@ -3558,6 +3709,54 @@ void launch_slice_work(hipStream_t s, const VolView &v, DevPose vol2cam, LevelGe
   const int tiles = v.tiles_x * v.tiles_y;
   hipLaunchKernelGGL(k_slice_work, dim3((tiles + 3) / 4), dim3(256), (size_t)(2 * v.Z + 1) * 4, s, gv, g0, dl0,
                      vol2cam, hist);
+}
+
+// Host frame upload by the GPU itself: the source is page-locked host memory
+// mapped into the device address space (the pinned ring or a buffer the caller
+// registered), read over PCIe by a small grid of 16-B loads, several in flight
+// per lane, and written to the device slot.  Replaces hipMemcpyAsync, whose
+// host-side cost per call (~0.15 ms for a VGA frame, tools/host_input_probe.py)
+// made the caller's thread the bottleneck of kfx_pipeline_async.
+struct HostFetch {
+  const unsigned char *src[2];
+  unsigned char *dst[2];
+  size_t bytes[2];
+};
+constexpr int kFetchUnroll = 4;
+__global__ __launch_bounds__(256) void k_host_fetch(HostFetch f) {
+  const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t nth = (size_t)gridDim.x * blockDim.x;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const unsigned char *src = f.src[s];
+    unsigned char *dst = f.dst[s];
+    const size_t n = f.bytes[s];
+    if (!n) continue;
+    if (((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst) | n) & 15u) == 0) {
+      using u32x4 = unsigned __attribute__((ext_vector_type(4)));
+      const u32x4 *s4 = reinterpret_cast<const u32x4 *>(src);
+      u32x4 *d4 = reinterpret_cast<u32x4 *>(dst);
+      const size_t n4 = n / 16;
+      for (size_t i = tid; i < n4; i += nth * kFetchUnroll) {
+        u32x4 v[kFetchUnroll];
+#pragma unroll
+        for (int u = 0; u < kFetchUnroll; ++u)
+          if (i + u * nth < n4) v[u] = __builtin_nontemporal_load(s4 + i + u * nth);
+#pragma unroll
+        for (int u = 0; u < kFetchUnroll; ++u)
+          if (i + u * nth < n4) d4[i + u * nth] = v[u];
+      }
+    } else {  // unaligned caller buffers: bytes
+      for (size_t i = tid; i < n; i += nth) dst[i] = src[i];
+    }
+  }
+}
+void launch_host_fetch(hipStream_t s, const void *src0, void *dst0, size_t n0, const void *src1, void *dst1,
+                       size_t n1) {
+  HostFetch f{{static_cast<const unsigned char *>(src0), static_cast<const unsigned char *>(src1)},
+              {static_cast<unsigned char *>(dst0), static_cast<unsigned char *>(dst1)},
+              {n0, n1}};
+  hipLaunchKernelGGL(k_host_fetch, dim3(64), dim3(256), 0, s, f);
 }
 
 void launch_inv_lambda(hipStream_t s, LevelGeom g0, float *inv_lambda) {

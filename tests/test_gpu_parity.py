@@ -433,6 +433,17 @@ def test_async_host_input_matches_staged(u16, seq_qvga):
     zc.unregister_host_buffer(hb)
     with pytest.raises(KfxError):
         zc.unregister_host_buffer(hb)
+    # registered colour frames at an odd address (the fetch kernel's byte path)
+    raw = np.empty(hb.nbytes + 16, np.uint8)
+    hu = raw[3:3 + hb.nbytes].reshape(hb.shape)
+    hu[...] = hb
+    un, _ = make(intr, dims=64)
+    fu = frames.copy()  # (a page range is registered by one context at a time)
+    un.register_host_buffer(hu)
+    un.register_host_buffer(fu)
+    for k in range(len(frames)):
+        un.pipeline_async(hu[k], fu[k])
+    assert un.synchronize() == KFX_TRACKING_LOST
     ref, _ = make(intr, dims=64)
     ref.stage_frames(bgr, frames.astype(np.float32))
     for k in range(len(frames)):
@@ -440,10 +451,12 @@ def test_async_host_input_matches_staged(u16, seq_qvga):
     assert ref.synchronize() == KFX_TRACKING_LOST
     assert np.array_equal(kf.pose_record, ref.pose_record) and kf.frame_count == ref.frame_count
     assert np.array_equal(zc.pose_record, ref.pose_record) and zc.frame_count == ref.frame_count
-    for a, b, z in zip(kf.volume_soa(), ref.volume_soa(), zc.volume_soa()):
-        assert np.array_equal(a, b) and np.array_equal(z, b)
+    assert np.array_equal(un.pose_record, ref.pose_record) and un.frame_count == ref.frame_count
+    for a, b, z, u in zip(kf.volume_soa(), ref.volume_soa(), zc.volume_soa(), un.volume_soa()):
+        assert np.array_equal(a, b) and np.array_equal(z, b) and np.array_equal(u, b)
     kf.close()
     zc.close()
+    un.close()
     ref.close()
 
 
