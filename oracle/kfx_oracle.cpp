@@ -365,9 +365,28 @@ void kfo_sincos(double theta, double *s, double *c) {
   *c = std::fma(x2, pc, 1.0);
 }
 
+// 3x3 inverse by cofactors (icp_update's block solve): returns det(m); out =
+// adj(m) / det (the cofactors as one multiply and one fused multiply-subtract)
+static double kfo_inv3(const double m[3][3], double out[3][3]) {
+  double c[3][3];
+  c[0][0] = std::fma(m[1][1], m[2][2], -(m[1][2] * m[2][1]));
+  c[0][1] = std::fma(m[1][2], m[2][0], -(m[1][0] * m[2][2]));
+  c[0][2] = std::fma(m[1][0], m[2][1], -(m[1][1] * m[2][0]));
+  c[1][0] = std::fma(m[0][2], m[2][1], -(m[0][1] * m[2][2]));
+  c[1][1] = std::fma(m[0][0], m[2][2], -(m[0][2] * m[2][0]));
+  c[1][2] = std::fma(m[0][1], m[2][0], -(m[0][0] * m[2][1]));
+  c[2][0] = std::fma(m[0][1], m[1][2], -(m[0][2] * m[1][1]));
+  c[2][1] = std::fma(m[0][2], m[1][0], -(m[0][0] * m[1][2]));
+  c[2][2] = std::fma(m[0][0], m[1][1], -(m[0][1] * m[1][0]));
+  const double det = std::fma(m[0][2], c[0][2], std::fma(m[0][1], c[0][1], m[0][0] * c[0][0]));
+  const double rd = 1.0 / det;
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) out[i][j] = c[j][i] * rd;
+  return det;
+}
+
 // icp_registration.cpp:33-42: A/b unpack (rigid_icp.cu:156-165), det check
-// (cv::determinant, LU), solve (D: LU with partial pivoting and pivot
-// reciprocals instead of SVD),
+// (cv::determinant), solve (D: 3+3 block solve instead of SVD),
 // Tinc = Affine3f(rvec, t) (OpenCV Rodrigues, float/double mix), pose*Tinc (A6).
 int kfo_icp_update(const int64_t sums[27], kfx_pose *pose, double x_out[6]) {
   double A[6][6], b[6];
@@ -380,39 +399,37 @@ int kfo_icp_update(const int64_t sums[27], kfx_pose *pose, double x_out[6]) {
       else
         A[i][j] = A[j][i] = v;
     }
-  // D: A = JᵀJ is symmetric: LDLᵀ factorisation (no pivoting, one division
-  // per column, fused multiply-subtracts) instead of cv::solve(DECOMP_SVD);
-  // det = d0·…·d5 as cv::determinant's value of A.
-  double L[6][6] = {}, d[6], rd[6];
-  for (int j = 0; j < 6; ++j) {
-    double w[6];
-    double dj = A[j][j];
-    for (int k = 0; k < j; ++k) {
-      w[k] = L[j][k] * d[k];
-      dj = std::fma(-L[j][k], w[k], dj);
+  // D: A = JᵀJ is symmetric positive (semi)definite: instead of
+  // cv::solve(DECOMP_SVD), a 3+3 block solve — P = A[0:3,0:3] (rotation), Q =
+  // A[0:3,3:6], R = A[3:6,3:6], S = R − Qᵀ P⁻¹ Q (Schur complement), the 3×3
+  // inverses by cofactors (one division each), det A = det P · det S as
+  // cv::determinant's value.  Two divisions on the dependency chain instead of
+  // six (the kernel's icp_update runs these exact operations).
+  double P[3][3], Q[3][3], R[3][3];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) {
+      P[i][j] = A[i][j];
+      Q[i][j] = A[i][j + 3];
+      R[i][j] = A[i + 3][j + 3];
     }
-    d[j] = dj;
-    rd[j] = 1.0 / dj;
-    for (int i = j + 1; i < 6; ++i) {
-      double s = A[i][j];
-      for (int k = 0; k < j; ++k) s = std::fma(-L[i][k], w[k], s);
-      L[i][j] = s * rd[j];
-    }
-  }
-  double det = d[0];
-  for (int k = 1; k < 6; ++k) det = det * d[k];
+  double Pi[3][3], Si[3][3], S[3][3], M[3][3];
+  const double detP = kfo_inv3(P, Pi);
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j)
+      M[i][j] = std::fma(Pi[i][2], Q[2][j], std::fma(Pi[i][1], Q[1][j], Pi[i][0] * Q[0][j]));
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j)
+      S[i][j] = std::fma(-Q[2][i], M[2][j], std::fma(-Q[1][i], M[1][j], std::fma(-Q[0][i], M[0][j], R[i][j])));
+  const double detS = kfo_inv3(S, Si);
+  const double det = detP * detS;
   if (std::fabs(det) < 1e-15 || std::isnan(det)) return 1;
-  double y[6], x[6];
-  for (int i = 0; i < 6; ++i) {  // L y = b
-    double acc = b[i];
-    for (int k = 0; k < i; ++k) acc = std::fma(-L[i][k], y[k], acc);
-    y[i] = acc;
-  }
-  for (int i = 5; i >= 0; --i) {  // Lᵀ x = D⁻¹ y
-    double acc = y[i] * rd[i];
-    for (int k = i + 1; k < 6; ++k) acc = std::fma(-L[k][i], x[k], acc);
-    x[i] = acc;
-  }
+  double y1[3], z[3], x[6];
+  for (int i = 0; i < 3; ++i) y1[i] = std::fma(Pi[i][2], b[2], std::fma(Pi[i][1], b[1], Pi[i][0] * b[0]));
+  for (int i = 0; i < 3; ++i)
+    z[i] = std::fma(-Q[2][i], y1[2], std::fma(-Q[1][i], y1[1], std::fma(-Q[0][i], y1[0], b[3 + i])));
+  for (int i = 0; i < 3; ++i) x[3 + i] = std::fma(Si[i][2], z[2], std::fma(Si[i][1], z[1], Si[i][0] * z[0]));
+  for (int i = 0; i < 3; ++i)
+    x[i] = std::fma(-M[i][2], x[5], std::fma(-M[i][1], x[4], std::fma(-M[i][0], x[3], y1[i])));
   if (x_out)
     for (int i = 0; i < 6; ++i) x_out[i] = x[i];
   // cv::Affine3f(Vec3f rvec, Vec3f t): the Vec3d arguments narrow to float.

@@ -336,7 +336,7 @@ int enqueue_icp_sharded(kfx_ctx *c, bool begin) {
 // integrate + raycast of the frame whose maps are in the current set
 void enqueue_map(kfx_ctx *c, FrameInput in, hipEvent_t *ev) {
   hipStream_t s = c->stream;
-  launch_integrate(s, c->vol, c->g[0], c->dl0, in.bgr, c->st, c->pose_log,
+  launch_integrate(s, c->vol, c->g[0], c->dl0, c->cur.d[0], c->inv_lambda, in.bgr, c->st, c->pose_log,
                    to_dev(c->p.volu_pose), nullptr, nullptr);
   if (ev) (void)hipEventRecord(ev[3], s);
   launch_raycast(s, c->vol, c->L, c->g, c->cur, c->prev, c->st, c->pose_log,
@@ -1574,7 +1574,7 @@ int kfx_stage_icp(kfx_ctx *c, kfx_pose *out) {
 // integrate
 static int integrate_stats_impl(kfx_ctx *c, int64_t out[8], const float *xpose) {
   HIPCHK(hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * 128, c->stream));
-  launch_integrate(c->stream, c->vol, c->g[0], c->dl0, c->last_bgr ? c->last_bgr : c->bgr, c->st,
+  launch_integrate(c->stream, c->vol, c->g[0], c->dl0, c->cur.d[0], c->inv_lambda, c->last_bgr ? c->last_bgr : c->bgr, c->st,
                    c->pose_log, to_dev(c->p.volu_pose), xpose, c->counters);
   HIPCHK(hipGetLastError());
   unsigned long long h[128];
@@ -1608,7 +1608,7 @@ int kfx_stage_integrate(kfx_ctx *c, const kfx_pose *vol2cam, int64_t *nu, int64_
   HIPCHK(hipMemcpyAsync(c->xpose, xp, sizeof(xp), hipMemcpyHostToDevice, c->stream));
   if (nu || nc)
     if ((r = integrate_counts_impl(c, nu, nc, c->xpose))) return r;
-  launch_integrate(c->stream, c->vol, c->g[0], c->dl0, c->bgr, c->st, c->pose_log,
+  launch_integrate(c->stream, c->vol, c->g[0], c->dl0, c->cur.d[0], c->inv_lambda, c->bgr, c->st, c->pose_log,
                    to_dev(c->p.volu_pose), c->xpose, nullptr);
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(c->stream));

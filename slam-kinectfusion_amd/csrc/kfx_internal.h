@@ -223,9 +223,10 @@ void launch_group_sum_icp(hipStream_t s, DevState *const *st, int n);
 // DevState + pose log (no separate commit launch).  `xpose` (device, 12 or 21
 // floats: pose [, Rinv]) overrides them for the stage seams; bookkeeping is
 // then skipped.
-// dl0: level-0 {depth m, 1/lambda} (written by launch_preprocess_maps)
-void launch_integrate(hipStream_t s, VolView v, LevelGeom g0, const float2 *dl0,
-                      const uint8_t *bgr, DevState *st, DevPose *log, DevPose vpose,
+// dl0: level-0 {depth m, 1/lambda} (written by launch_preprocess_maps); dmap:
+// the same filtered depth alone (the frame's level-0 map); invl: 1/lambda
+void launch_integrate(hipStream_t s, VolView v, LevelGeom g0, const float2 *dl0, const float *dmap,
+                      const float *invl, const uint8_t *bgr, DevState *st, DevPose *log, DevPose vpose,
                       const float *xpose,
                       unsigned long long *counters /* non-null: count-only, 32 words */);
 // raycast of level 0 + resizePointsNormals of levels >= 1 in one launch; with

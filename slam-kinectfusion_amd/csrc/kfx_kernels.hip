@@ -75,6 +75,9 @@
 #ifndef KFX_INT_PCHUNKR
 #define KFX_INT_PCHUNKR 100  // planned integrate: chunk weights (100: equal chunks)
 #endif
+#ifndef KFX_INT_ZCLASS
+#define KFX_INT_ZCLASS 0  // integrate: 4-B depth gathers, voxels classified by the vc.z bound, exact sdf only near surfaces (A/B)
+#endif
 #ifndef KFX_INT_CERT
 #define KFX_INT_CERT 0  // integrate: certified free-space groups skip projection, gather and sdf (measured slower)
 #endif
@@ -593,6 +596,9 @@ __global__ __launch_bounds__(256) void k_preprocess_maps(BilatArgs a) {
 #define KFX_ICP_PIX 4
 #endif
 constexpr int kIcpPix = KFX_ICP_PIX;
+#ifndef KFX_RAY_SLAB_SKIP
+#define KFX_RAY_SLAB_SKIP 1  // slab raycast: rays jump over the samples before the stored slices
+#endif
 #ifndef KFX_RAY_N32
 #define KFX_RAY_N32 1  // raycast normals: 32-bit tile-column offsets + buffer loads (kIdx32 volumes)
 #endif
@@ -1037,13 +1043,14 @@ __device__ __forceinline__ double bcast(double v, int src) {
 }
 
 // icp_registration.cpp:33-42 on the device: A/b unpack (rigid_icp.cu:156-165),
-// LDLᵀ factorisation with det check and the triangular solves (D: instead of
-// SVD; A = JᵀJ is symmetric), Rodrigues, pose = pose * Tinc.  Every lane
+// 3+3 block solve with det check (D: instead of SVD; A = JᵀJ is symmetric),
+// Rodrigues, pose = pose * Tinc.  Every lane
 // runs the whole solve on its own registers (identical, wave-uniform values:
 // no cross-lane traffic on the critical path).  Each double operation is the
 // oracle's (kfo_icp_update) in the same order, so the result is
-// bit-identical.  (The earlier partial-pivot LU spent most of its ~3.4k
-// cycles on data-dependent row moves.)  a27: the 27 sums already unpacked by
+// bit-identical.  (A partial-pivot LU spent most of its ~3.4k cycles on
+// data-dependent row moves; the LDLᵀ after it ran six divisions in a row.)
+// a27: the 27 sums already unpacked by
 // icp_sum_value (any memory, read by all lanes; the unpack is done once per
 // value by 27 threads, not 27 times per solver lane).
 // D: cos / sin of the Rodrigues angle as the oracle's kfo_sincos (theta < 0.5:
@@ -1073,6 +1080,27 @@ __device__ __forceinline__ void det_sincos(double theta, double *s, double *c) {
   *c = fma(x2, pc, 1.0);
 }
 
+// 3x3 inverse by cofactors (the oracle's kfo_inv3): returns det(m), out = adj(m) / det
+__device__ __forceinline__ double inv3(const double (&m)[3][3], double (&out)[3][3]) {
+  double c[3][3];
+  c[0][0] = fma(m[1][1], m[2][2], -(m[1][2] * m[2][1]));
+  c[0][1] = fma(m[1][2], m[2][0], -(m[1][0] * m[2][2]));
+  c[0][2] = fma(m[1][0], m[2][1], -(m[1][1] * m[2][0]));
+  c[1][0] = fma(m[0][2], m[2][1], -(m[0][1] * m[2][2]));
+  c[1][1] = fma(m[0][0], m[2][2], -(m[0][2] * m[2][0]));
+  c[1][2] = fma(m[0][1], m[2][0], -(m[0][0] * m[2][1]));
+  c[2][0] = fma(m[0][1], m[1][2], -(m[0][2] * m[1][1]));
+  c[2][1] = fma(m[0][2], m[1][0], -(m[0][0] * m[1][2]));
+  c[2][2] = fma(m[0][0], m[1][1], -(m[0][1] * m[1][0]));
+  const double det = fma(m[0][2], c[0][2], fma(m[0][1], c[0][1], m[0][0] * c[0][0]));
+  const double rd = 1.0 / det;
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) out[i][j] = c[j][i] * rd;
+  return det;
+}
+
 __device__ int icp_update(const double *a27, DevPose &pose, double *xo) {
   double A[6][7];  // column 6 = b
   {
@@ -1086,48 +1114,43 @@ __device__ int icp_update(const double *a27, DevPose &pose, double *xo) {
         if (j < 6) A[j][i] = v;
       }
   }
-  // LDLᵀ of the symmetric A (no pivoting: no data-dependent register moves;
-  // one division per column; fused multiply-subtracts as the oracle's),
-  // det = d0·…·d5
-  double L[6][6], d[6], rd[6];
+  // D: 3+3 block solve (the oracle's kfo_icp_update, operation for
+  // operation): P = A[0:3,0:3], Q = A[0:3,3:6], R = A[3:6,3:6], S = R − Qᵀ P⁻¹ Q;
+  // 3×3 inverses by cofactors, det A = det P · det S.  Two divisions on the
+  // dependency chain (the LDLᵀ it replaces had six plus two substitution
+  // chains), so the per-iteration solve every lane runs is shorter.
+  double P[3][3], Q[3][3], R[3][3];
 #pragma unroll
-  for (int j = 0; j < 6; ++j) {
-    double w[6];
-    double dj = A[j][j];
+  for (int i = 0; i < 3; ++i)
 #pragma unroll
-    for (int k = 0; k < j; ++k) {
-      w[k] = L[j][k] * d[k];
-      dj = fma(-L[j][k], w[k], dj);
+    for (int j = 0; j < 3; ++j) {
+      P[i][j] = A[i][j];
+      Q[i][j] = A[i][j + 3];
+      R[i][j] = A[i + 3][j + 3];
     }
-    d[j] = dj;
-    rd[j] = 1.0 / dj;
+  double Pi[3][3], Si[3][3], S[3][3], M[3][3];
+  const double detP = inv3(P, Pi);
 #pragma unroll
-    for (int i = j + 1; i < 6; ++i) {
-      double s = A[i][j];
+  for (int i = 0; i < 3; ++i)
 #pragma unroll
-      for (int k = 0; k < j; ++k) s = fma(-L[i][k], w[k], s);
-      L[i][j] = s * rd[j];
-    }
-  }
-  double det = d[0];
+    for (int j = 0; j < 3; ++j) M[i][j] = fma(Pi[i][2], Q[2][j], fma(Pi[i][1], Q[1][j], Pi[i][0] * Q[0][j]));
 #pragma unroll
-  for (int k = 1; k < 6; ++k) det = det * d[k];
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      S[i][j] = fma(-Q[2][i], M[2][j], fma(-Q[1][i], M[1][j], fma(-Q[0][i], M[0][j], R[i][j])));
+  const double detS = inv3(S, Si);
+  const double det = detP * detS;
   if (fabs(det) < 1e-15 || isnan(det)) return 1;
-  double y[6], x[6];
+  double y1[3], z[3], x[6];
 #pragma unroll
-  for (int i = 0; i < 6; ++i) {  // L y = b
-    double acc = A[i][6];
+  for (int i = 0; i < 3; ++i) y1[i] = fma(Pi[i][2], A[2][6], fma(Pi[i][1], A[1][6], Pi[i][0] * A[0][6]));
 #pragma unroll
-    for (int k = 0; k < i; ++k) acc = fma(-L[i][k], y[k], acc);
-    y[i] = acc;
-  }
+  for (int i = 0; i < 3; ++i) z[i] = fma(-Q[2][i], y1[2], fma(-Q[1][i], y1[1], fma(-Q[0][i], y1[0], A[3 + i][6])));
 #pragma unroll
-  for (int i = 5; i >= 0; --i) {  // Lᵀ x = D⁻¹ y
-    double acc = y[i] * rd[i];
+  for (int i = 0; i < 3; ++i) x[3 + i] = fma(Si[i][2], z[2], fma(Si[i][1], z[1], Si[i][0] * z[0]));
 #pragma unroll
-    for (int k = i + 1; k < 6; ++k) acc = fma(-L[k][i], x[k], acc);
-    x[i] = acc;
-  }
+  for (int i = 0; i < 3; ++i) x[i] = fma(-M[i][2], x[5], fma(-M[i][1], x[4], fma(-M[i][0], x[3], y1[i])));
 #pragma unroll
   for (int r = 0; r < 6; ++r) xo[r] = x[r];
   // cv::Affine3f(Vec3f rvec, Vec3f t): the Vec3d arguments narrow to float.
@@ -1564,6 +1587,8 @@ __device__ __forceinline__ bool cert_free(f3 vc, f3 zs, const LevelGeom &g, cons
 template <bool kCount, bool kIdx32, bool kPlan>
 __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(KFX_INT_OCC, KFX_INT_OCC))) void k_integrate(VolView v, LevelGeom g,
                                                    const float2 *__restrict__ dl,
+                                                   const float *__restrict__ dmap,
+                                                   const float *__restrict__ invl,
                                                    const uint8_t *__restrict__ bgr,
                                                    DevState *__restrict__ st, DevPose *log,
                                                    DevPose vpose, const float *xpose,
@@ -1673,7 +1698,30 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
   using Mem = VoxMem<kIdx32>;
   using Idx = typename Mem::Idx;
   const Mem mem(v);
+#if KFX_INT_ZCLASS
+  // pixel offsets in 4-byte units: the gather reads the filtered depth map alone
+  constexpr unsigned kPixB = 4u, kPixSh = 2u;
+  const __amdgpu_buffer_rsrc_t rdm = make_rsrc(dmap, (unsigned)(4 * g.w * g.h));
+  const __amdgpu_buffer_rsrc_t riv = make_rsrc(invl, (unsigned)(4 * g.w * g.h));
+  // For a voxel whose rounded projection lies in the image, RN(1/lambda *
+  // |vc|) lies in [vc.z / cB, vc.z * cB]: its ray and its pixel's centre ray
+  // differ by <= 0.51 px, so lambda_v^2 - lambda_p^2 (and its negative) is at
+  // most ex (2 xmax + ex) + ey (2 ymax + ey), lambda_p >= 1; 1e-5 of relative
+  // margin covers the roundings of the table, sqrt_rn and the product.  The
+  // exact sdf is then >= d - vc.z cB and <= d - vc.z / cB.
+  const float zex = 0.51f / g.fx, zey = 0.51f / g.fy;
+  const float zxm = (fmaxf(g.cx, (float)g.w - 1.f - g.cx) + 0.51f) / g.fx;
+  const float zym = (fmaxf(g.cy, (float)g.h - 1.f - g.cy) + 0.51f) / g.fy;
+  const float zcb = sqrtf(1.f + zex * (2.f * zxm + zex) + zey * (2.f * zym + zey)) * 1.00001f;
+  const float zcbi = 1.f / zcb;
+  const float zfree = trunc + 1e-5f, zrej = -trunc - 1e-5f;
+  (void)dl;
+#else
+  constexpr unsigned kPixB = 8u, kPixSh = 3u;
   const __amdgpu_buffer_rsrc_t rdl = make_rsrc(dl, (unsigned)(8 * g.w * g.h));
+  (void)dmap;
+  (void)invl;
+#endif
   constexpr Idx slice = 64;  // index step per z (tile-column layout)
   Idx iz = (Idx)base + (Idx)(za - v.zb) * slice;  // voxel index of (x, y, z)
   const bool fast = __all(!live || column_fast(vc, zs, v.Z));  // wave-uniform
@@ -1734,9 +1782,6 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
       dd_pix = kOob;
 #endif
     } else {
-    float n2[kB];
-#pragma unroll
-    for (int j = 0; j < kB; ++j) n2[j] = dot(p[j], p[j]);
     // projection: ok = in the image in front of the camera (tsdf_volume.cu:56-66)
     if (fast) {  // the cheap exact sequences, two voxels per packed-FP32 op
       static_assert(kB % 2 == 0, "voxel pairs");
@@ -1755,11 +1800,11 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
           // value; 24-bit multiply (w, h < 2^24)
           const int iu = (int)rintf(uu[k]), iv = (int)rintf(vv[k]);
           ok[j + k] = (z + j + k >= la) & (z + j + k <= lb) & (pz[k] > 0) & ((unsigned)iu < (unsigned)g.w) & ((unsigned)iv < (unsigned)g.h);
-          pix[j + k] = ok[j + k] ? __umul24((unsigned)iv, 8u * (unsigned)g.w) + ((unsigned)iu << 3) : kOob;
+          pix[j + k] = ok[j + k] ? __umul24((unsigned)iv, kPixB * (unsigned)g.w) + ((unsigned)iu << kPixSh) : kOob;
 #else
           const float uf = rintf(uu[k]), vf = rintf(vv[k]);
           ok[j + k] = (z + j + k >= la) & (z + j + k <= lb) & (pz[k] > 0) & (uf >= 0.f) & (uf < fw) & (vf >= 0.f) & (vf < fh);
-          pix[j + k] = ok[j + k] ? ((unsigned)(int)vf * (unsigned)g.w + (unsigned)(int)uf) * 8u : kOob;
+          pix[j + k] = ok[j + k] ? ((unsigned)(int)vf * (unsigned)g.w + (unsigned)(int)uf) * kPixB : kOob;
 #endif
         }
       }
@@ -1769,10 +1814,54 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
         const float uf = rintf((p[j].x / p[j].z) * g.fx + g.cx);
         const float vf = rintf((p[j].y / p[j].z) * g.fy + g.cy);
         ok[j] = (z + j >= la) & (z + j <= lb) & (p[j].z > 0) & (uf >= 0.f) & (uf < fw) & (vf >= 0.f) & (vf < fh);
-        pix[j] = ok[j] ? ((unsigned)(int)vf * (unsigned)g.w + (unsigned)(int)uf) * 8u : kOob;
+        pix[j] = ok[j] ? ((unsigned)(int)vf * (unsigned)g.w + (unsigned)(int)uf) * kPixB : kOob;
       }
     }
+#if KFX_INT_ZCLASS
+    // 4-B depth gathers; the vc.z bound settles free space (sdf >= trunc: ts =
+    // 1, no colour band) and voxels far behind the surface (sdf < -trunc); only
+    // voxels near +-trunc gather 1/lambda and take the exact sdf
+    float dd[kB];
+#pragma unroll
+    for (int j = 0; j < kB; ++j) dd[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rdm, pix[j], 0, 0));
+    bool bnd[kB];
+    bool banyl = false;
+#pragma unroll
+    for (int j = 0; j < kB; ++j) {
+      const bool fr = fmaf(-p[j].z, zcb, dd[j]) >= zfree;
+      const bool rj = fmaf(-p[j].z, zcbi, dd[j]) < zrej;
+      bnd[j] = ok[j] & (dd[j] > 0.f) & !fr & !rj;
+      sdf[j] = fr ? 2.f * trunc : -2.f * trunc;
+      banyl |= bnd[j];
+    }
+    if (__any(banyl)) {  // exact sdf (tsdf_volume.cu:67-68) of the voxels near +-trunc
+      float il[kB], n2[kB];
+#pragma unroll
+      for (int j = 0; j < kB; ++j) {
+        il[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(riv, bnd[j] ? pix[j] : kOob, 0, 0));
+        n2[j] = dot(p[j], p[j]);
+      }
+      if (fast) {
+#pragma unroll
+        for (int j = 0; j < kB; j += 2) {
+          const pf2 sd = -(pf2{il[j], il[j + 1]} * sqrt_rn2(pf2{n2[j], n2[j + 1]}) - pf2{dd[j], dd[j + 1]});
+          if (bnd[j]) sdf[j] = sd.x;
+          if (bnd[j + 1]) sdf[j + 1] = sd.y;
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < kB; ++j)
+          if (bnd[j]) sdf[j] = -(il[j] * sqrtf(n2[j]) - dd[j]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kB; ++j) ok[j] = ok[j] & (dd[j] > 0) & (sdf[j] >= -trunc);
+    }
+#else
     float2 d[kB];
+    float n2[kB];
+#pragma unroll
+    for (int j = 0; j < kB; ++j) n2[j] = dot(p[j], p[j]);
 #if KFX_INT_DEDUP
     // consecutive voxels of a column often project to the same pixel: such a
     // voxel reuses the previous one's {depth, 1/lambda} instead of gathering
@@ -1824,6 +1913,7 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
 #pragma unroll
     for (int j = 0; j < kB; ++j) ok[j] = ok[j] & (d[j].x > 0) & (sdf[j] >= -trunc);
     }
+#endif
     if (kCount) {
       iz += (Idx)kB * slice;
       ++cb;
@@ -1894,7 +1984,7 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
 #endif
       if (sdf[j] <= thres_color && sdf[j] >= -thres_color) {  // colour band (rare)
         const uint32_t c0 = mem.ld_c(i);
-        const uint8_t *px = bgr + 3 * (size_t)(pix[j] >> 3);
+        const uint8_t *px = bgr + 3 * (size_t)(pix[j] >> kPixSh);
         const float c = (float)(new_w + 1);
         const float rc = rtab[new_w + 1];
         uint32_t out = 0u;
@@ -2170,6 +2260,34 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KFX_RAY_OCC
     constexpr int kR = KFX_RAY_KR;
     int sprev = isnan(tprev) ? 0 : (tprev > 0.f ? 1 : (tprev < 0.f ? -1 : 0));
     uint32_t kbase = 1u;  // loop sample index of the batch's first sample
+#if KFX_RAY_SLAB_SKIP
+    if (kSlab && live) {
+      // A slab stores slices [zb, zb + zn): the samples a ray takes before it
+      // reaches them read no voxel (NaN: no event, tsdf_volume.cu:184-188), so
+      // the ray jumps over them at once — the exact positions and ray_len of
+      // that many float adds (ff_add), the sample index advanced by as many —
+      // instead of marching them batch by batch (the middle slabs' rays cross
+      // the whole volume before theirs).  The count keeps 1.5 voxels and one
+      // sample of margin over the continuous model of the accumulated adds.
+      const float czv = nextp.z * rc.vs_inv.z, dcz = vstep.z * rc.vs_inv.z;
+      float nf = 0.f;
+      if (dcz > 0.f) nf = ((float)v.zb - 1.5f - czv) / dcz;
+      else if (dcz < 0.f) nf = (czv - ((float)(v.zb + v.zn) + 0.5f)) / -dcz;
+      if (nf >= 2.f) {
+        const int n0 = (int)fminf(nf, 1.0e7f) - 1;
+        // the reference tests ray_len < tfar before each of the n0 steps
+        if (!(ff_add(ray_len, rc.step, n0 - 1) < tfar)) {
+          live = false;  // the march ends among the skipped samples: no event here
+        } else {
+          nextp = {ff_add(nextp.x, vstep.x, n0), ff_add(nextp.y, vstep.y, n0), ff_add(nextp.z, vstep.z, n0)};
+          ray_len = ff_add(ray_len, rc.step, n0);
+          kbase += (uint32_t)n0;
+          tprev = voxel2tsdf(v, rc, nextp);
+          sprev = isnan(tprev) ? 0 : (tprev > 0.f ? 1 : (tprev < 0.f ? -1 : 0));
+        }
+      }
+    }
+#endif
     const RayMem<kIdx32> mem(v);
     // voxel validity 1 <= i <= dim-2 (tsdf_volume.cu:184-185) tested on the
     // rounded floats (exact integers; NaN fails like __float2int_rn's INT_MIN)
@@ -3417,8 +3535,8 @@ __global__ __launch_bounds__(1024) void k_int_order(const unsigned *__restrict__
   for (int i = t; i < n; i += 1024) perm[atomicAdd(&hist[bucket(i)], 1u)] = (unsigned)i;
 }
 
-void launch_integrate(hipStream_t s, VolView v, LevelGeom g0, const float2 *dl0,
-                      const uint8_t *bgr, DevState *st, DevPose *log, DevPose vpose,
+void launch_integrate(hipStream_t s, VolView v, LevelGeom g0, const float2 *dl0, const float *dmap,
+                      const float *invl, const uint8_t *bgr, DevState *st, DevPose *log, DevPose vpose,
                       const float *xpose, unsigned long long *counters) {
   const int tiles = v.tiles_x * v.tiles_y;
   const int nchunk = integrate_chunks(v);
@@ -3451,16 +3569,16 @@ void launch_integrate(hipStream_t s, VolView v, LevelGeom g0, const float2 *dl0,
   (void)hipMemsetAsync(trace_buf, 0, sizeof(unsigned long long) * 4 * g_int_trace_waves, s);  // waves that exit early write none
   if (!counters) {
     if (planned)
-      hipLaunchKernelGGL((k_integrate<false, true, true>), grd, dim3(KFX_INT_BLOCK), 0, s, v, g0, dl0, bgr, st,
+      hipLaunchKernelGGL((k_integrate<false, true, true>), grd, dim3(KFX_INT_BLOCK), 0, s, v, g0, dl0, dmap, invl, bgr, st,
                          log, vpose, xpose, trace_buf);
     else
-      hipLaunchKernelGGL((k_integrate<false, true, false>), grd, dim3(KFX_INT_BLOCK), 0, s, v, g0, dl0, bgr, st,
+      hipLaunchKernelGGL((k_integrate<false, true, false>), grd, dim3(KFX_INT_BLOCK), 0, s, v, g0, dl0, dmap, invl, bgr, st,
                          log, vpose, xpose, trace_buf);
     return;
   }
 #endif
 #define KFX_LAUNCH_INT(C, I, P)                                                                             \
-  hipLaunchKernelGGL((k_integrate<C, I, P>), grd, dim3(KFX_INT_BLOCK), 0, s, v, g0, dl0, bgr, st, log, vpose, xpose, \
+  hipLaunchKernelGGL((k_integrate<C, I, P>), grd, dim3(KFX_INT_BLOCK), 0, s, v, g0, dl0, dmap, invl, bgr, st, log, vpose, xpose, \
                      counters)
   if (counters) {
     if (planned) KFX_LAUNCH_INT(true, false, true);

@@ -168,6 +168,30 @@ def test_icp_identical_frames_zero_increment(oracle_lib):
     assert np.array_equal(pose.matrix(), np.eye(4, dtype=np.float32))
 
 
+def test_icp_block_solve_matches_numpy(oracle_lib):
+    """The 3+3 block solve (D: instead of cv::solve(DECOMP_SVD)) on random
+    normal equations A = JᵀJ, b = Jᵀr given as the 2^-32 fixed-point sums:
+    x agrees with numpy's LU solve of the same A, b to 1e-9 relative."""
+    rng = np.random.default_rng(11)
+    iu = [(i, j) for i in range(6) for j in range(i, 7)]
+    for trial in range(20):
+        J = rng.normal(size=(400, 6)) * rng.uniform(0.05, 2.0, size=6)
+        r = rng.normal(size=400) * 1e-3
+        A = J.T @ J
+        b = J.T @ r
+        Ab = np.concatenate([A, b[:, None]], 1)
+        sums = np.array([round(Ab[i, j] * 2.0 ** 32) for i, j in iu], np.int64)
+        Aq = np.zeros((6, 7))
+        for k, (i, j) in enumerate(iu):
+            Aq[i, j] = sums[k] / 2.0 ** 32
+            if j < 6:
+                Aq[j, i] = Aq[i, j]
+        st, _, x = oracle_lib.icp_update(sums, Pose.identity())
+        xe = np.linalg.solve(Aq[:, :6], Aq[:, 6])
+        assert st == 0
+        assert np.abs(x - xe).max() <= 1e-9 * np.abs(xe).max(), trial
+
+
 def test_icp_singular_fails(oracle_lib):
     st, _, _ = oracle_lib.icp_update(np.zeros(27, np.int64), Pose.identity())
     assert st == 1  # det < 1e-15 -> tracking fail (icp_registration.cpp:35-37)
