@@ -348,11 +348,15 @@ def extract_record(kf, n):
     marching-cubes extract): kfx_extract_points (FullScan6 zero crossings,
     tsdf_volume.cu:307-481) and kfx_extract_mesh on the volume the timed frames
     built; device ms of the count pass, the offset scan and the emit pass
-    (HIP events).  Roofline: each pass reads every scanned voxel's int16 tsdf +
-    u8 weight (3 B; neighbours come from cache), the emit pass also writes
-    12 B per point / 36 B per triangle."""
+    (HIP events).  Roofline: each pass of the reference's full scan reads every
+    voxel's int16 tsdf + u8 weight (3 B; neighbours come from cache), the emit
+    pass also writes 12 B per point / 36 B per triangle.  The kernels skip the
+    waves whose brick the occupancy map proves empty, so `achieved` is the
+    full-scan-equivalent rate."""
     vox = n * n * (n - 1)  # z = 0 .. Z-2 (the +z neighbour must exist)
-    out = {"voxels_scanned": vox, "peak": HBM_PEAK_GBS, "unit": "GB/s"}
+    out = {"voxels_scanned": vox, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "bytes_basis": "2 full-volume passes of 3 B/voxel + outputs (the reference's scan); "
+                          "clear bricks are skipped, so achieved is the full-scan-equivalent rate"}
     for name, fn, per in (("points", kf.extract_points, 12), ("mesh", kf.extract_mesh, 36)):
         items = fn(cap=50_000_000)
         ms = kf.extract_ms()

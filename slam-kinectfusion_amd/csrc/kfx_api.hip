@@ -1029,7 +1029,11 @@ static int pipeline_async(kfx_ctx *c, const uint8_t *bgr, const void *depth, boo
       HIPCHK(hipHostMalloc((void **)&c->ring_host, c->ring_slot * kfx_ctx::kRing, hipHostMallocMapped));
     if (!c->ring_host_dev) HIPCHK(hipHostGetDevicePointer((void **)&c->ring_host_dev, c->ring_host, 0));
     if (!c->ring_dev && (r = dalloc(c, (void **)&c->ring_dev, c->ring_slot * kfx_ctx::kRing))) return r;
-    if (!c->cstream) HIPCHK(hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
+    if (!c->cstream) {  // the lowest priority: the frame kernels are dispatched ahead of the uploads
+      int lo = 0, hi = 0;
+      HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+      HIPCHK(hipStreamCreateWithPriority(&c->cstream, hipStreamNonBlocking, lo));
+    }
     for (int k = 0; k < kfx_ctx::kRing; ++k) {
       if (!c->ring_h2d[k]) HIPCHK(hipEventCreateWithFlags(&c->ring_h2d[k], hipEventDisableTiming));
       if (!c->ring_done[k]) HIPCHK(hipEventCreateWithFlags(&c->ring_done[k], hipEventDisableTiming));

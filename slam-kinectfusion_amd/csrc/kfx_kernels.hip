@@ -596,6 +596,9 @@ __global__ __launch_bounds__(256) void k_preprocess_maps(BilatArgs a) {
 #define KFX_ICP_PIX 4
 #endif
 constexpr int kIcpPix = KFX_ICP_PIX;
+#ifndef KFX_EXTRACT_SKIP
+#define KFX_EXTRACT_SKIP 1  // point / mesh extraction: waves of clear bricks read nothing
+#endif
 #ifndef KFX_RAY_SLAB_SKIP
 #define KFX_RAY_SLAB_SKIP 1  // slab raycast: rays jump over the samples before the stored slices
 #endif
@@ -2935,6 +2938,17 @@ __device__ __forceinline__ int extract_voxel(const VolView &v, const DevPose &af
 // kEmit = false: counts[wave] = points of the wave; true: write them at
 // offsets[wave] + rank (rank < cap only).  z in [zlo, zhi) (global slices,
 // zhi <= Z - 1; a slab passes its owned range).
+// Extraction waves own one tile x one 8-slice chunk (kExtractZ), i.e. one
+// brick.  Every point needs a negative tsdf at the voxel or its +x/+y/+z
+// neighbour, and every marching-cubes triangle a negative corner: all of them
+// lie in the brick or a neighbouring one, so a clear (dilated) brick bit of
+// the occupancy map proves the wave outputs nothing — it reads no voxel.
+__device__ __forceinline__ bool brick_clear(const VolView &v, int tile, int c0) {
+  const int lbz = (c0 >> 3) - v.bz0;
+  if (lbz < 0 || lbz >= v.nbz) return false;
+  return !((v.bocc[(size_t)tile * v.bw + (lbz >> 6)] >> (lbz & 63)) & 1ull);
+}
+
 template <bool kEmit>
 __global__ __launch_bounds__(256) void k_extract(VolView v, DevPose aff, int zlo, int zhi,
                                                  unsigned *counts, const unsigned long long *offsets,
@@ -2950,6 +2964,11 @@ __global__ __launch_bounds__(256) void k_extract(VolView v, DevPose aff, int zlo
   // too), so concatenating slabs in rank order reproduces the single volume
   const int c0 = (zlo / kExtractZ) * kExtractZ + (int)blockIdx.y * kExtractZ;
   const int z0 = max(zlo, c0), z1 = min(zhi, c0 + kExtractZ);
+  static_assert(kExtractZ == 8, "one brick per wave");
+  if (KFX_EXTRACT_SKIP && brick_clear(v, tile, c0)) {  // wave-uniform
+    if (!kEmit && lane == 0) counts[wave] = 0;
+    return;
+  }
   unsigned long long base = kEmit ? offsets[wave] : 0ull;
   unsigned total = 0;
   const unsigned long long below = (1ull << lane) - 1ull;
@@ -3018,6 +3037,10 @@ __global__ __launch_bounds__(256) void k_mesh(VolView v, DevPose aff, int zlo, i
   const int y = (tile / v.tiles_x) * 8 + (lane >> 3);
   const int c0 = (zlo / kExtractZ) * kExtractZ + (int)blockIdx.y * kExtractZ;
   const int z0 = max(zlo, c0), z1 = min(zhi, c0 + kExtractZ);
+  if (KFX_EXTRACT_SKIP && brick_clear(v, tile, c0)) {  // wave-uniform
+    if (!kEmit && (threadIdx.x & 63) == 0) counts[wave] = 0;
+    return;
+  }
   unsigned long long base = kEmit ? offsets[wave] : 0ull;
   unsigned total = 0;
   for (int z = z0; z < z1; ++z) {
@@ -3840,6 +3863,9 @@ struct HostFetch {
   unsigned char *dst[2];
   size_t bytes[2];
 };
+#ifndef KFX_FETCH_BLOCKS
+#define KFX_FETCH_BLOCKS 64  // host fetch grid (PCIe-latency bound: 64 x 256 lanes x 4 x 16 B in flight)
+#endif
 constexpr int kFetchUnroll = 4;
 __global__ __launch_bounds__(256) void k_host_fetch(HostFetch f) {
   const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -3874,7 +3900,7 @@ void launch_host_fetch(hipStream_t s, const void *src0, void *dst0, size_t n0, c
   HostFetch f{{static_cast<const unsigned char *>(src0), static_cast<const unsigned char *>(src1)},
               {static_cast<unsigned char *>(dst0), static_cast<unsigned char *>(dst1)},
               {n0, n1}};
-  hipLaunchKernelGGL(k_host_fetch, dim3(64), dim3(256), 0, s, f);
+  hipLaunchKernelGGL(k_host_fetch, dim3(KFX_FETCH_BLOCKS), dim3(256), 0, s, f);
 }
 
 void launch_inv_lambda(hipStream_t s, LevelGeom g0, float *inv_lambda) {
