@@ -80,6 +80,9 @@ def parse():
                     help="auto: single at N=1, slab at N>1")
     ap.add_argument("--icp", choices=["replicated", "allreduce"], default="replicated",
                     help="slab mode: every rank runs the full ICP, or its band with the partials all-reduced")
+    ap.add_argument("--zslab", choices=["none", "c2", "c4", "c5"], default="c4",
+                    help="N>1 with the replica line: also time ONE stream of this config Z-slab sharded over "
+                         "the N GPUs (strong scaling, RCCL combine) as the `zslab` record")
     ap.add_argument("--replicas", type=int, default=1,
                     help="slab mode at N>1: time independent replica streams first (the fallback line)")
     ap.add_argument("--zslab-timeout", type=float, default=300.0)
@@ -254,14 +257,23 @@ CONFIGS = {  # BASELINE.json configs[1..4]: (width, height, volume dims, volume 
 
 
 def resolve(a, world):
-    """Config and mode: C2 single GPU at N=1, the C4 Z-slab stream at N>1."""
-    name = a.config if a.config != "auto" else ("c2" if world == 1 else "c4")
+    """Config and mode.  The line's workload is the metric's config (C2) at every
+    N: one stream at N=1, N independent C2 streams (one per GPU, weak scaling)
+    at N>1, so the per-N values form one curve; the Z-slab sharded stream (C4 by
+    default, `--zslab`) is timed beside it as the `zslab` record.  An explicit
+    --config c4 / c5 at N>1 makes the Z-slab stream itself the line."""
+    name = a.config if a.config != "auto" else "c2"
     W, H, n, L = CONFIGS[name]
     over = [a.width, a.height, a.dims, a.range]
     if any(v is not None for v in over):
         W, H, n, L = [v if v is not None else d for v, d in zip(over, (W, H, n, L))]
         name = "custom" if (W, H, n, L) != CONFIGS[name] else name
-    mode = a.mode if a.mode != "auto" else ("slab" if world > 1 else "single")
+    if a.mode != "auto":
+        mode = a.mode
+    elif world == 1:
+        mode = "single"
+    else:
+        mode = "slab" if a.config in ("c4", "c5") else "replicas"
     return name, W, H, n, L, mode
 
 
@@ -466,6 +478,21 @@ def main():
         timer.cancel()
     if replicas is not None and "zslab" not in out:
         out["replicas"] = replicas
+    # N>1 replica line: one Z-slab sharded stream beside it, under
+    # its own time limit, so that a failing or hung collective still leaves the line
+    if mode == "replicas" and world > 1 and a.zslab != "none":
+        def on_zslab_timeout():
+            out["zslab"] = {"error": f"timed out after {a.zslab_timeout:.0f} s"}
+            emit(out)
+            os._exit(0)
+        zt = threading.Timer(a.zslab_timeout, on_zslab_timeout)
+        zt.daemon = True
+        zt.start()
+        try:
+            out["zslab"] = zslab_record(a, intr, (bgr, dep, order), D, rank, world, local, icp_ar, (W, H, L))
+        except Exception as e:  # noqa: BLE001 -- recorded, the replica line stands
+            out["zslab"] = {"error": f"{type(e).__name__}: {e}"[:300]}
+        zt.cancel()
     # N=1: the C3 record (1024^3 @ 2 mm on the same frames) beside the C2 line
     if world == 1 and mode == "single" and a.c3_frames and name == "c2":
         import copy
@@ -494,6 +521,39 @@ def base_line(a, world, value, ms, scaling, config):
         "data": "synthetic",
         "config": config,
     }
+
+
+def zslab_record(a, intr, frames, D, rank, world, local, icp_ar, geom):
+    """ONE stream of config a.zslab, its volume Z-slab sharded over the N ranks
+    (work-balanced cuts, RCCL combine of the raycast, ICP replicated or
+    all-reduced): frames/s of the stream (strong scaling) and every rank's
+    kernel ms, integrate work and slab extent (the W/K contract of the line)."""
+    from kfx import synth
+    from kfx.abi import default_params
+    W, H, n, L = CONFIGS[a.zslab]
+    params = default_params(dims=n, range_m=L)
+    if (W, H, L) == geom:
+        zintr, zframes = intr, frames
+    else:
+        zintr = intrinsics(W, H)
+        unique = 16 if W * H > 640 * 480 else 48
+        bgr, dep, _ = synth.sequence(unique, zintr, L=L, noise=True, traj_seed=7, dropout=0.005)
+        zframes = (bgr, dep.astype(np.float32), synth.ping_pong(unique, a.warmup + a.steps))
+    kf, r = run_stream(a, zintr, params, zframes, D, local, slab=(rank, world), icp_ar=icp_ar)
+    kt = r["ktime"] or {}
+    work = kf.integrate_stats()
+    zb, zn, o0, o1 = kf.slab_info()
+    kf.close()
+    row = [kt.get("icp", float("nan")), kt.get("integrate", float("nan")), kt.get("raycast_local", float("nan")),
+           kt.get("combine", float("nan")), float(work["updated"]), float(o1 - o0), float(zn)]
+    rows = D.gather(row)
+    per_rank = [{"rank": k, "icp_ms": round(x[0], 4), "integrate_ms": round(x[1], 4), "raycast_ms": round(x[2], 4),
+                 "combine_ms": round(x[3], 4), "integrate_updated": int(x[4]), "owned_slices": int(x[5]),
+                 "stored_slices": int(x[6])} for k, x in enumerate(rows)]
+    return {"workload": workload_text(a.zslab, W, H, n, L, "slab", world, icp_ar),
+            "value": round(a.steps / r["elapsed"], 3), "unit": "frames/s", "scaling": "strong",
+            "ms_per_step": round(1000.0 * r["elapsed"] / a.steps, 4), "steps": a.steps, "warmup": a.warmup,
+            "tracked_frames": int(r["tracked"]), "per_rank": per_rank}
 
 
 def measure_main(a, name, intr, params, frames, D, rank, world, local, mode, icp_ar):

@@ -596,6 +596,12 @@ __global__ __launch_bounds__(256) void k_preprocess_maps(BilatArgs a) {
 #define KFX_ICP_PIX 4
 #endif
 constexpr int kIcpPix = KFX_ICP_PIX;
+#ifndef KFX_INT_PRIO
+#define KFX_INT_PRIO 0  // integrate: s_setprio of the first (longest) chunk's waves (A/B)
+#endif
+#ifndef KFX_RAY_PRIO
+#define KFX_RAY_PRIO 0  // raycast: raise a wave's priority after this many batches (A/B; 0 = off)
+#endif
 #ifndef KFX_EXTRACT_SKIP
 #define KFX_EXTRACT_SKIP 1  // point / mesh extraction: waves of clear bricks read nothing
 #endif
@@ -1628,6 +1634,10 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
   const unsigned item = v.iperm ? v.iperm[blockIdx.x] : blockIdx.x;  // chunk * tiles + tile
   const int tile = (int)(item % (unsigned)ntiles), chunk = (int)(item / (unsigned)ntiles);
   if (chunk >= nchunk) return;
+#if KFX_INT_PRIO
+  // the longest (first) chunks set the kernel's end: let the SIMD arbiter favour them
+  if (chunk == 0) __builtin_amdgcn_s_setprio(KFX_INT_PRIO);
+#endif
   const int x = (tile % v.tiles_x) * 8 + (lane & 7);
   const int y = (tile / v.tiles_x) * 8 + (lane >> 3);
   const size_t base = (size_t)tile * v.tile_voxels() + lane;  // this column's (x, y, zb)
@@ -2306,6 +2316,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KFX_RAY_OCC
     // after the candidate sample from the saved state — same samples, same
     // order, same result.
     bool cand = false;
+#if KFX_RAY_PRIO
+    int wave_batches = 0;  // wave-uniform
+#endif
     f3 cvert = {0.f, 0.f, 0.f}, r_nextp = nextp;
     float cts = 0.f;  // the candidate's Ts (slab payload)
     float r_rl = 0.f, r_tprev = 0.f;
@@ -2451,6 +2464,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KFX_RAY_OCC
         }
       }
       if (!__any(live)) break;
+#if KFX_RAY_PRIO
+      // waves still marching after KFX_RAY_PRIO batches are the kernel's tail:
+      // the SIMD arbiter favours them from then on
+      if (++wave_batches == KFX_RAY_PRIO) __builtin_amdgcn_s_setprio(2);
+#endif
       int16_t raw[kR];
       unsigned pm = 0u, nm = 0u, am = 0u, ownm = 0u;
       if (kStats || kTrace) st_batches += live ? 1u : 0u;
@@ -3864,7 +3882,7 @@ struct HostFetch {
   size_t bytes[2];
 };
 #ifndef KFX_FETCH_BLOCKS
-#define KFX_FETCH_BLOCKS 64  // host fetch grid (PCIe-latency bound: 64 x 256 lanes x 4 x 16 B in flight)
+#define KFX_FETCH_BLOCKS 16  // host fetch grid (PCIe-latency bound: 16 x 256 lanes x 4 x 16 B in flight; 16 beat 64 and 256 by 3 % of a host frame)
 #endif
 constexpr int kFetchUnroll = 4;
 __global__ __launch_bounds__(256) void k_host_fetch(HostFetch f) {

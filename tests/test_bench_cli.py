@@ -28,7 +28,10 @@ def args(**kw):
 def test_resolve_defaults_follow_baseline_configs():
     b = load_bench()
     assert b.resolve(args(), 1) == ("c2", 640, 480, 512, 2.048, "single")
-    assert b.resolve(args(), 8) == ("c4", 640, 480, 1024, 2.048, "slab")
+    # N>1: the metric's config on every GPU (independent streams); the Z-slab
+    # stream is the `zslab` record, or the line itself with an explicit c4 / c5
+    assert b.resolve(args(), 8) == ("c2", 640, 480, 512, 2.048, "replicas")
+    assert b.resolve(args(config="c4"), 8) == ("c4", 640, 480, 1024, 2.048, "slab")
     assert b.resolve(args(config="c5"), 8) == ("c5", 1280, 720, 2048, 4.096, "slab")
     assert b.resolve(args(config="c3"), 1) == ("c3", 640, 480, 1024, 2.048, "single")
     assert b.resolve(args(mode="replicas"), 4)[-1] == "replicas"
