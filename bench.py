@@ -480,7 +480,7 @@ def main():
         out["replicas"] = replicas
     # N>1 replica line: one Z-slab sharded stream beside it, under
     # its own time limit, so that a failing or hung collective still leaves the line
-    if mode == "replicas" and world > 1 and a.zslab != "none":
+    if mode == "replicas" and (world > 1 or a.mode == "replicas") and a.zslab != "none":
         def on_zslab_timeout():
             out["zslab"] = {"error": f"timed out after {a.zslab_timeout:.0f} s"}
             emit(out)

@@ -3882,7 +3882,7 @@ struct HostFetch {
   size_t bytes[2];
 };
 #ifndef KFX_FETCH_BLOCKS
-#define KFX_FETCH_BLOCKS 16  // host fetch grid (PCIe-latency bound: 16 x 256 lanes x 4 x 16 B in flight; 16 beat 64 and 256 by 3 % of a host frame)
+#define KFX_FETCH_BLOCKS 4  // host fetch grid (PCIe-latency bound, 4 x 256 lanes x 4 x 16 B in flight: 2.15 MB in ~0.1 ms, hidden behind the frame before it; 4 blocks beat 16 / 64 / 256 by 3-5 % of a host frame: fewer CUs taken from the frame kernels)
 #endif
 constexpr int kFetchUnroll = 4;
 __global__ __launch_bounds__(256) void k_host_fetch(HostFetch f) {
