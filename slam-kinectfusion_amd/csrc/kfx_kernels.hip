@@ -617,6 +617,9 @@ constexpr int kIcpPix = KFX_ICP_PIX;
 #ifndef KFX_ICP_SLEEP
 #define KFX_ICP_SLEEP 1  // ICP release poll: s_sleep units (64 clocks) between polls (0: busy poll)
 #endif
+#ifndef KFX_ICP_XCOARSE
+#define KFX_ICP_XCOARSE 0  // ICP: coarse levels run on the blocks of as few XCD groups (blockIdx mod 8) as fit (A/B)
+#endif
 #ifndef KFX_ICP_THREADS
 #define KFX_ICP_THREADS 256  // ICP: threads per block
 #endif
@@ -911,11 +914,16 @@ __global__ __launch_bounds__(kIcpThreads, 2) void k_icp_track(IcpPlan pl, DevSta
   int slot = 0;
   for (int l = pl.levels - 1; l >= 0 && !fail; --l) {
     const LevelGeom g = pl.g[l];
-    const bool mine = (int)blockIdx.x < pl.groups[l];
+    // blocks dealt round-robin over the 8 XCDs: with xgroups < 8 only the
+    // blocks of that many residues mod 8 (as many XCDs, under round-robin
+    // placement — speed only, the protocol is agent-scope either way) work
+    const int nx = pl.xgroups[l];
+    const int prank = nx >= 8 ? (int)blockIdx.x : (int)(blockIdx.x / 8) * nx + (int)(blockIdx.x % 8);
+    const bool mine = (nx >= 8 || (int)(blockIdx.x % 8) < nx) && prank < pl.groups[l];
     f3 n0[kIcpPix], v0[kIcpPix];
     bool ok[kIcpPix];
     if (mine)
-      icp_load_cur(g, pl.xe[l], pl.npix[l], KFX_ICP_XCD ? xcd_remap(blockIdx.x, pl.groups[l]) : (int)blockIdx.x,
+      icp_load_cur(g, pl.xe[l], pl.npix[l], nx < 8 ? prank : (KFX_ICP_XCD ? xcd_remap(blockIdx.x, pl.groups[l]) : (int)blockIdx.x),
                    pl.ppl[l], pl.cv[l], pl.cn[l], n0, v0, ok);
     for (int it = 0; it < pl.iters[l] && !fail; ++it, ++slot) {
       unsigned long long *sh = sy->sums + (size_t)slot * kIcpShards * 27;
@@ -933,7 +941,7 @@ __global__ __launch_bounds__(kIcpThreads, 2) void k_icp_track(IcpPlan pl, DevSta
         if (tr && blockIdx.x == 0) sy->trace[slot][9] = wall_clock64() + (bsum == -7 ? 1 : 0);
         if (threadIdx.x < 64) {
           if (threadIdx.x < 27)
-            __hip_atomic_fetch_add(&sh[(blockIdx.x % kIcpShards) * 27 + threadIdx.x],
+            __hip_atomic_fetch_add(&sh[(prank % kIcpShards) * 27 + threadIdx.x],
                                    (unsigned long long)bsum, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
           // the partial adds are device-scope atomics (performed past the
@@ -3421,6 +3429,7 @@ IcpPlan make_icp_plan(int levels, const LevelGeom *g, const int *iters, FrameVie
     // CU (256), so coarse levels spread over more waves (shorter lane phase)
     pl.ppl[l] = std::max(1, std::min(kIcpPix, (pl.npix[l] + KFX_ICP_PPLCAP * kIcpThreads - 1) / (KFX_ICP_PPLCAP * kIcpThreads)));
     pl.groups[l] = std::max(1, (pl.npix[l] + kIcpThreads * pl.ppl[l] - 1) / (kIcpThreads * pl.ppl[l]));
+    pl.xgroups[l] = 8;
     pl.iters[l] = iters[l];
     pl.cv[l] = cur.v[l];
     pl.cn[l] = cur.n[l];
@@ -3430,6 +3439,26 @@ IcpPlan make_icp_plan(int levels, const LevelGeom *g, const int *iters, FrameVie
     pl.slots += iters[l];
   }
   pl.nblocks = std::max(pl.nblocks, 1);
+#if KFX_ICP_XCOARSE
+  // coarse levels on the fewest XCD groups whose blocks hold them at their
+  // pixels per lane (KFX_ICP_XCOARSE = 1: level 2 only, 2: levels 2 and 1)
+  const int per_group = (pl.nblocks + 7) / 8;  // blocks of one residue mod 8
+  for (int l = std::max(1, levels - KFX_ICP_XCOARSE); l < levels; ++l) {
+    int ppl = pl.ppl[l], gr = pl.groups[l];
+    int nx = (gr + per_group - 1) / per_group;
+    const int nx_max = l == levels - 1 ? 1 : 2;  // the coarsest level on one XCD, the next on two
+    while (nx > nx_max && ppl < kIcpPix) {  // more pixels per lane until it fits
+      ++ppl;
+      gr = (pl.npix[l] + kIcpThreads * ppl - 1) / (kIcpThreads * ppl);
+      nx = (gr + per_group - 1) / per_group;
+    }
+    if (nx < 8) {
+      pl.ppl[l] = ppl;
+      pl.groups[l] = gr;
+      pl.xgroups[l] = nx;
+    }
+  }
+#endif
   return pl;
 }
 
