@@ -596,6 +596,9 @@ __global__ __launch_bounds__(256) void k_preprocess_maps(BilatArgs a) {
 #define KFX_ICP_PIX 4
 #endif
 constexpr int kIcpPix = KFX_ICP_PIX;
+#ifndef KFX_INT_LEAN
+#define KFX_INT_LEAN 0  // integrate (A/B bits): 1 unconditional tsdf store of updated voxels, 2 negative marks after the batch
+#endif
 #ifndef KFX_INT_PRIO
 #define KFX_INT_PRIO 0  // integrate: s_setprio of the first (longest) chunk's waves (A/B)
 #endif
@@ -1974,6 +1977,9 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
 #endif
     }
     iz += (Idx)kB * slice;
+#if KFX_INT_LEAN & 2
+    unsigned negm = 0u;  // voxels of this batch written with a negative tsdf
+#endif
 #pragma unroll
     for (int j = 0; j < kB; ++j) {
       // saturated free space (w = 64 at the tsdf fixed point T* of a ts = 1
@@ -1988,6 +1994,9 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
       const float new_t = div_rn(fmaf(pre_t, (float)pre_w, ts), (float)(pre_w + 1), rtab[pre_w + 1]);
       int q = (int)(new_t * (float)kShortMax);
       q = max(-kShortMax, min(kShortMax, q));
+#if KFX_INT_LEAN & 2
+      negm |= q < 0 ? 1u << j : 0u;  // marked after the batch (rare)
+#else
       if (q < 0) {
         const int k = ((z + j) >> 3) - gbs;
         if (k < 62) {
@@ -1997,10 +2006,15 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
           nhi = max(nhi, z + j);
         }
       }
+#endif
       // saturated voxels (w = 64 at a tsdf fixed point) keep their values:
       // skipping those stores changes nothing and saves write bandwidth
 #if KFX_INT_EXP != 3  // 3: timing experiment only (wrong values): no tsdf/weight stores
+#if KFX_INT_LEAN & 1
+      mem.st_t(i, (int16_t)q);  // (an unchanged value rewritten: no compare, no branch)
+#else
       if (q != t0[j]) mem.st_t(i, (int16_t)q);
+#endif
       if (new_w != pre_w) mem.st_w(i, (int16_t)new_w);
 #endif
       if (sdf[j] <= thres_color && sdf[j] >= -thres_color) {  // colour band (rare)
@@ -2018,6 +2032,21 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
         if (out != c0) mem.st_c(i, out);
       }
     }
+#if KFX_INT_LEAN & 2
+    if (negm) {  // (rare) the occupancy marks of the negative voxels
+#pragma unroll
+      for (int j = 0; j < kB; ++j)
+        if ((negm >> j) & 1u) {
+          const int k = ((z + j) >> 3) - gbs;
+          if (k < 62) {
+            nbm |= 1ull << k;
+          } else {
+            nlo = min(nlo, z + j);
+            nhi = max(nhi, z + j);
+          }
+        }
+    }
+#endif
   }
   if (!kCount) {  // raycast skip maps
 #pragma unroll
