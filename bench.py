@@ -72,6 +72,8 @@ def parse():
                     help="integrate PMC traffic record; attached only when it was measured on this command's "
                          "workload and step counts with the same libkfx.so (sha256)")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--graph-full", action="store_true",
+                    help="overlapped frames also replay ICP/integrate/raycast as a graph (kfx_set_graph_mode 2)")
     ap.add_argument("--sample-every", type=int, default=8,
                     help="time kernels on every k-th timed frame with HIP events (0 = off)")
     ap.add_argument("--no-overlap", action="store_true",
@@ -256,6 +258,18 @@ CONFIGS = {  # BASELINE.json configs[1..4]: (width, height, volume dims, volume 
 }
 
 
+def graph_parts(a, mode):
+    """The part of each timed frame replayed as a captured graph."""
+    if a.no_graph:
+        return "none (eager)"
+    if a.no_overlap:
+        return "whole frame (single stream)"
+    if mode == "slab":
+        return "none (overlapped slab frames launch eagerly)"
+    return ("pyrDown+preprocess graph and ICP+integrate+raycast graph" if a.graph_full else
+            "pyrDown+preprocess graph; ICP, integrate, raycast eager")
+
+
 def resolve(a, world):
     """Config and mode.  The line's workload is the metric's config (C2) at every
     N: one stream at N=1, N independent C2 streams (one per GPU, weak scaling)
@@ -303,7 +317,7 @@ def run_stream(a, intr, params, frames, D, local, slab=None, icp_ar=False, timin
     if slab is not None:
         kf.comm_init(D.bcast_bytes(kfx.comm_unique_id() if slab[0] == 0 else None))
         kf.set_icp_allreduce(icp_ar)
-    kf.set_graph_mode(not a.no_graph)
+    kf.set_graph_mode(0 if a.no_graph else (2 if a.graph_full else 1))
     kf.set_frame_overlap(not a.no_overlap)
     kf.stage_frames(bgr, dep)
     for i in range(a.warmup):
@@ -581,6 +595,8 @@ def measure_main(a, name, intr, params, frames, D, rank, world, local, mode, icp
         kf.register_host_buffer(hb)
         kf.register_host_buffer(hd)
         ho = synth.ping_pong(unique, a.host_frames)
+        for i in ho[:8]:  # untimed: every ring slot used once (its graphs captured)
+            kf.pipeline_async(hb[i], hd[i])
         kf.synchronize()
         D.barrier()
         t0 = time.perf_counter()
@@ -691,8 +707,9 @@ def measure_main(a, name, intr, params, frames, D, rank, world, local, mode, icp
         "workload": workload_text(name, W, H, n, L, mode, world, icp_ar),
         "width": W, "height": H, "volume_dims": n, "volume_range_m": L,
         "frames_unique": len(bgr),
-        # staged frames with overlap launch eagerly on two streams; graphs only without it
-        "graph": (not a.no_graph) and a.no_overlap, "overlap": not a.no_overlap,
+        # what the timed frames replay as graphs (kfx_set_graph_mode); the few
+        # stage-timing sample frames launch eagerly with their events
+        "graph": graph_parts(a, mode), "overlap": not a.no_overlap,
         "parallelism": (f"zslab x{world}" + (" + icp allreduce" if icp_ar else "") if mode == "slab" else
                         (f"replicas x{world} (independent streams)" if world > 1 else "single")),
         "tracked_frames": int(tracked),

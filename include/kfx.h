@@ -127,7 +127,13 @@ int kfx_pipeline_async_u16(kfx_ctx *ctx, const uint8_t *bgr, const uint16_t *dep
  * pending uploads).  kfx_destroy unregisters what is left. */
 int kfx_register_host_buffer(kfx_ctx *ctx, void *ptr, size_t bytes);
 int kfx_unregister_host_buffer(kfx_ctx *ctx, void *ptr);
-/* Use a captured hipGraph for the per-frame launch sequence (default on). */
+/* Captured hipGraphs for the per-frame launch sequence: 0 eager launches;
+ * 1 (default) single-stream frames replay one graph per input, overlapped
+ * staged / async frames replay their pyrDown + preprocess as a graph and
+ * launch ICP, integrate and raycast eagerly; 2 as 1, and overlapped frames
+ * also replay ICP + integrate + raycast as a second graph (measured slower,
+ * DESIGN.md §3).  Z-slab and group frames always launch eagerly when
+ * overlapped.  Results are identical in every mode. */
 int kfx_set_graph_mode(kfx_ctx *ctx, int enabled);
 /* Overlap each staged frame's preprocess with the previous frame's tracking on
  * a second stream, over double-buffered frame maps (default on; staged frames

@@ -144,6 +144,11 @@ struct kfx_ctx {
   bool profiling = false;
   hipGraphExec_t graph[2] = {nullptr, nullptr};  // [u16 input], inputs in raw[0]/bgr
   std::vector<hipGraphExec_t> staged_graph;       // one per staged frame (reads it in place)
+  // overlapped staged frames: per staged frame and buffer set p, [4i+2p] the
+  // pyrDown/preprocess graph (pstream), [4i+2p+1] the ICP/integrate/raycast graph
+  std::vector<hipGraphExec_t> ov_graph;
+  bool ov_graph_full = false;  // also capture ICP/integrate/raycast (kfx_set_graph_mode 2)
+  bool cap_ext = false;        // capturing: the ev_icp record becomes an event-record node
   const uint8_t *last_bgr = nullptr;              // colour the last frame integrated
   hipEvent_t ev[kStageEvents]{};  // stage events; [5]: local raycast done, [6]: combine starts (slabs)
   float stage_ms[5]{};
@@ -166,6 +171,7 @@ struct kfx_ctx {
   size_t ring_slot = 0;  // bytes per slot: f32 depth + BGR8
   hipEvent_t ring_h2d[kRing]{}, ring_done[kRing]{};
   bool ring_used[kRing]{};
+  hipGraphExec_t ring_graph[kRing][2][4]{};  // overlapped-frame graphs per slot and [u16 input]
   int ring_next = 0;
   bool ring_ready = false;  // every ring resource above created
   struct HostReg {
@@ -228,6 +234,18 @@ void destroy_graphs(kfx_ctx *c) {
       (void)hipGraphExecDestroy(gx);
       gx = nullptr;
     }
+  for (auto &slot : c->ring_graph)
+    for (auto &gs : slot)
+      for (auto &gx : gs)
+        if (gx) {
+          (void)hipGraphExecDestroy(gx);
+          gx = nullptr;
+        }
+  for (auto &gx : c->ov_graph)
+    if (gx) {
+      (void)hipGraphExecDestroy(gx);
+      gx = nullptr;
+    }
 }
 
 // Frame input: depth (f32 mm, or u16 mm) and BGR8 colour, in device memory;
@@ -240,6 +258,27 @@ struct FrameInput {
   hipEvent_t ready = nullptr;
   hipEvent_t done = nullptr;
 };
+
+// ev_icp behind the ICP just enqueued on s.  While a graph is being captured
+// (cap_ext) the record is added as an event-record node on the captured ICP,
+// so every replay records the event for the next frame's preprocess.
+int record_icp_event(kfx_ctx *c, hipStream_t s) {
+  if (!c->cap_ext) {
+    HIPCHK(hipEventRecord(c->ev_icp, s));
+    return KFX_OK;
+  }
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  unsigned long long id = 0;
+  hipGraph_t g = nullptr;
+  const hipGraphNode_t *deps = nullptr;
+  size_t nd = 0;
+  HIPCHK(hipStreamGetCaptureInfo_v2(s, &cs, &id, &g, &deps, &nd));
+  if (cs != hipStreamCaptureStatusActive || !g) return set_err(KFX_ERR_HIP, "ev_icp record: stream not capturing");
+  hipGraphNode_t node = nullptr;
+  HIPCHK(hipGraphAddEventRecordNode(&node, g, deps, nd, c->ev_icp));
+  HIPCHK(hipStreamUpdateCaptureDependencies(s, &node, 1, hipStreamSetCaptureDependencies));
+  return KFX_OK;
+}
 
 // The per-frame launch sequence (kinectfusion.cpp:78-127 with the frame-1 and
 // failure branches resolved on the device).  `ev` (or null) receives the stage
@@ -374,7 +413,7 @@ int enqueue_track(kfx_ctx *c, FrameInput in, hipEvent_t *ev, bool begin) {
   if (ev) (void)hipEventRecord(ev[2], s);
   // overlapped frames: the next preprocess waits here; a group: the next
   // member's ICP on this device waits here
-  if (begin || c->group_chain) (void)hipEventRecord(c->ev_icp, s);
+  if ((begin || c->group_chain) && !r && (r = record_icp_event(c, s))) return r;
   enqueue_map(c, in, ev);
   return r;
 }
@@ -386,17 +425,9 @@ int enqueue_track(kfx_ctx *c, FrameInput in, hipEvent_t *ev, bool begin) {
 // cross-stream dependencies: ~9 us/frame for the wait on ev_prep, while
 // dropping the ev_free ordering (unsafe) is slower, as preprocess then
 // competes with integrate/raycast.
-int enqueue_frame_overlap(kfx_ctx *c, FrameInput in, hipEvent_t *ev) {
-  const int p = c->par ^ 1;
-  set_par(c, p);
+// pyrDown + preprocess of an overlapped frame into the current set, on pstream.
+void enqueue_prep_overlap(kfx_ctx *c, FrameInput in) {
   hipStream_t b = c->pstream;
-  HIPCHK(hipStreamWaitEvent(b, c->ev_free[p], 0));  // the frame before last is done with set p
-  if (in.ready) HIPCHK(hipStreamWaitEvent(b, in.ready, 0));  // host input uploaded
-#if KFX_PREP_AFTER_ICP
-  // start behind the previous frame's ICP: the latency-bound persistent ICP
-  // then runs alone and the preprocess shares the GPU with integrate/raycast
-  HIPCHK(hipStreamWaitEvent(b, c->ev_icp, 0));
-#endif
   const float *raw[kMaxLevels];
   for (int l = 0; l < kMaxLevels; ++l) raw[l] = c->raw[l];
   raw[0] = in.d32;
@@ -411,24 +442,52 @@ int enqueue_frame_overlap(kfx_ctx *c, FrameInput in, hipEvent_t *ev) {
   launch_preprocess_maps(b, c->L, raw, in.d16, c->g, c->cur, c->p.bfilter_kernel_size,
                          c->p.bfilter_color_sigma, c->p.bfilter_spatial_sigma, c->p.dfilter_dist,
                          c->inv_lambda, c->dl0);
-  HIPCHK(hipEventRecord(c->ev_prep, b));
-  HIPCHK(hipStreamWaitEvent(c->stream, c->ev_prep, 0));
+}
+
+// ICP (frame_begin folded in) + integrate + raycast (+ slab combine) of an
+// overlapped frame, on the frame stream.
+int enqueue_main_overlap(kfx_ctx *c, FrameInput in, hipEvent_t *ev) {
   if (ev) HIPCHK(hipEventRecord(ev[1], c->stream));
   int r = enqueue_track(c, in, ev, true);
   if (ev) HIPCHK(hipEventRecord(ev[5], c->stream));
   if (ev) HIPCHK(hipEventRecord(ev[6], c->stream));
   if (!r && c->slab) r = enqueue_combine(c);
   if (ev) HIPCHK(hipEventRecord(ev[4], c->stream));
+  return r;
+}
+
+// gx (optional): this frame's two captured graphs for the set it uses
+// (ensure_ov_graphs), replayed in place of the eager launches; the cross-frame
+// and cross-stream event waits stay around them.
+int enqueue_frame_overlap(kfx_ctx *c, FrameInput in, hipEvent_t *ev, hipGraphExec_t *gx) {
+  const int p = c->par ^ 1;
+  set_par(c, p);
+  hipStream_t b = c->pstream;
+  HIPCHK(hipStreamWaitEvent(b, c->ev_free[p], 0));  // the frame before last is done with set p
+  if (in.ready) HIPCHK(hipStreamWaitEvent(b, in.ready, 0));  // host input uploaded
+#if KFX_PREP_AFTER_ICP
+  // start behind the previous frame's ICP: the latency-bound persistent ICP
+  // then runs alone and the preprocess shares the GPU with integrate/raycast
+  HIPCHK(hipStreamWaitEvent(b, c->ev_icp, 0));
+#endif
+  if (gx) HIPCHK(hipGraphLaunch(gx[0], b));
+  else enqueue_prep_overlap(c, in);
+  HIPCHK(hipEventRecord(c->ev_prep, b));
+  HIPCHK(hipStreamWaitEvent(c->stream, c->ev_prep, 0));
+  int r = KFX_OK;
+  if (gx && gx[1]) HIPCHK(hipGraphLaunch(gx[1], c->stream));
+  else r = enqueue_main_overlap(c, in, ev);
   HIPCHK(hipEventRecord(c->ev_free[p], c->stream));
   if (in.done) HIPCHK(hipEventRecord(in.done, c->stream));
   return r;
 }
 
-int build_graph(kfx_ctx *c, FrameInput in, hipGraphExec_t *out) {
+template <typename F>
+int capture_graph(kfx_ctx *c, hipStream_t s, F &&body, hipGraphExec_t *out) {
   hipGraph_t graph = nullptr;
-  HIPCHK(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-  const int r = enqueue_frame(c, in, nullptr);
-  const hipError_t ec = hipStreamEndCapture(c->stream, &graph);
+  HIPCHK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+  const int r = body();
+  const hipError_t ec = hipStreamEndCapture(s, &graph);
   if (r) {
     if (graph) (void)hipGraphDestroy(graph);
     return r;
@@ -437,7 +496,43 @@ int build_graph(kfx_ctx *c, FrameInput in, hipGraphExec_t *out) {
   hipError_t e = hipGraphInstantiate(out, graph, nullptr, nullptr, 0);
   (void)hipGraphDestroy(graph);
   if (e != hipSuccess) return set_err(KFX_ERR_HIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(e));
+  // upload now: a graph's first launch otherwise pays for it (staged frames'
+  // graphs are each launched only a few times)
+  HIPCHK(hipGraphUpload(*out, s));
   return KFX_OK;
+}
+
+// Overlapped frames replay graphs when they run on one device without slab
+// exchange or group chaining (those keep their eager launches).
+bool ov_graphs_apply(const kfx_ctx *c) {
+  return c->graph_mode && !c->slab && !c->comm && !c->group_chain && !c->icp_sharded;
+}
+
+// The graphs of an overlapped frame for buffer set p: gx[0] pyrDown +
+// preprocess (replayed on pstream) and, with kfx_set_graph_mode(ctx, 2),
+// gx[1] ICP + integrate + raycast (on the frame stream; its ev_icp record is
+// an event-record node, so the next frame's preprocess still starts behind
+// this frame's ICP).  gx[1] is off by default: its replay measured 4-6 us per
+// frame slower than the eager launches of the same three kernels (the graph
+// uploaded beforehand), while the preprocess graph is neutral to slightly
+// faster.
+int ensure_ov_graphs(kfx_ctx *c, FrameInput in, hipGraphExec_t *gx, int p) {
+  if (gx[0] && (gx[1] || !c->ov_graph_full)) return KFX_OK;
+  const int keep = c->par;
+  set_par(c, p);
+  int r = gx[0] ? KFX_OK
+                : capture_graph(c, c->pstream, [&] { enqueue_prep_overlap(c, in); return KFX_OK; }, &gx[0]);
+  if (!r && !gx[1] && c->ov_graph_full) {
+    c->cap_ext = true;
+    r = capture_graph(c, c->stream, [&] { return enqueue_main_overlap(c, in, nullptr); }, &gx[1]);
+    c->cap_ext = false;
+  }
+  set_par(c, keep);
+  return r;
+}
+
+int build_graph(kfx_ctx *c, FrameInput in, hipGraphExec_t *out) {
+  return capture_graph(c, c->stream, [&] { return enqueue_frame(c, in, nullptr); }, out);
 }
 
 int read_state(kfx_ctx *c, DevState *out) {
@@ -507,13 +602,21 @@ hipEvent_t *timing_sample(kfx_ctx *c) {
 
 // graph: the cached executable for this input (built on first use), or null
 // overlap: the input stays valid until the frame completes (staged frames)
-int run_frame(kfx_ctx *c, FrameInput in, hipGraphExec_t *graph, bool overlap = false) {
+// ovg: the input's four overlapped-frame graphs (ensure_ov_graphs, two per
+// buffer set), or null for eager overlapped launches
+int run_frame(kfx_ctx *c, FrameInput in, hipGraphExec_t *graph, bool overlap = false,
+              hipGraphExec_t *ovg = nullptr) {
   int r = ensure_pose_capacity(c, 1);
   if (r) return r;
   c->last_bgr = in.bgr;
   hipEvent_t *tev = timing_sample(c);  // this frame's timing sample, if sampled
   if (overlap && c->overlap && !c->profiling) {
-    if ((r = enqueue_frame_overlap(c, in, tev))) return r;
+    hipGraphExec_t *gx = nullptr;
+    if (ovg && !tev && ov_graphs_apply(c)) {  // a timing sample launches eagerly with its events
+      gx = ovg + 2 * (c->par ^ 1);
+      if ((r = ensure_ov_graphs(c, in, gx, c->par ^ 1))) return r;
+    }
+    if ((r = enqueue_frame_overlap(c, in, tev, gx))) return r;
     HIPCHK(hipGetLastError());
     c->pending += 1;
     return KFX_OK;
@@ -1068,7 +1171,7 @@ static int pipeline_async(kfx_ctx *c, const uint8_t *bgr, const void *depth, boo
   FrameInput in{u16 ? c->raw[0] : (const float *)ds, u16 ? (const uint16_t *)ds : nullptr, ds + np * 4};
   in.ready = c->ring_h2d[k];
   in.done = c->ring_done[k];
-  return run_frame(c, in, nullptr, true);
+  return run_frame(c, in, nullptr, true, c->ring_graph[k][u16 ? 1 : 0]);
 }
 
 int kfx_pipeline_async(kfx_ctx *c, const uint8_t *bgr, const float *depth_mm) {
@@ -1095,6 +1198,7 @@ int kfx_stage_frames(kfx_ctx *c, int n, const uint8_t *bgr, const float *depth_m
   c->n_staged = 0;
   destroy_graphs(c);
   c->staged_graph.assign(n, nullptr);
+  c->ov_graph.assign(4 * (size_t)n, nullptr);
   if ((r = dalloc(c, (void **)&c->staged_depth, np * 4 * (size_t)n))) return r;
   if ((r = dalloc(c, (void **)&c->staged_bgr, np * 3 * (size_t)n))) return r;
   HIPCHK(hipMemcpyAsync(c->staged_depth, depth_mm, np * 4 * (size_t)n, hipMemcpyHostToDevice,
@@ -1102,12 +1206,15 @@ int kfx_stage_frames(kfx_ctx *c, int n, const uint8_t *bgr, const float *depth_m
   HIPCHK(hipMemcpyAsync(c->staged_bgr, bgr, np * 3 * (size_t)n, hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   c->n_staged = n;
-  // capture every staged frame's graph now, outside any timed frame loop
-  // (overlapped frames launch eagerly on two streams and need none)
-  for (int i = 0; i < n && !c->overlap; ++i)
-    if ((r = ensure_graph(c, {c->staged_depth + np * i, nullptr, c->staged_bgr + np * 3 * i},
-                          &c->staged_graph[i])))
-      return r;
+  // capture every staged frame's graphs now, outside any timed frame loop
+  // (overlapped frames: two per buffer set)
+  for (int i = 0; i < n; ++i) {
+    const FrameInput in{c->staged_depth + np * i, nullptr, c->staged_bgr + np * 3 * i};
+    if (!c->overlap) r = ensure_graph(c, in, &c->staged_graph[i]);
+    else if (ov_graphs_apply(c))
+      for (int p = 0; p < 2 && !r; ++p) r = ensure_ov_graphs(c, in, &c->ov_graph[4 * i + 2 * p], p);
+    if (r) return r;
+  }
   return KFX_OK;
 }
 
@@ -1118,7 +1225,7 @@ int kfx_pipeline_staged(kfx_ctx *c, int idx) {
   const size_t np = (size_t)c->intr.width * c->intr.height;
   // the captured graph for this staged frame reads it in place (no copy)
   return run_frame(c, {c->staged_depth + np * idx, nullptr, c->staged_bgr + np * 3 * idx},
-                   &c->staged_graph[idx], true);
+                   &c->staged_graph[idx], true, &c->ov_graph[4 * (size_t)idx]);
 }
 
 int kfx_synchronize(kfx_ctx *c) {
@@ -1199,7 +1306,14 @@ int kfx_get_kernel_timing(kfx_ctx *c, float out_ms[3], int *n_samples) {
 
 int kfx_set_graph_mode(kfx_ctx *c, int enabled) {
   if (!c) return set_err(KFX_ERR_ARG, "null context");
+  if (enabled < 0 || enabled > 2) return set_err(KFX_ERR_ARG, "graph mode is 0, 1 or 2");
   c->graph_mode = enabled != 0;
+  if (c->ov_graph_full != (enabled == 2)) {
+    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipStreamSynchronize(c->pstream));
+    destroy_graphs(c);
+    c->ov_graph_full = enabled == 2;
+  }
   return KFX_OK;
 }
 

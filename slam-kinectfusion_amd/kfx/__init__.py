@@ -399,8 +399,10 @@ class KinectFusion:
         frames completed since the last status check was dropped (reset)."""
         return _check(lib().kfx_synchronize(self._h), "kfx_synchronize", ok=(KFX_OK, KFX_TRACKING_LOST))
 
-    def set_graph_mode(self, on: bool):
-        _check(lib().kfx_set_graph_mode(self._h, int(on)), "kfx_set_graph_mode")
+    def set_graph_mode(self, mode):
+        """0/False eager, 1/True (default) graphs, 2 overlapped frames also
+        replay ICP + integrate + raycast as a graph (kfx.h kfx_set_graph_mode)."""
+        _check(lib().kfx_set_graph_mode(self._h, int(mode)), "kfx_set_graph_mode")
 
     def set_kernel_timing(self, every: int, max_samples: int = 1024):
         """Bracket every `every`-th pipelined frame with HIP events (0 = off)."""

@@ -285,18 +285,22 @@ def test_pipeline_matches_oracle(which, seq_qvga, seq_vga):
 
 
 def test_pipeline_modes_and_inputs_identical(seq_qvga):
-    """graph / eager / profiled launches, u16 / f32 / staged inputs and the
-    persistent vs per-iteration ICP launches all give the same poses and volume."""
+    """graph / eager / profiled launches, u16 / f32 / staged inputs (overlapped
+    staged frames replayed as graphs or launched eagerly) and the persistent vs
+    per-iteration ICP launches all give the same poses and volume."""
     bgr, dep, gt = seq_qvga
     intr = synth.Intrinsics.qvga()
     res = []
-    for mode in ("graph", "eager", "profile", "u16", "staged", "staged_graph", "staged_mixed",
-                 "staged_per_iter", "icp_per_iter", "icp_coop", "staged_coop"):
+    for mode in ("graph", "eager", "profile", "u16", "staged", "staged_eager", "staged_full",
+                 "staged_graph", "staged_mixed", "staged_per_iter", "icp_per_iter", "icp_coop",
+                 "staged_coop"):
         kf, p = make(intr, dims=64)
         if mode == "staged_graph":  # staged frames without the two-stream overlap
             kf.set_frame_overlap(False)
-        if mode == "eager":
+        if mode in ("eager", "staged_eager"):  # staged_eager: overlapped frames launched eagerly
             kf.set_graph_mode(False)
+        if mode == "staged_full":  # overlapped frames: ICP/integrate/raycast replayed as a graph too
+            kf.set_graph_mode(2)
         if mode in ("icp_per_iter", "staged_per_iter"):
             assert kf.set_icp_persistent(False)  # persistent path was the one in use
             kf.set_graph_mode(False)
@@ -304,7 +308,8 @@ def test_pipeline_modes_and_inputs_identical(seq_qvga):
             assert kf.set_icp_persistent(2)
         if mode == "profile":
             kf.set_profiling(True)
-        if mode in ("staged", "staged_graph", "staged_per_iter", "staged_coop"):
+        if mode in ("staged", "staged_eager", "staged_full", "staged_graph", "staged_per_iter",
+                    "staged_coop"):
             kf.stage_frames(bgr, dep.astype(np.float32))
             for k in range(len(dep)):
                 kf.pipeline_staged(k)
