@@ -582,7 +582,26 @@ def measure_main(a, name, intr, params, frames, D, rank, world, local, mode, icp
     elapsed, ktime, tracked = r["elapsed"], r["ktime"], r["tracked"]
     ms_source = (f"timed region, {ktime['samples']} HIP-event-bracketed frames" if ktime else "profiled frames")
 
-    # host-input throughput (not `value`): the same frames from host memory
+    # per-stage device ms on further frames (profiled, eager; single volume)
+    stages = {k: [] for k in ("preprocess", "icp", "integrate", "raycast", "total")}
+    int_ms, int_work = [], []
+    nprof = a.profile_frames if mode != "slab" else 0
+    if nprof:
+        kf.set_profiling(True)
+        for i in range(a.warmup + a.steps, a.warmup + a.steps + nprof):
+            kf.pipeline_staged(order[i])
+            ms = kf.stage_ms()
+            for k in stages:
+                stages[k].append(ms[k])
+            int_work.append(kf.integrate_stats())
+            int_ms.append(ms["integrate"])
+        kf.set_profiling(False)
+    else:
+        int_work.append(kf.integrate_stats())  # the last timed frame's integrate work
+    ray_work = kf.raycast_stats() if nprof else None
+    # host-input throughput (not `value`; after the profiled frames, so that their
+    # integrate work, the roofline's bytes, follows the timed frames directly): the
+    # same frames from host memory
     # through kfx_pipeline_async (pinned ring, H2D overlapped with the previous
     # frame), PCIe included, f32 depth as the reference's pipeline() takes it
     host_in = None
@@ -614,23 +633,6 @@ def measure_main(a, name, intr, params, frames, D, rank, world, local, mode, icp
                            "H2D straight from the caller's page-locked frames on a copy stream, overlapped with "
                            "the previous frame (no host copy); f32 depth mm + BGR8"}
 
-    # per-stage device ms on further frames (profiled, eager; single volume)
-    stages = {k: [] for k in ("preprocess", "icp", "integrate", "raycast", "total")}
-    int_ms, int_work = [], []
-    nprof = a.profile_frames if mode != "slab" else 0
-    if nprof:
-        kf.set_profiling(True)
-        for i in range(a.warmup + a.steps, a.warmup + a.steps + nprof):
-            kf.pipeline_staged(order[i])
-            ms = kf.stage_ms()
-            for k in stages:
-                stages[k].append(ms[k])
-            int_work.append(kf.integrate_stats())
-            int_ms.append(ms["integrate"])
-        kf.set_profiling(False)
-    else:
-        int_work.append(kf.integrate_stats())  # the last timed frame's integrate work
-    ray_work = kf.raycast_stats() if nprof else None
     extract = extract_record(kf, n) if (mode == "single" and a.extract) else None
     zb, zn, o0, o1 = kf.slab_info()
     kf.synchronize()
