@@ -300,6 +300,8 @@ def test_pipeline_modes_and_inputs_identical(seq_qvga):
         if mode in ("eager", "staged_eager"):  # staged_eager: overlapped frames launched eagerly
             kf.set_graph_mode(False)
         if mode == "staged_full":  # overlapped frames: ICP/integrate/raycast replayed as a graph too
+            with pytest.raises(KfxError):
+                kf.set_graph_mode(3)  # modes are 0, 1, 2
             kf.set_graph_mode(2)
         if mode in ("icp_per_iter", "staged_per_iter"):
             assert kf.set_icp_persistent(False)  # persistent path was the one in use
