@@ -419,7 +419,8 @@ def test_staged_tracking_failure_reported_by_synchronize(seq_qvga):
 def test_async_host_input_matches_staged(u16, seq_qvga):
     """kfx_pipeline_async (pinned ring + H2D on a copy stream, no per-frame host
     sync; more frames than ring slots, a dropped frame among them) gives the
-    staged path's poses and volume bit for bit, and reports the drop once."""
+    staged path's poses and volume bit for bit, and reports the drop once; with
+    graph modes 1, 2 and 0 on the ring, registered and odd-address inputs."""
     bgr, dep, gt = seq_qvga
     intr = synth.Intrinsics.qvga()
     frames = dep.astype(np.uint16 if u16 else np.float32).copy()
@@ -431,6 +432,7 @@ def test_async_host_input_matches_staged(u16, seq_qvga):
     assert kf.synchronize() == KFX_OK
     # zero copy: the same frames uploaded straight from registered host buffers
     zc, _ = make(intr, dims=64)
+    zc.set_graph_mode(2)  # the ring slots' frames replay both graphs (kf: preprocess graph)
     hb = np.ascontiguousarray(bgr)
     zc.register_host_buffer(hb)
     zc.register_host_buffer(frames)
@@ -445,6 +447,7 @@ def test_async_host_input_matches_staged(u16, seq_qvga):
     hu = raw[3:3 + hb.nbytes].reshape(hb.shape)
     hu[...] = hb
     un, _ = make(intr, dims=64)
+    un.set_graph_mode(0)  # eager launches
     fu = frames.copy()  # (a page range is registered by one context at a time)
     un.register_host_buffer(hu)
     un.register_host_buffer(fu)
