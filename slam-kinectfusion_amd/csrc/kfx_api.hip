@@ -1008,8 +1008,9 @@ static int create_impl(const kfx_intrinsics *intr, const kfx_params *params, int
   for (int b = 0; b < 2; ++b)
     c->planb[b] = make_icp_plan(c->L, c->g, c->p.icp_iter_count, c->curb[b], c->prev,
                                 c->p.icp_dist_threshold, c->angle_thr);
+  // (both sets: the fit may cap nblocks and select the strided kernel)
+  c->icp_persistent = icp_persistent_ok(c->planb[0], c->device) && icp_persistent_ok(c->planb[1], c->device);
   set_par(c, 0);
-  c->icp_persistent = icp_persistent_ok(c->icp_plan, c->device);
   if ((r = dalloc(c, (void **)&c->counters, sizeof(unsigned long long) * 128))) return fail(r);
   if ((r = dalloc(c, (void **)&c->xpose, sizeof(float) * 32))) return fail(r);
   launch_inv_lambda(c->stream, c->g[0], c->inv_lambda);

@@ -59,7 +59,11 @@ struct IcpPlan {
   int xgroups[kMaxLevels];  // 8, or the block residues mod 8 (XCD groups) taking part at that level
   const float *cv[kMaxLevels], *cn[kMaxLevels], *pv[kMaxLevels], *pn[kMaxLevels];
   float dist2_max, sine2_max;  // sqrt_le_bound of the distance / sine thresholds
+  // 1: nblocks (co-resident) is below some level's groups; block b also takes
+  // groups b + k * nblocks (k_icp_track<true>), at most kIcpStrideMax per block
+  int stride;
 };
+constexpr int kIcpStrideMax = 16;
 
 // Device workspace of the persistent ICP kernel; zero between launches
 // (the kernel's last block restores that).
@@ -202,7 +206,7 @@ int icp_blocks(const LevelGeom &g);
 // single launch; shards = 8 x 27 int64 zeroed, ticket zeroed (both self-reset)
 IcpPlan make_icp_plan(int levels, const LevelGeom *g, const int *iters, FrameView cur,
                       FrameView prev, float dist_thr, float angle_thr);
-bool icp_persistent_ok(const IcpPlan &pl, int device);  // grid co-resident + slots fit
+bool icp_persistent_ok(IcpPlan &pl, int device);  // grid co-resident + slots fit
 // begin: run the frame's frame_begin inside the launch (no separate kernel)
 // coop: cooperative launch (the runtime guarantees the grid co-resident)
 // Returns the launch error (a refused cooperative launch: the caller falls

@@ -896,6 +896,13 @@ __global__ __launch_bounds__(kIcpThreads) void k_icp_acc(LevelGeom g, int xe, in
 // begin: the frame's frame_begin is folded in (overlapped frames): every block
 // derives the begun state itself and block 0's thread 0, the only writer of
 // these fields during the kernel, stores it first
+// kStride: a level may have more pixel groups than the grid has blocks
+// (IcpPlan::stride, 1280x720 level 0); block b then also takes groups b +
+// gridDim, b + 2 gridDim, ... whose current-frame pixels it re-reads every
+// iteration.  Their products join the lane sums before the block reduce: the
+// sums stay integers below 2^53 (<= 16 groups per block, IcpPlan docs), so the
+// fp64 adds remain exact and the int64 totals are the oracle's.
+template <bool kStride>
 __global__ __launch_bounds__(kIcpThreads, 2) void k_icp_track(IcpPlan pl, DevState *__restrict__ st,
                                                    IcpSync *__restrict__ sy, int begin) {
   DevPose P;
@@ -923,14 +930,17 @@ __global__ __launch_bounds__(kIcpThreads, 2) void k_icp_track(IcpPlan pl, DevSta
     const int nx = pl.xgroups[l];
     const int prank = nx >= 8 ? (int)blockIdx.x : (int)(blockIdx.x / 8) * nx + (int)(blockIdx.x % 8);
     const bool mine = (nx >= 8 || (int)(blockIdx.x % 8) < nx) && prank < pl.groups[l];
+    // (level-uniform) more groups than blocks: identity group order, strided
+    const bool stride = kStride && nx >= 8 && pl.groups[l] > (int)gridDim.x;
     f3 n0[kIcpPix], v0[kIcpPix];
     bool ok[kIcpPix];
     if (mine)
-      icp_load_cur(g, pl.xe[l], pl.npix[l], nx < 8 ? prank : (KFX_ICP_XCD ? xcd_remap(blockIdx.x, pl.groups[l]) : (int)blockIdx.x),
+      icp_load_cur(g, pl.xe[l], pl.npix[l],
+                   nx < 8 ? prank : (stride ? (int)blockIdx.x : (KFX_ICP_XCD ? xcd_remap(blockIdx.x, pl.groups[l]) : (int)blockIdx.x)),
                    pl.ppl[l], pl.cv[l], pl.cn[l], n0, v0, ok);
     for (int it = 0; it < pl.iters[l] && !fail; ++it, ++slot) {
       unsigned long long *sh = sy->sums + (size_t)slot * kIcpShards * 27;
-      target += pl.groups[l];
+      target += stride ? gridDim.x : pl.groups[l];  // arrivals: the blocks with a group
       const bool tr = threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x - 1);
       if (tr && blockIdx.x == 0) sy->trace[slot][0] = wall_clock64();
 #ifdef KFX_ICP_BLOCK_TRACE
@@ -939,6 +949,16 @@ __global__ __launch_bounds__(kIcpThreads, 2) void k_icp_track(IcpPlan pl, DevSta
       if (mine) {
         double acc[27];
         icp_lane(g, P, n0, v0, ok, pl.ppl[l], pl.pv[l], pl.pn[l], pl.dist2_max, pl.sine2_max, acc);
+        if (stride)
+          for (int gx = (int)blockIdx.x + (int)gridDim.x; gx < pl.groups[l]; gx += (int)gridDim.x) {
+            f3 n1[kIcpPix], v1[kIcpPix];
+            bool ok1[kIcpPix];
+            double a1[27];
+            icp_load_cur(g, pl.xe[l], pl.npix[l], gx, pl.ppl[l], pl.cv[l], pl.cn[l], n1, v1, ok1);
+            icp_lane(g, P, n1, v1, ok1, pl.ppl[l], pl.pv[l], pl.pn[l], pl.dist2_max, pl.sine2_max, a1);
+#pragma unroll
+            for (int i = 0; i < 27; ++i) acc[i] += a1[i];
+          }
         if (tr && blockIdx.x == 0) sy->trace[slot][8] = wall_clock64() + (acc[3] == -1.5 ? 1 : 0);
         const long long bsum = icp_block_reduce(red, acc);
         if (tr && blockIdx.x == 0) sy->trace[slot][9] = wall_clock64() + (bsum == -7 ? 1 : 0);
@@ -3491,14 +3511,26 @@ IcpPlan make_icp_plan(int levels, const LevelGeom *g, const int *iters, FrameVie
   return pl;
 }
 
-bool icp_persistent_ok(const IcpPlan &pl, int device) {
+bool icp_persistent_ok(IcpPlan &pl, int device) {
   if (pl.slots > kIcpMaxSlots) return false;
   int per_cu = 0, cus = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_icp_track, kIcpThreads, 0) != hipSuccess)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_icp_track<false>, kIcpThreads, 0) != hipSuccess)
     return false;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
     return false;
-  return (long long)per_cu * cus >= pl.nblocks;
+  pl.stride = 0;
+  if ((long long)per_cu * cus >= pl.nblocks) return true;
+  // too many groups to be co-resident: the strided kernel on the blocks that are
+  int per_cu_s = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_s, k_icp_track<true>, kIcpThreads, 0) != hipSuccess)
+    return false;
+  const int cap = per_cu_s * cus;
+  if (cap <= 0 || (pl.nblocks + cap - 1) / cap > kIcpStrideMax) return false;
+  for (int l = 0; l < pl.levels; ++l)
+    if (pl.xgroups[l] < 8) return false;  // (XCD-group levels index by residue, not strided)
+  pl.nblocks = cap;
+  pl.stride = 1;
+  return true;
 }
 
 hipError_t launch_icp_track(hipStream_t s, const IcpPlan &pl, DevState *st, IcpSync *sync, int begin, bool coop) {
@@ -3510,10 +3542,15 @@ hipError_t launch_icp_track(hipStream_t s, const IcpPlan &pl, DevState *st, IcpS
     IcpSync *a2 = sync;
     int a3 = begin;
     void *args[] = {&a0, &a1, &a2, &a3};
-    return hipLaunchCooperativeKernel(reinterpret_cast<const void *>(k_icp_track), dim3(pl.nblocks),
+    return hipLaunchCooperativeKernel(pl.stride ? reinterpret_cast<const void *>(k_icp_track<true>)
+                                                : reinterpret_cast<const void *>(k_icp_track<false>),
+                                      dim3(pl.nblocks),
                                       dim3(kIcpThreads), args, 0, s);
   }
-  hipLaunchKernelGGL(k_icp_track, dim3(pl.nblocks), dim3(kIcpThreads), 0, s, pl, st, sync, begin);
+  if (pl.stride)
+    hipLaunchKernelGGL(k_icp_track<true>, dim3(pl.nblocks), dim3(kIcpThreads), 0, s, pl, st, sync, begin);
+  else
+    hipLaunchKernelGGL(k_icp_track<false>, dim3(pl.nblocks), dim3(kIcpThreads), 0, s, pl, st, sync, begin);
   return hipGetLastError();
 }
 

@@ -127,6 +127,34 @@ def test_icp_track_matches_oracle(dist, angle, seq_vga):
     kf.close()
 
 
+def test_icp_track_720p_strided_matches_oracle():
+    """1280x720 (C5's frames): level 0 has more pixel groups than the persistent
+    grid holds co-resident, so blocks take several groups (k_icp_track<true>);
+    the int64 sums, and so the pose, still match the oracle's kfo_icp_track.
+    The persistent kernel must be the one that ran (no per-iteration fallback)."""
+    import ctypes as C
+    from kfx.abi import fptr
+    intr = synth.Intrinsics.hd720()
+    bgr, dep, gt = synth.sequence(4, intr, noise=True, dropout=0.01)
+    I = Intrinsics.from_any(intr)
+    kf, p = make(intr, dims=64)
+    prev = O.preprocess(dep[1].astype(np.float32), I, p)
+    cur = O.preprocess(dep[2].astype(np.float32), I, p)
+    kf.stage_preprocess(bgr[2], dep[2].astype(np.float32))
+    for l in range(3):
+        kf.set_frame_maps(KFX_FRAME_PREV, l, prev[1][l], prev[2][l])
+    rc, gpose = kf.stage_icp()
+    PA = C.POINTER(C.c_float) * 3
+    opose = Pose()
+    st = O.lib().kfo_icp_track(PA(*[fptr(a) for a in cur[1]]), PA(*[fptr(a) for a in cur[2]]),
+                               PA(*[fptr(a) for a in prev[1]]), PA(*[fptr(a) for a in prev[2]]),
+                               C.byref(I), C.byref(p), C.byref(opose))
+    assert rc == KFX_OK and st == 0
+    assert np.abs(gpose.matrix() - opose.matrix()).max() <= 1e-6
+    assert kf.set_icp_persistent(False)  # True: the persistent path was the one in use
+    kf.close()
+
+
 def _vol_equal(kf, vol):
     t, w, c = kf.volume_soa()
     assert np.array_equal(t, vol.tsdf), f"tsdf: {(t != vol.tsdf).sum()} voxels differ"
