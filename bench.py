@@ -82,9 +82,10 @@ def parse():
                     help="auto: single at N=1, slab at N>1")
     ap.add_argument("--icp", choices=["replicated", "allreduce"], default="replicated",
                     help="slab mode: every rank runs the full ICP, or its band with the partials all-reduced")
-    ap.add_argument("--zslab", choices=["none", "c2", "c4", "c5"], default="c4",
+    ap.add_argument("--zslab", choices=["none", "c2", "c4", "c5"], default="c5",
                     help="N>1 with the replica line: also time ONE stream of this config Z-slab sharded over "
-                         "the N GPUs (strong scaling, RCCL combine) as the `zslab` record")
+                         "the N GPUs (strong scaling, RCCL combine) as the `zslab` record; default c5, the "
+                         "2048^3 volume north_star's integrate-scaling claim is about")
     ap.add_argument("--replicas", type=int, default=1,
                     help="slab mode at N>1: time independent replica streams first (the fallback line)")
     ap.add_argument("--zslab-timeout", type=float, default=300.0)
@@ -94,6 +95,9 @@ def parse():
                     help="N=1: time point extraction and marching cubes on the final volume (0 = skip)")
     ap.add_argument("--c3-frames", type=int, default=20,
                     help="N=1, C2: timed frames of the C3 record (1024^3 @ 2 mm, same frames; 0 = skip)")
+    ap.add_argument("--c5-frames", type=int, default=10,
+                    help="N=1, C2: timed frames of the C5 single-volume record (1280x720, 2048^3 @ 2 mm: the "
+                         "N=1 point of the zslab curve; 0 = skip)")
     return ap.parse_args()
 
 
@@ -459,11 +463,15 @@ def main():
     lock = threading.Lock()
     printed = []
 
-    def emit(line):
+    def emit(line, extra=None):
+        """Print the line once; `extra` is merged into a copy taken under the lock
+        (a watchdog thread never changes the main thread's dict)."""
         with lock:
             if printed:
                 return
             printed.append(1)
+            if extra:
+                line = dict(line, **extra)
             if rank == 0:
                 os.write(json_fd, (json.dumps(line) + "\n").encode())
 
@@ -476,9 +484,9 @@ def main():
 
     timer = None
     if replicas is not None:
-        def on_timeout():
+        def on_timeout():  # the line is printed, but a hang is a failure: exit 3
             emit(fallback(f"timed out after {a.zslab_timeout:.0f} s"))
-            os._exit(0)
+            os._exit(3)
         timer = threading.Timer(a.zslab_timeout, on_timeout)
         timer.daemon = True
         timer.start()
@@ -495,10 +503,9 @@ def main():
     # N>1 replica line: one Z-slab sharded stream beside it, under
     # its own time limit, so that a failing or hung collective still leaves the line
     if mode == "replicas" and (world > 1 or a.mode == "replicas") and a.zslab != "none":
-        def on_zslab_timeout():
-            out["zslab"] = {"error": f"timed out after {a.zslab_timeout:.0f} s"}
-            emit(out)
-            os._exit(0)
+        def on_zslab_timeout():  # the replica line stands, the hang exits 3
+            emit(out, {"zslab": {"error": f"timed out after {a.zslab_timeout:.0f} s"}})
+            os._exit(3)
         zt = threading.Timer(a.zslab_timeout, on_zslab_timeout)
         zt.daemon = True
         zt.start()
@@ -515,6 +522,19 @@ def main():
         W3, H3, n3, L3 = CONFIGS["c3"]
         f3 = (bgr, dep, synth.ping_pong(len(bgr), b.warmup + b.steps))
         out["c3_record"] = single_record(b, "c3", intr, n3, L3, f3, D, local)
+    # N=1: the C5 single volume (1280x720, 2048^3 @ 2 mm), the N=1 point of the
+    # zslab curve the driver's N>1 runs record
+    if world == 1 and mode == "single" and a.c5_frames and name == "c2":
+        import copy
+        b = copy.copy(a)
+        b.steps = a.c5_frames
+        W5, H5, n5, L5 = CONFIGS["c5"]
+        i5 = intrinsics(W5, H5)
+        u5 = 16
+        bgr5, dep5, _ = synth.sequence(u5, i5, L=L5, noise=True, traj_seed=7, dropout=0.005)
+        f5 = (bgr5, dep5.astype(np.float32), synth.ping_pong(u5, b.warmup + b.steps))
+        out["c5_record"] = single_record(b, "c5", i5, n5, L5, f5, D, local)
+        del bgr5, dep5, f5
     emit(out)
     D.close()
 
@@ -567,7 +587,18 @@ def zslab_record(a, intr, frames, D, rank, world, local, icp_ar, geom):
     return {"workload": workload_text(a.zslab, W, H, n, L, "slab", world, icp_ar),
             "value": round(a.steps / r["elapsed"], 3), "unit": "frames/s", "scaling": "strong",
             "ms_per_step": round(1000.0 * r["elapsed"] / a.steps, 4), "steps": a.steps, "warmup": a.warmup,
-            "tracked_frames": int(r["tracked"]), "per_rank": per_rank}
+            "tracked_frames": int(r["tracked"]), "per_rank": per_rank,
+            "integrate_ms_per_rank": [p["integrate_ms"] for p in per_rank],
+            "integrate_imbalance_max_over_mean": imbalance([p["integrate_ms"] for p in per_rank])}
+
+
+def imbalance(xs):
+    """max / mean of the per-rank values (1.0 = perfectly balanced; None when
+    any rank has no sample)."""
+    xs = [float(x) for x in xs]
+    if not xs or any(x != x for x in xs) or sum(xs) <= 0:
+        return None
+    return round(max(xs) / (sum(xs) / len(xs)), 4)
 
 
 def measure_main(a, name, intr, params, frames, D, rank, world, local, mode, icp_ar):
@@ -714,6 +745,10 @@ def measure_main(a, name, intr, params, frames, D, rank, world, local, mode, icp
         "graph": graph_parts(a, mode), "overlap": not a.no_overlap,
         "parallelism": (f"zslab x{world}" + (" + icp allreduce" if icp_ar else "") if mode == "slab" else
                         (f"replicas x{world} (independent streams)" if world > 1 else "single")),
+        "collective": ("RCCL: raycast combine per frame" + (" + ICP partials per iteration" if icp_ar else "")
+                       if mode == "slab" else
+                       ("none: N independent C2 streams; this line is NOT the Z-slab sharded scaling "
+                        "(that is the `zslab` record)" if world > 1 else "none (one GPU)")),
         "tracked_frames": int(tracked),
         "reference_ms_per_frame": REF_MS_PER_FRAME,
     })

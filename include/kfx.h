@@ -361,7 +361,13 @@ int kfx_create_slab(const kfx_intrinsics *intr, const kfx_params *params, int de
  * from the frame's filtered depth: voxel slots visited, updated voxels
  * weighted more); kfx_slab_balance turns such a
  * histogram into cuts minimising the largest slab's stored-range work (halos
- * included).  Results stay bit-identical to the single volume for any cuts. */
+ * included).  Results stay bit-identical to the single volume for any cuts.
+ * Side effect: kfx_slice_work(_parts) preprocesses the given frame into the
+ * context's buffer set 0 (current-frame maps, colour input, {depth, 1/lambda}
+ * table); the volume, poses and previous-frame maps are untouched.  Called on
+ * a context mid-sequence, kfx_get_frame_maps(KFX_FRAME_CUR), kfx_render and
+ * kfx_integrate_stats then describe this frame, not the last tracked one:
+ * call it before the sequence (as bench.py does) or on a scratch context. */
 int kfx_create_slab_cuts(const kfx_intrinsics *intr, const kfx_params *params, int device,
                          int rank, int world, const int *cuts, kfx_ctx **out);
 int kfx_slice_work(kfx_ctx *ctx, const uint8_t *bgr, const float *depth_mm, int64_t *work);

@@ -113,6 +113,7 @@ struct kfx_ctx {
   hipEvent_t ev_prep = nullptr, ev_free[2]{};
   hipEvent_t ev_icp = nullptr;  // after the last overlapped frame's ICP (the next preprocess starts there)
   bool group_chain = false;     // kfx_pipeline_group member: record ev_icp after every ICP
+  bool graphs_stale = false;    // a refused persistent ICP launch: captured graphs still hold it
 
   // sampled kernel timing (kfx_set_kernel_timing): every `timing_every`-th
   // pipelined frame records its stage events into the next unused set
@@ -390,6 +391,7 @@ bool try_icp_persistent(kfx_ctx *c, hipStream_t s, int begin) {
   if (launch_icp_track(s, c->icp_plan, c->st, c->icp_sync, begin, c->icp_coop) == hipSuccess) return true;
   (void)hipGetLastError();
   c->icp_persistent_enabled = false;
+  c->graphs_stale = true;  // (maybe mid-capture: run_frame drops the graphs before the next frame)
   return false;
 }
 
@@ -608,6 +610,12 @@ int run_frame(kfx_ctx *c, FrameInput in, hipGraphExec_t *graph, bool overlap = f
               hipGraphExec_t *ovg = nullptr) {
   int r = ensure_pose_capacity(c, 1);
   if (r) return r;
+  if (c->graphs_stale) {  // captured with the persistent ICP launch the runtime refused
+    HIPCHK(hipStreamSynchronize(c->pstream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    destroy_graphs(c);
+    c->graphs_stale = false;
+  }
   c->last_bgr = in.bgr;
   hipEvent_t *tev = timing_sample(c);  // this frame's timing sample, if sampled
   if (overlap && c->overlap && !c->profiling) {
@@ -1252,10 +1260,10 @@ int kfx_set_kernel_timing(kfx_ctx *c, int every, int max_samples) {
   if (r) return r;
   if (every < 0 || max_samples < 0) return set_err(KFX_ERR_ARG, "negative timing argument");
   HIPCHK(hipStreamSynchronize(c->stream));
+  // (the extraction events c->xev are not timing samples: they stay)
   for (hipEvent_t e : c->tsets) (void)hipEventDestroy(e);
-  for (hipEvent_t e : c->xev)
-    if (e) (void)hipEventDestroy(e);
   c->tsets.clear();
+  c->ext_pending = nullptr;  // pointed into tsets (kfx_slab_frame_local)
   c->tnext = 0;
   c->frame_seq = 0;
   c->timing_every = every;
@@ -2163,6 +2171,13 @@ int kfx_pipeline_group(kfx_ctx **cs, int n, const uint8_t *bgr, const float *dep
   }
   int r;
   const bool sharded = cs[0]->icp_sharded && n > 1;
+  struct ChainScope {  // group_chain holds for this call only (every exit)
+    kfx_ctx **cs;
+    int n;
+    ~ChainScope() {
+      for (int k = 0; k < n; ++k) cs[k]->group_chain = false;
+    }
+  } chain_scope{cs, n};
   hipEvent_t *tev[kMaxGroup] = {};  // members' timing samples (replicated ICP only)
   for (int k = 0; k < n; ++k) {  // local phase: preprocess, ICP, integrate, slab raycast
     kfx_ctx *c = cs[k];

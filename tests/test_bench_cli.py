@@ -82,3 +82,22 @@ def test_dist_gather_over_gloo():
     for rank, rows, mx in res:
         assert rows == [[0.0, 10.0, 0.5], [1.0, 11.0, 0.5]]
         assert mx == 1.25
+
+
+def test_cli_defaults_pin_the_measured_configs(monkeypatch):
+    """The N>1 side record is one C5 stream (2048^3, north_star's scaling
+    claim) Z-slab sharded over the ranks; at N=1 the C3 and C5 single-volume
+    records run beside the C2 line (the N=1 points of their curves)."""
+    b = load_bench()
+    monkeypatch.setattr(sys, "argv", ["bench.py"])
+    a = b.parse()
+    assert (a.gpus, a.config, a.mode, a.zslab, a.cuts, a.icp) == (1, "auto", "auto", "c5", "balanced", "replicated")
+    assert a.c3_frames > 0 and a.c5_frames > 0 and a.cpu_frames > 0
+    assert b.CONFIGS["c5"] == (1280, 720, 2048, 4.096)
+
+
+def test_imbalance():
+    b = load_bench()
+    assert b.imbalance([1.0, 1.0]) == 1.0
+    assert b.imbalance([3.0, 1.0]) == 1.5
+    assert b.imbalance([1.0, float("nan")]) is None

@@ -246,6 +246,48 @@ def test_c3_pipeline_two_frames_match_oracle(seq_vga):
         assert np.array_equal(gt_, ot[idx]) and np.array_equal(gw, ow[idx])
         assert np.array_equal(gc.reshape(-1, n, 4), oc.reshape(-1, 4)[idx])
         assert (gw > 0).sum() > 10000
+    else:  # a last-ulp Rodrigues difference: the maps / volume are not comparable bit for bit
+        pytest.xfail(f"pose differs from the oracle by {err:.3g} (<= 1e-6): maps and volume not compared")
+    kf.close()
+
+
+@pytest.mark.timeout(600)
+def test_720p_pipeline_matches_oracle():
+    """C5's frame size (1280x720) through the whole pipeline against the
+    serial oracle: 512^3 @ 8 mm (L = 4.096 m, C5's volume extent), 4 frames.
+    This pins the A2 ICP floor grid at 720p (rows 704 / 352 / 160 of 720 / 360
+    / 180; rigid_icp.cu:135-139), the strided persistent ICP (k_icp_track<true>:
+    level 0 has more pixel groups than the co-resident grid), and the 720p
+    raycast + resize.  Poses (tolerance 1e-6, 0 expected), every level of the
+    raycast model maps bit for bit, and the whole volume bit for bit."""
+    intr = synth.Intrinsics.hd720()
+    L = 4.096
+    bgr, dep, _ = synth.sequence(4, intr, L=L, noise=True, dropout=0.01)
+    I = Intrinsics.from_any(intr)
+    p = default_params(dims=512, range_m=L)
+    kf = KinectFusion(I, p)
+    pipe = O.Pipeline(I, p)
+    for k in range(len(dep)):
+        d = dep[k].astype(np.float32)
+        assert kf.pipeline(bgr[k], d) == pipe.process(bgr[k], d) == KFX_OK, k
+    gp, op = kf.pose_record, pipe.poses()
+    assert gp.shape == op.shape == (len(dep), 4, 4)
+    err = float(np.abs(gp - op).max())
+    assert err <= 1e-6, err
+    assert np.abs(gp[-1] - np.eye(4)).max() > 1e-3  # the camera moved: ICP did work
+    if err != 0:
+        pytest.xfail(f"pose differs from the oracle by {err:.3g} (<= 1e-6): maps and volume not compared")
+    for l in range(3):
+        _, gv, gn = kf.frame_maps(KFX_FRAME_PREV, l)
+        assert feq(gv, pipe.map(1, 1, l)), f"vmap level {l}: {mismatch(gv, pipe.map(1, 1, l))} differ"
+        assert feq(gn, pipe.map(1, 2, l)), f"nmap level {l}: {mismatch(gn, pipe.map(1, 2, l))} differ"
+    t, w, c = kf.volume_soa()
+    ot, ow, oc = pipe.volume()
+    assert np.array_equal(t, ot), f"tsdf: {(t != ot).sum()} voxels differ"
+    assert np.array_equal(w, ow), f"weight: {(w != ow).sum()} voxels differ"
+    assert np.array_equal(c, oc), f"rgb: {(c != oc).sum()} bytes differ"
+    assert (w > 0).sum() > 100000
+    assert kf.set_icp_persistent(False)  # True: the (strided) persistent ICP was the path in use
     kf.close()
 
 

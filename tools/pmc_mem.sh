@@ -20,7 +20,7 @@ for v in "$@"; do
     i=$((i+1))
     echo "=== $v pass $i: $p"
     KFX_LIB_PATH=$L timeout -s KILL 120 rocprofv3 --pmc $p --output-format csv -d "$ROOT/gpurun_out/pmcm/$v/p$i" -- \
-        python3 "$ROOT/bench.py" $ARGS --profile-frames 2 --cpu-frames 0 --c1-frames 0 --c3-frames 0 --host-frames 0 --extract 0 \
+        python3 "$ROOT/bench.py" $ARGS --profile-frames 2 --cpu-frames 0 --c1-frames 0 --c3-frames 0 --c5-frames 0 --host-frames 0 --extract 0 \
         > "$ROOT/gpurun_out/pmcm/$v/p$i.log" 2>&1 || { echo "rc=$?"; tail -5 "$ROOT/gpurun_out/pmcm/$v/p$i.log"; exit 1; }
   done
 done
