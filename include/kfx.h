@@ -241,9 +241,8 @@ int kfx_integrate_counts(kfx_ctx *ctx, int64_t *n_updated, int64_t *n_colored);
 /* Work statistics of the same count-only pass: out = {updated, coloured,
  * visited (voxels evaluated inside the per-column candidate z intervals),
  * gathered (visited voxels that project into the image and read a depth),
- * wave batches executed (4 voxels per lane each), updated voxels of certified
- * free-space groups (no projection / gather / sdf), wave batches of
- * such groups, 0}. */
+ * wave batches executed (4 voxels per lane each), 0, 0, 0} (slots 5-7 are
+ * reserved; they held the dropped free-space certification's counts). */
 int kfx_integrate_stats(kfx_ctx *ctx, int64_t out[8]);
 /* Work statistics of the last processed frame's raycast (re-run on the same
  * state, nothing written): out = {rays marched, empty-space skip lookups,

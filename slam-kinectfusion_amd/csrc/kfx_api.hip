@@ -975,11 +975,9 @@ static int create_impl(const kfx_intrinsics *intr, const kfx_params *params, int
   if ((r = dalloc(c, (void **)&c->raw0_u16, np0 * 2))) return fail(r);
   if ((r = dalloc(c, (void **)&c->bgr, np0 * 3))) return fail(r);
   if ((r = dalloc(c, (void **)&c->inv_lambda, np0 * 4))) return fail(r);
-  // {depth, 1/lambda} per pixel + 16 max-depth shards + the min-depth pyramid
-  // (levels 1..4, < np0 / 3 + W + H + 4 floats; kfx_kernels.hip dmin_level)
-  const size_t pyr = np0 / 3 + (size_t)intr->width + (size_t)intr->height + 64;
+  // {depth, 1/lambda} per pixel + 16 max-depth shards
   for (float2 *&d : c->dl0b)
-    if ((r = dalloc(c, (void **)&d, np0 * 8 + 64 + pyr * 4))) return fail(r);
+    if ((r = dalloc(c, (void **)&d, np0 * 8 + 64))) return fail(r);
   c->vol = make_vol(p, rank, world, cuts);
   const size_t n = nvox(c);
   {
@@ -1001,10 +999,6 @@ static int create_impl(const kfx_intrinsics *intr, const kfx_params *params, int
     std::vector<unsigned> iota(items);
     for (size_t i = 0; i < items; ++i) iota[i] = (unsigned)i;
     HIPCHK(hipMemcpy(c->vol.iperm, iota.data(), items * 4, hipMemcpyHostToDevice));
-    if (integrate_planned(c->vol)) {  // k_int_plan's per-item ranges and chunk start values
-      if ((r = dalloc(c, (void **)&c->vol.prange, items * sizeof(int2)))) return fail(r);
-      if ((r = dalloc(c, (void **)&c->vol.pckpt, items * 64 * sizeof(float4)))) return fail(r);
-    }
   }
   if ((r = dalloc(c, (void **)&c->st, sizeof(DevState)))) return fail(r);
   c->pose_cap = kInitialPoseCap;
@@ -1696,9 +1690,8 @@ int kfx_stage_icp(kfx_ctx *c, kfx_pose *out) {
   return failed ? KFX_TRACKING_LOST : KFX_OK;
 }
 
-// out: {updated, coloured, visited, gathered, wave batches, updated in
-// certified free-space groups, certified wave batches, 0} of the last frame's
-// integrate
+// out: {updated, coloured, visited, gathered, wave batches, 0, 0, 0} of the
+// last frame's integrate
 static int integrate_stats_impl(kfx_ctx *c, int64_t out[8], const float *xpose) {
   HIPCHK(hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * 128, c->stream));
   launch_integrate(c->stream, c->vol, c->g[0], c->dl0, c->cur.d[0], c->inv_lambda, c->last_bgr ? c->last_bgr : c->bgr, c->st,

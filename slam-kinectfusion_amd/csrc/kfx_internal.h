@@ -124,10 +124,6 @@ struct VolView {
   unsigned *iperm;
   int inchunk;
   int iadapt;  // length-capped chunks + longest-first order (deep volumes), else geometric chunks
-  // Integrate plan (k_int_plan, volumes with several chunks per tile): per
-  // item {za, zb} and per item lane the chunk's start vc + interval bits
-  int2 *prange;
-  float4 *pckpt;
   __host__ __device__ size_t bocc_bytes() const { return (size_t)tiles_x * tiles_y * bw * 8; }
   __host__ __device__ size_t socc_bytes() const { return (size_t)stx * sty * sw * 4; }
   __host__ __device__ size_t local_voxels() const { return slice * (size_t)zn; }
@@ -292,7 +288,6 @@ int integrate_chunks(const VolView &v);
 // per global slice: voxels passing integrate's depth test at vol2cam (an estimate, slab balancing)
 void launch_slice_work(hipStream_t s, const VolView &v, DevPose vol2cam, LevelGeom g0, const float2 *dl0,
                        unsigned long long *hist);
-bool integrate_planned(const VolView &v);
 // owned-slice records of n (x, y) columns (device cols), column-major outputs
 void launch_gather_columns(hipStream_t s, VolView v, const int32_t *cols, int n, int16_t *t, int16_t *w,
                            uint32_t *c);

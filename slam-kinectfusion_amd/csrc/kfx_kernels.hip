@@ -15,17 +15,11 @@
 #include "kfx_internal.h"
 #include "kfx_ffadd.h"
 
-#ifndef KFX_INT_ICHECK
-#define KFX_INT_ICHECK 1  // integrate fast path: integer image-range tests
-#endif
 #ifndef KFX_INT_KB
 #define KFX_INT_KB 4  // integrate: voxels per batch (loads in flight per lane)
 #endif
 #ifndef KFX_RAY_OCC
 #define KFX_RAY_OCC 5  // raycast: waves per SIMD the register budget must allow (4800 waves at VGA: one round at 5)
-#endif
-#ifndef KFX_RAY_SREPLAY
-#define KFX_RAY_SREPLAY 0  // raycast skip replay as four scalar add chains (A/B)
 #endif
 #ifndef KFX_RAY_KR
 #define KFX_RAY_KR 14  // raycast: samples per batch (loads in flight per lane)
@@ -57,32 +51,11 @@
 #ifndef KFX_INT_MAXCHUNK
 #define KFX_INT_MAXCHUNK 8  // integrate: most z-chunks per column tile
 #endif
-#ifndef KFX_FFADD
-#define KFX_FFADD 1  // integrate's vc replay by the exact fast-forward (kfx_ffadd.h)
-#endif
 #ifndef KFX_FF_MIN
 #define KFX_FF_MIN 768  // fast-forward replays of at least this many adds (shorter ones: the adds; A/B r3m: 384 costs C2 +8 %)
 #endif
-#ifndef KFX_INT_LPT
-#define KFX_INT_LPT 0  // integrate: longest-first dispatch order in every chunk mode (A/B)
-#endif
-#ifndef KFX_INT_PLAN
-#define KFX_INT_PLAN 0  // integrate: chunk start values from one sweep per tile (k_int_plan) instead of per-chunk replays (measured: the plan kernel costs what the replays cost)
-#endif
-#ifndef KFX_INT_PWAVES
-#define KFX_INT_PWAVES 16384  // planned integrate: target wave count (C2: 4 equal chunks of 4096 tiles)
-#endif
-#ifndef KFX_INT_PCHUNKR
-#define KFX_INT_PCHUNKR 100  // planned integrate: chunk weights (100: equal chunks)
-#endif
-#ifndef KFX_INT_ZCLASS
-#define KFX_INT_ZCLASS 0  // integrate: 4-B depth gathers, voxels classified by the vc.z bound, exact sdf only near surfaces (A/B)
-#endif
-#ifndef KFX_INT_CERT
-#define KFX_INT_CERT 0  // integrate: certified free-space groups skip projection, gather and sdf (measured slower)
-#endif
-#ifndef KFX_INT_DEDUP
-#define KFX_INT_DEDUP 0  // integrate: a voxel projecting to the previous voxel's pixel reuses its gather (A/B)
+#ifndef KFX_INT_PXY
+#define KFX_INT_PXY 0  // integrate fast projection: packed {x, y} of one voxel (A/B)
 #endif
 #ifndef KFX_INT_WAVES
 #define KFX_INT_WAVES 12288  // integrate: target wave count (z-chunks per column tile; C2: 3 chunks of 4096 tiles)
@@ -242,19 +215,6 @@ __device__ __forceinline__ void frame_begin(DevState *st) {
 // the frame's max-depth shards live after the level-0 dl table (one per cur buffer)
 __device__ __forceinline__ unsigned *dmax_shards(const float2 *dl0, const LevelGeom &g0) {
   return (unsigned *)(const_cast<float2 *>(dl0) + (size_t)g0.w * g0.h);
-}
-
-// Min-depth pyramid of the level-0 filtered depth, after the max-depth shards:
-// level k = 1..kPyrLevels holds the minimum over each 2^k x 2^k pixel cell
-// (cells clipped at the image edge; 0 where any pixel of the cell has no depth),
-// ceil(W / 2^k) x ceil(H / 2^k) floats, levels back to back.  Written by
-// k_preprocess_maps (level 0 blocks are 16x16 tiles = one level-4 cell);
-// read by integrate's free-space certification.
-[[maybe_unused]] constexpr int kPyrLevels = 4;
-__device__ __forceinline__ const float *dmin_level(const float2 *dl0, const LevelGeom &g0, int k) {
-  const float *p = reinterpret_cast<const float *>(dl0 + (size_t)g0.w * g0.h) + kDmaxShards;
-  for (int i = 1; i < k; ++i) p += (size_t)((g0.w + (1 << i) - 1) >> i) * ((g0.h + (1 << i) - 1) >> i);
-  return p;
 }
 
 // z is the global slice; the view stores slices [zb, zb+zn) (tile-column
@@ -536,38 +496,6 @@ __global__ __launch_bounds__(256) void k_preprocess_maps(BilatArgs a) {
     }
     st3(a.n[l], o, n);
   }
-#if KFX_INT_CERT
-  if (l == 0) {  // block-uniform: the min-depth pyramid (dmin_level) of this 16x16 tile
-    // lanes: threadIdx = cy * 16 + cx, a wave = 4 rows; levels 1 and 2 within
-    // the wave (partners differ in lane bits 0/4, 1/5), levels 3 and 4 in LDS
-    float mn = in ? dval : __builtin_huge_valf();  // outside the image: neutral
-    mn = fminf(mn, __shfl_xor(mn, 1));
-    mn = fminf(mn, __shfl_xor(mn, 16));
-    float *p1 = const_cast<float *>(dmin_level(a.dl0, g, 1));
-    const int w1 = (g.w + 1) >> 1;
-    if (in && !(cx & 1) && !(cy & 1)) p1[(size_t)(y >> 1) * w1 + (x >> 1)] = mn;
-    mn = fminf(mn, __shfl_xor(mn, 2));
-    mn = fminf(mn, __shfl_xor(mn, 32));
-    float *p2 = const_cast<float *>(dmin_level(a.dl0, g, 2));
-    const int w2 = (g.w + 3) >> 2;
-    if (in && !(cx & 3) && !(cy & 3)) p2[(size_t)(y >> 2) * w2 + (x >> 2)] = mn;
-    __shared__ float q4[16];  // the 4x4 level-2 cells of the tile
-    if (!(cx & 3) && !(cy & 3)) q4[(cy >> 2) * 4 + (cx >> 2)] = mn;
-    __syncthreads();
-    if (threadIdx.x < 4) {  // level 3: 2x2 cells of 8x8 pixels
-      const int qx = (threadIdx.x & 1) * 2, qy = (threadIdx.x >> 1) * 2;
-      const float m3 = fminf(fminf(q4[qy * 4 + qx], q4[qy * 4 + qx + 1]), fminf(q4[(qy + 1) * 4 + qx], q4[(qy + 1) * 4 + qx + 1]));
-      const int x3 = (X0 >> 3) + (threadIdx.x & 1), y3 = (Y0 >> 3) + (threadIdx.x >> 1);
-      const int w3 = (g.w + 7) >> 3, h3 = (g.h + 7) >> 3;
-      if (x3 < w3 && y3 < h3) const_cast<float *>(dmin_level(a.dl0, g, 3))[(size_t)y3 * w3 + x3] = m3;
-    }
-    if (threadIdx.x == 0) {  // level 4: the tile
-      float m4 = q4[0];
-      for (int i = 1; i < 16; ++i) m4 = fminf(m4, q4[i]);
-      const_cast<float *>(dmin_level(a.dl0, g, 4))[(size_t)(Y0 >> 4) * ((g.w + 15) >> 4) + (X0 >> 4)] = m4;
-    }
-  }
-#endif
   if (l == 0) {  // block-uniform
     unsigned m = (in && dval > 0.f) ? __float_as_uint(dval) : 0u;
     for (int off = 32; off > 0; off >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, off));
@@ -596,15 +524,6 @@ __global__ __launch_bounds__(256) void k_preprocess_maps(BilatArgs a) {
 #define KFX_ICP_PIX 4
 #endif
 constexpr int kIcpPix = KFX_ICP_PIX;
-#ifndef KFX_INT_LEAN
-#define KFX_INT_LEAN 0  // integrate (A/B bits): 1 unconditional tsdf store of updated voxels, 2 negative marks after the batch
-#endif
-#ifndef KFX_INT_PRIO
-#define KFX_INT_PRIO 0  // integrate: s_setprio of the first (longest) chunk's waves (A/B)
-#endif
-#ifndef KFX_RAY_PRIO
-#define KFX_RAY_PRIO 0  // raycast: raise a wave's priority after this many batches (A/B; 0 = off)
-#endif
 #ifndef KFX_EXTRACT_SKIP
 #define KFX_EXTRACT_SKIP 1  // point / mesh extraction: waves of clear bricks read nothing
 #endif
@@ -619,9 +538,6 @@ constexpr int kIcpPix = KFX_ICP_PIX;
 #endif
 #ifndef KFX_ICP_SLEEP
 #define KFX_ICP_SLEEP 1  // ICP release poll: s_sleep units (64 clocks) between polls (0: busy poll)
-#endif
-#ifndef KFX_ICP_XCOARSE
-#define KFX_ICP_XCOARSE 0  // ICP: coarse levels run on the blocks of as few XCD groups (blockIdx mod 8) as fit (A/B)
 #endif
 #ifndef KFX_ICP_THREADS
 #define KFX_ICP_THREADS 256  // ICP: threads per block
@@ -1397,31 +1313,22 @@ struct RayMem<false> {
 // reference, kept as three scalar v_add_f32 chains — the compiler otherwise
 // packs {x, y} into v_pk_add_f32, whose dependent latency makes such chains
 // several times slower (tools/chain_bench.hip).
-#ifndef KFX_SREPLAY
-#define KFX_SREPLAY 1
-#endif
 __device__ __forceinline__ f3 replay_add(f3 a, f3 b) {
-#if KFX_SREPLAY
   asm volatile("v_add_f32 %0, %0, %1" : "+v"(a.x) : "v"(b.x));
   asm volatile("v_add_f32 %0, %0, %1" : "+v"(a.y) : "v"(b.y));
   asm volatile("v_add_f32 %0, %0, %1" : "+v"(a.z) : "v"(b.z));
   return a;
-#else
-  return add(a, b);
-#endif
 }
 // a advanced from slice z to slice za (za - z adds when za > z): the exact
 // fast-forward of kfx_ffadd.h for long replays, the adds themselves (8 per
 // trip) for short ones
 __device__ __forceinline__ f3 replay(f3 a, f3 b, int z, int za) {
-#if KFX_FFADD
   if (za - z >= KFX_FF_MIN) {
     a.x = ff_add(a.x, b.x, za - z);
     a.y = ff_add(a.y, b.y, za - z);
     a.z = ff_add(a.z, b.z, za - z);
     return a;
   }
-#endif
   for (; z + 8 <= za; z += 8) {
 #pragma unroll
     for (int u = 0; u < 8; ++u) a = replay_add(a, b);
@@ -1514,117 +1421,13 @@ __device__ __forceinline__ bool int_chunk(const VolView &v, int chunkr, int chun
   return true;
 }
 
-// Integrate plan (volumes with several z-chunks per tile): one wave per
-// column tile computes its lanes' intervals and the union once, splits it
-// into the chunks, and sweeps vc from z = 1 through the chunk starts with the
-// reference's float adds, storing every chunk's start value: the chunk waves
-// of k_integrate then begin at their first slice instead of each replaying
-// the column from z = 1 (the replays of 3 chunks cost ~7 % of integrate at
-// C2; the sweep here is shared by all chunks of a tile).  Per item
-// (chunk * tiles + tile): prange = {za, zb} ({1, 0}: nothing to do),
-// pckpt[item * 64 + lane] = {vc(za - 1) x, y, z, bits zl | zh << 16}.
-__global__ __launch_bounds__(64) void k_int_plan(VolView v, LevelGeom g, const float2 *__restrict__ dl,
-                                                 const DevState *__restrict__ st, const DevPose *log,
-                                                 DevPose vpose, const float *xpose, int write_work) {
-  __shared__ DevPose s_pose;
-  __shared__ int s_kind;
-  if (threadIdx.x == 0) {
-#if KFX_PLAN_EXP == 2  // timing experiment only (wrong values): no pose loads
-    s_pose = vpose;
-    s_kind = 1;
-#else
-    DevPose gp;
-    s_kind = int_frame_pose(st, log, vpose, xpose, s_pose, gp);
-#endif
-  }
-  __syncthreads();
-  const int tiles = v.tiles_x * v.tiles_y, nchunk = v.inchunk;
-  const int tile = blockIdx.x, lane = threadIdx.x;
-  int2 *rg = v.prange + tile;
-  if (s_kind == 2) return;  // reset frame: integrate zeroes the volume, no plan read
-  const int x = (tile % v.tiles_x) * 8 + (lane & 7);
-  const int y = (tile / v.tiles_x) * 8 + (lane >> 3);
-  f3 vc, zs;
-  int zl, zh;
-  int_column(v, g, dl, s_pose, x, y, vc, zs, zl, zh);
-  int wl = zl, wh = zh;
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    wl = min(wl, __shfl_xor(wl, off));
-    wh = max(wh, __shfl_xor(wh, off));
-  }
-  // the next frame's dispatch order (k_int_order) from this interval length
-  if (write_work && lane == 0 && v.iwork) v.iwork[tile] = wh >= wl ? (unsigned)(wh - wl + 1) : 0u;
-  const unsigned zbits = zl <= zh ? ((unsigned)zl | ((unsigned)zh << 16)) : 0xFFFFu;
-  int z = 1;
-  for (int c = 0; c < nchunk; ++c) {
-    int za = 1, zb = 0;
-    if (wl > wh || !int_chunk(v, KFX_INT_PCHUNKR, c, nchunk, wl, wh, za, zb) ||
-        __all(!(max(za, zl) <= min(zb, zh)))) {
-      if (lane == 0) rg[(size_t)c * tiles] = make_int2(1, 0);
-      continue;
-    }
-#if KFX_PLAN_EXP == 1  // timing experiment only (wrong values): no sweep
-    if (za > z) vc = add(vc, scl(zs, (float)(za - z)));
-    z = max(z, za);
-#else
-    vc = replay(vc, zs, z, za);
-    z = max(z, za);
-#endif
-    v.pckpt[((size_t)c * tiles + tile) * 64 + lane] = make_float4(vc.x, vc.y, vc.z, __uint_as_float(zbits));
-    if (lane == 0) rg[(size_t)c * tiles] = make_int2(za, zb);
-  }
-}
-
-#ifndef KFX_CERT_G
-#define KFX_CERT_G 16  // integrate: slices per certification group (a multiple of KFX_INT_KB)
-#endif
-// Does the group of KFX_CERT_G voxels after vc (the next one is vc + zs) lie in
-// certified free space?  Every voxel of the group projects (rounded, as the
-// exact path computes it) into the pixel box [ilo, ihi] x [jlo, jhi]: along a
-// column u = (a + z b) / (c + z d) fx + cx is monotonic while vc.z > 0, so the
-// box of the two end voxels (approximate quotients, 0.01 px of margin: the
-// rcp / fma errors and the accumulated adds' deviation from the linear model
-// over KFX_CERT_G adds stay below 1e-3 px) holds every rounded projection.
-// If that box is inside the image, the minimum depth over a min-depth pyramid
-// cell cover of it (dmin_level) is the least depth any voxel reads; with vc.z
-// at most zhi (monotonic too), sdf = d - RN(il * |vc|) >= dmin - zhi * bfac >=
-// trunc, evaluated with 1e-5 m of margin for the float evaluation here.
-#if KFX_INT_CERT
-__device__ __forceinline__ bool cert_free(f3 vc, f3 zs, const LevelGeom &g, const float2 *dl, float bfac,
-                                          float need) {
-  const f3 pa = add(vc, zs);
-  const float G = (float)KFX_CERT_G;
-  const f3 pb = {fmaf(G, zs.x, vc.x), fmaf(G, zs.y, vc.y), fmaf(G, zs.z, vc.z)};
-  const float zlo = fminf(pa.z, pb.z), zhi = fmaxf(pa.z, pb.z);
-  if (!(zlo > 1e-3f)) return false;  // (NaN-safe)
-  const float ra = __builtin_amdgcn_rcpf(pa.z), rb = __builtin_amdgcn_rcpf(pb.z);
-  const float ua = fmaf(pa.x * ra, g.fx, g.cx), ub = fmaf(pb.x * rb, g.fx, g.cx);
-  const float va = fmaf(pa.y * ra, g.fy, g.cy), vb = fmaf(pb.y * rb, g.fy, g.cy);
-  const float ulo = fminf(ua, ub) - 0.51f, uhi = fmaxf(ua, ub) + 0.51f;
-  const float vlo = fminf(va, vb) - 0.51f, vhi = fmaxf(va, vb) + 0.51f;
-  if (!(ulo > -1.f && vlo > -1.f && uhi < (float)g.w && vhi < (float)g.h)) return false;
-  const int ilo = (int)ceilf(ulo), ihi = (int)floorf(uhi), jlo = (int)ceilf(vlo), jhi = (int)floorf(vhi);
-  if (ilo < 0 || jlo < 0 || ihi > g.w - 1 || jhi > g.h - 1) return false;
-  const int span = max(ihi - ilo, jhi - jlo) + 1;
-  const int k = span <= 2 ? 1 : (span <= 4 ? 2 : (span <= 8 ? 3 : (span <= 16 ? 4 : 0)));
-  static_assert(kPyrLevels == 4, "the level choice above covers spans up to 16 px");
-  if (!k) return false;
-  const float *lv = dmin_level(dl, g, k);
-  const int wk = (g.w + (1 << k) - 1) >> k;
-  const int x0 = ilo >> k, x1 = ihi >> k, y0 = jlo >> k, y1 = jhi >> k;
-  const float dmin = fminf(fminf(lv[y0 * wk + x0], lv[y0 * wk + x1]), fminf(lv[y1 * wk + x0], lv[y1 * wk + x1]));
-  return dmin - zhi * bfac >= need;
-}
-#endif
-
 // Work split: a wave owns an 8x8 tile of columns and one of gridDim.y z-chunks
 // of every column's in-range interval (more waves per SIMD to hide latency);
 // each lane replays the vc adds up to its chunk start, so every voxel's vc is
 // the reference's bit for bit.
 // kCount: count-only variant (no voxel traffic) giving N_upd / N_col, the
 // algorithmic-byte inputs of the roofline.
-template <bool kCount, bool kIdx32, bool kPlan>
+template <bool kCount, bool kIdx32>
 __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(KFX_INT_OCC, KFX_INT_OCC))) void k_integrate(VolView v, LevelGeom g,
                                                    const float2 *__restrict__ dl,
                                                    const float *__restrict__ dmap,
@@ -1639,7 +1442,7 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
   __shared__ DevPose s_pose;
   __shared__ int s_kind;
   for (int i = threadIdx.x; i < 257; i += KFX_INT_BLOCK) rtab[i] = 1.f / (float)max(1, i);
-  if (threadIdx.x == 0) {  // (inline rather than int_frame_pose: that form spills in the unplanned loop)
+  if (threadIdx.x == 0) {  // (inline rather than int_frame_pose: that form spills in the loop)
     if (xpose) {  // stage seam: explicit vol2cam
       s_kind = 1;
       for (int i = 0; i < 9; ++i) s_pose.R[i] = xpose[i];
@@ -1665,10 +1468,6 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
   const unsigned item = v.iperm ? v.iperm[blockIdx.x] : blockIdx.x;  // chunk * tiles + tile
   const int tile = (int)(item % (unsigned)ntiles), chunk = (int)(item / (unsigned)ntiles);
   if (chunk >= nchunk) return;
-#if KFX_INT_PRIO
-  // the longest (first) chunks set the kernel's end: let the SIMD arbiter favour them
-  if (chunk == 0) __builtin_amdgcn_s_setprio(KFX_INT_PRIO);
-#endif
   const int x = (tile % v.tiles_x) * 8 + (lane & 7);
   const int y = (tile / v.tiles_x) * 8 + (lane >> 3);
   const size_t base = (size_t)tile * v.tile_voxels() + lane;  // this column's (x, y, zb)
@@ -1693,40 +1492,23 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
   const DevPose P = s_pose;
   f3 vc, zs;
   int zl, zh, za, zb, z;
-  if (kPlan) {  // planned (k_int_plan): this chunk's range, lane intervals and start vc
-    const int2 r = v.prange[item];
-    za = r.x, zb = r.y;
-    if (za > zb) return;  // wave-uniform
-    const float4 ck = v.pckpt[(size_t)item * 64 + lane];
-    const unsigned zbits = __float_as_uint(ck.w);
-    zl = (int)(zbits & 0xFFFFu), zh = (int)(zbits >> 16);
-    vc = {ck.x, ck.y, ck.z};
-    zs = {P.R[2] * v.vs[0], P.R[5] * v.vs[0], P.R[8] * v.vs[0]};
-    z = za;
-  } else {
-    int_column(v, g, dl, P, x, y, vc, zs, zl, zh);
-    // The wave takes a chunk of the UNION of its lanes' intervals, so all 64
-    // lanes step the same z and each voxel load / store of the wave is one
-    // 128-B line (per-lane intervals put the lanes on different slices: one
-    // line per lane); a lane only updates voxels inside its own interval.
-    int wl = zl, wh = zh;
+  int_column(v, g, dl, P, x, y, vc, zs, zl, zh);
+  // The wave takes a chunk of the UNION of its lanes' intervals, so all 64
+  // lanes step the same z and each voxel load / store of the wave is one
+  // 128-B line (per-lane intervals put the lanes on different slices: one
+  // line per lane); a lane only updates voxels inside its own interval.
+  int wl = zl, wh = zh;
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      wl = min(wl, __shfl_xor(wl, off));
-      wh = max(wh, __shfl_xor(wh, off));
-    }
-    // the next frame's dispatch order (k_int_order) from this interval length
-    if (!kCount && chunk == 0 && lane == 0 && v.iwork) v.iwork[tile] = wh >= wl ? (unsigned)(wh - wl + 1) : 0u;
-    if (wh < wl || !int_chunk(v, KFX_INT_CHUNKR, chunk, nchunk, wl, wh, za, zb)) return;  // wave-uniform
-    z = 1;
-#if KFX_INT_EXP == 5  // timing experiment only (wrong values): no per-chunk replay
-    if (za > z) vc = add(vc, scl(zs, (float)(za - z)));
-    z = max(z, za);
-#else
-    vc = replay(vc, zs, z, za);
-    z = max(z, za);
-#endif
+  for (int off = 32; off > 0; off >>= 1) {
+    wl = min(wl, __shfl_xor(wl, off));
+    wh = max(wh, __shfl_xor(wh, off));
   }
+  // the next frame's dispatch order (k_int_order) from this interval length
+  if (!kCount && chunk == 0 && lane == 0 && v.iwork) v.iwork[tile] = wh >= wl ? (unsigned)(wh - wl + 1) : 0u;
+  if (wh < wl || !int_chunk(v, KFX_INT_CHUNKR, chunk, nchunk, wl, wh, za, zb)) return;  // wave-uniform
+  z = 1;
+  vc = replay(vc, zs, z, za);
+  z = max(z, za);
   const int la = max(za, zl), lb = min(zb, zh);  // this lane's voxels of the chunk
   const bool live = lb >= la;
   if (__all(!live)) return;
@@ -1734,7 +1516,7 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
   const float trunc = v.trunc;
   const float thres_color = trunc / 2;
   // kCount: updated, coloured, visited, gathered voxels; wave batches
-  unsigned cu = 0, cc = 0, cv = 0, cg = 0, cb = 0, cfu = 0, cfb = 0;  // + certified updates / batches
+  unsigned cu = 0, cc = 0, cv = 0, cg = 0, cb = 0;
   // negative tsdf this lane wrote: bricks gbs .. gbs+61 as bits, beyond as a z range
   const int gbs = za >> 3;
   unsigned long long nbm = 0ull;
@@ -1742,30 +1524,10 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
   using Mem = VoxMem<kIdx32>;
   using Idx = typename Mem::Idx;
   const Mem mem(v);
-#if KFX_INT_ZCLASS
-  // pixel offsets in 4-byte units: the gather reads the filtered depth map alone
-  constexpr unsigned kPixB = 4u, kPixSh = 2u;
-  const __amdgpu_buffer_rsrc_t rdm = make_rsrc(dmap, (unsigned)(4 * g.w * g.h));
-  const __amdgpu_buffer_rsrc_t riv = make_rsrc(invl, (unsigned)(4 * g.w * g.h));
-  // For a voxel whose rounded projection lies in the image, RN(1/lambda *
-  // |vc|) lies in [vc.z / cB, vc.z * cB]: its ray and its pixel's centre ray
-  // differ by <= 0.51 px, so lambda_v^2 - lambda_p^2 (and its negative) is at
-  // most ex (2 xmax + ex) + ey (2 ymax + ey), lambda_p >= 1; 1e-5 of relative
-  // margin covers the roundings of the table, sqrt_rn and the product.  The
-  // exact sdf is then >= d - vc.z cB and <= d - vc.z / cB.
-  const float zex = 0.51f / g.fx, zey = 0.51f / g.fy;
-  const float zxm = (fmaxf(g.cx, (float)g.w - 1.f - g.cx) + 0.51f) / g.fx;
-  const float zym = (fmaxf(g.cy, (float)g.h - 1.f - g.cy) + 0.51f) / g.fy;
-  const float zcb = sqrtf(1.f + zex * (2.f * zxm + zex) + zey * (2.f * zym + zey)) * 1.00001f;
-  const float zcbi = 1.f / zcb;
-  const float zfree = trunc + 1e-5f, zrej = -trunc - 1e-5f;
-  (void)dl;
-#else
   constexpr unsigned kPixB = 8u, kPixSh = 3u;
   const __amdgpu_buffer_rsrc_t rdl = make_rsrc(dl, (unsigned)(8 * g.w * g.h));
   (void)dmap;
   (void)invl;
-#endif
   constexpr Idx slice = 64;  // index step per z (tile-column layout)
   Idx iz = (Idx)base + (Idx)(za - v.zb) * slice;  // voxel index of (x, y, z)
   const bool fast = __all(!live || column_fast(vc, zs, v.Z));  // wave-uniform
@@ -1775,69 +1537,41 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
   // (memory-level parallelism); each voxel's arithmetic is exactly the
   // reference's (tsdf_volume.cu:56-98).
   constexpr int kB = KFX_INT_KB;
-#if KFX_INT_DEDUP == 2
-  unsigned dd_pix = kOob;  // the previous batch's last voxel: pixel and gathered value
-  float2 dd_d = make_float2(0.f, 0.f);
-#endif
-#if KFX_INT_CERT
-  // Free-space certification: bfac bounds RN(1/lambda * |vc|) /
-  // vc.z for any voxel whose rounded projection lies in the image (the voxel's
-  // ray and its pixel's centre ray differ by <= 0.51 px: lambda_v^2 -
-  // lambda_p^2 <= ex (2 tx + ex) + ey (2 ty + ey), lambda_p >= 1), with 1e-5 of
-  // relative margin for the roundings of the table, sqrt_rn and the product
-  const float cex = 0.51f / g.fx, cey = 0.51f / g.fy;
-  const float ctx = (fmaxf(g.cx, fw - 1.f - g.cx) + 0.51f) / g.fx;
-  const float cty = (fmaxf(g.cy, fh - 1.f - g.cy) + 0.51f) / g.fy;
-  const float cbfac = sqrtf(1.f + cex * (2.f * ctx + cex) + cey * (2.f * cty + cey)) * 1.00001f;
-  const float cneed = trunc + 1e-5f;
-  int cert_left = 0;  // wave-uniform: batches left in the certified group
-#endif
   for (; z <= zb; z += kB) {
     float sdf[kB];
     unsigned pix[kB];
     bool ok[kB];
-#if KFX_INT_CERT
-    if (cert_left == 0) {
-      // the next KFX_CERT_G slices of every lane that updates any of them are
-      // certified free space: in the image, in front of the camera, depth > 0
-      // and sdf >= trunc for every voxel (so ts = 1, no colour band)
-      const bool any = max(z, la) <= min(z + KFX_CERT_G - 1, lb);
-      if (__all(!any || cert_free(vc, zs, g, dl, cbfac, cneed))) cert_left = KFX_CERT_G / kB;
-    }
-    const bool fastg = cert_left > 0;
-    if (fastg) --cert_left;
-#else
-    constexpr bool fastg = false;
-#endif
     f3 p[kB];
 #pragma unroll
     for (int j = 0; j < kB; ++j) {
       vc = add(vc, zs);
       p[j] = vc;
     }
-    if (fastg) {  // certified free space: no projection, gather or sdf
-#pragma unroll
-      for (int j = 0; j < kB; ++j) {
-        ok[j] = (z + j >= la) & (z + j <= lb);
-        sdf[j] = 2.f * trunc;  // any value >= trunc gives ts = 1 and no colour band
-        pix[j] = ok[j] ? 0u : kOob;
-      }
-#if KFX_INT_DEDUP == 2
-      dd_pix = kOob;
-#endif
-    } else {
     // projection: ok = in the image in front of the camera (tsdf_volume.cu:56-66)
     if (fast) {  // the cheap exact sequences, two voxels per packed-FP32 op
       static_assert(kB % 2 == 0, "voxel pairs");
 #pragma unroll
       for (int j = 0; j < kB; j += 2) {
-        const pf2 pz = {p[j].z, p[j + 1].z}, px = {p[j].x, p[j + 1].x}, py = {p[j].y, p[j + 1].y};
+        const pf2 pz = {p[j].z, p[j + 1].z};
         const pf2 yv = rcp_rn2(pz);
-        const pf2 uu = div_rn2(px, pz, yv) * pf2{g.fx, g.fx} + pf2{g.cx, g.cx};
-        const pf2 vv = div_rn2(py, pz, yv) * pf2{g.fy, g.fy} + pf2{g.cy, g.cy};
+#if KFX_INT_PXY
+        // one voxel's {x, y} per packed op: the intrinsics are the pairs
+        // {fx, fy}, {cx, cy} (4 SGPRs shared with the IEEE path, not 8 more)
+        pf2 uu, vv;
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
-#if KFX_INT_ICHECK
+          const pf2 q = div_rn2(pf2{p[j + k].x, p[j + k].y}, pf2{pz[k], pz[k]}, pf2{yv[k], yv[k]}) *
+                            pf2{g.fx, g.fy} + pf2{g.cx, g.cy};
+          uu[k] = q.x;
+          vv[k] = q.y;
+        }
+#else
+        const pf2 px = {p[j].x, p[j + 1].x}, py = {p[j].y, p[j + 1].y};
+        const pf2 uu = div_rn2(px, pz, yv) * pf2{g.fx, g.fx} + pf2{g.cx, g.cx};
+        const pf2 vv = div_rn2(py, pz, yv) * pf2{g.fy, g.fy} + pf2{g.cy, g.cy};
+#endif
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
           // uu, vv are finite here (|vc| components in {0} u [2^-40, 2^40]);
           // the conversion saturates out-of-range values, so one unsigned
           // compare per axis is the float range test [0, w) of the rounded
@@ -1845,11 +1579,6 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
           const int iu = (int)rintf(uu[k]), iv = (int)rintf(vv[k]);
           ok[j + k] = (z + j + k >= la) & (z + j + k <= lb) & (pz[k] > 0) & ((unsigned)iu < (unsigned)g.w) & ((unsigned)iv < (unsigned)g.h);
           pix[j + k] = ok[j + k] ? __umul24((unsigned)iv, kPixB * (unsigned)g.w) + ((unsigned)iu << kPixSh) : kOob;
-#else
-          const float uf = rintf(uu[k]), vf = rintf(vv[k]);
-          ok[j + k] = (z + j + k >= la) & (z + j + k <= lb) & (pz[k] > 0) & (uf >= 0.f) & (uf < fw) & (vf >= 0.f) & (vf < fh);
-          pix[j + k] = ok[j + k] ? ((unsigned)(int)vf * (unsigned)g.w + (unsigned)(int)uf) * kPixB : kOob;
-#endif
         }
       }
     } else {  // IEEE division (tiny or huge operands)
@@ -1861,87 +1590,13 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
         pix[j] = ok[j] ? ((unsigned)(int)vf * (unsigned)g.w + (unsigned)(int)uf) * kPixB : kOob;
       }
     }
-#if KFX_INT_ZCLASS
-    // 4-B depth gathers; the vc.z bound settles free space (sdf >= trunc: ts =
-    // 1, no colour band) and voxels far behind the surface (sdf < -trunc); only
-    // voxels near +-trunc gather 1/lambda and take the exact sdf
-    float dd[kB];
-#pragma unroll
-    for (int j = 0; j < kB; ++j) dd[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rdm, pix[j], 0, 0));
-    bool bnd[kB];
-    bool banyl = false;
-#pragma unroll
-    for (int j = 0; j < kB; ++j) {
-      const bool fr = fmaf(-p[j].z, zcb, dd[j]) >= zfree;
-      const bool rj = fmaf(-p[j].z, zcbi, dd[j]) < zrej;
-      bnd[j] = ok[j] & (dd[j] > 0.f) & !fr & !rj;
-      sdf[j] = fr ? 2.f * trunc : -2.f * trunc;
-      banyl |= bnd[j];
-    }
-    if (__any(banyl)) {  // exact sdf (tsdf_volume.cu:67-68) of the voxels near +-trunc
-      float il[kB], n2[kB];
-#pragma unroll
-      for (int j = 0; j < kB; ++j) {
-        il[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(riv, bnd[j] ? pix[j] : kOob, 0, 0));
-        n2[j] = dot(p[j], p[j]);
-      }
-      if (fast) {
-#pragma unroll
-        for (int j = 0; j < kB; j += 2) {
-          const pf2 sd = -(pf2{il[j], il[j + 1]} * sqrt_rn2(pf2{n2[j], n2[j + 1]}) - pf2{dd[j], dd[j + 1]});
-          if (bnd[j]) sdf[j] = sd.x;
-          if (bnd[j + 1]) sdf[j + 1] = sd.y;
-        }
-      } else {
-#pragma unroll
-        for (int j = 0; j < kB; ++j)
-          if (bnd[j]) sdf[j] = -(il[j] * sqrtf(n2[j]) - dd[j]);
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < kB; ++j) ok[j] = ok[j] & (dd[j] > 0) & (sdf[j] >= -trunc);
-    }
-#else
     float2 d[kB];
     float n2[kB];
 #pragma unroll
     for (int j = 0; j < kB; ++j) n2[j] = dot(p[j], p[j]);
-#if KFX_INT_DEDUP
-    // consecutive voxels of a column often project to the same pixel: such a
-    // voxel reuses the previous one's {depth, 1/lambda} instead of gathering
-    // it (its lane issues no cache request: kOob), cutting L1/L2 gather lines
-    unsigned gpix[kB];
-#if KFX_INT_DEDUP == 2  // also against the previous batch's last voxel
-    gpix[0] = pix[0] == dd_pix ? kOob : pix[0];
-#else
-    gpix[0] = pix[0];
-#endif
-#pragma unroll
-    for (int j = 1; j < kB; ++j) gpix[j] = pix[j] == pix[j - 1] ? kOob : pix[j];
 #pragma unroll
     for (int j = 0; j < kB; ++j)
-      d[j] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rdl, gpix[j], 0, 0));
-#if KFX_INT_DEDUP == 2
-    if (pix[0] == dd_pix) d[0] = dd_d;
-#endif
-#pragma unroll
-    for (int j = 1; j < kB; ++j)
-      if (pix[j] == pix[j - 1]) d[j] = d[j - 1];
-#if KFX_INT_DEDUP == 2
-    dd_pix = pix[kB - 1];
-    dd_d = d[kB - 1];
-#endif
-#else
-#pragma unroll
-    for (int j = 0; j < kB; ++j)
-#if KFX_INT_EXP == 4  // timing experiment only (wrong values): no depth gathers
-      d[j] = make_float2(pix[j] == kOob ? 0.f : 2.0f, 1.0f);
-#elif KFX_INT_EXP == 1  // timing experiment only (wrong values): contiguous gather addresses
-      d[j] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rdl, pix[j] == kOob ? kOob : 8u * (unsigned)lane + 4096u * (unsigned)j, 0, 0));
-#else
       d[j] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rdl, pix[j], 0, 0));
-#endif
-#endif
     // sdf and the depth test (tsdf_volume.cu:67-71)
     if (fast) {
 #pragma unroll
@@ -1956,16 +1611,9 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
     }
 #pragma unroll
     for (int j = 0; j < kB; ++j) ok[j] = ok[j] & (d[j].x > 0) & (sdf[j] >= -trunc);
-    }
-#endif
     if (kCount) {
       iz += (Idx)kB * slice;
       ++cb;
-      if (fastg) {
-        ++cfb;
-#pragma unroll
-        for (int j = 0; j < kB; ++j) cfu += ok[j];
-      }
 #pragma unroll
       for (int j = 0; j < kB; ++j) {
         cv += (z + j >= la) & (z + j <= lb);
@@ -1988,18 +1636,10 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
     for (int j = 0; j < kB; ++j) {
       vi[j] = iz + (Idx)j * slice;
       const Idx i = ok[j] ? vi[j] : Mem::kNone;
-#if KFX_INT_EXP == 2  // timing experiment only (wrong values): no voxel loads
-      t0[j] = 0;
-      w0[j] = (int16_t)(i == Mem::kNone ? 0 : 0);
-#else
       t0[j] = mem.ld_t(i);
       w0[j] = mem.ld_w(i);
-#endif
     }
     iz += (Idx)kB * slice;
-#if KFX_INT_LEAN & 2
-    unsigned negm = 0u;  // voxels of this batch written with a negative tsdf
-#endif
 #pragma unroll
     for (int j = 0; j < kB; ++j) {
       // saturated free space (w = 64 at the tsdf fixed point T* of a ts = 1
@@ -2014,9 +1654,6 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
       const float new_t = div_rn(fmaf(pre_t, (float)pre_w, ts), (float)(pre_w + 1), rtab[pre_w + 1]);
       int q = (int)(new_t * (float)kShortMax);
       q = max(-kShortMax, min(kShortMax, q));
-#if KFX_INT_LEAN & 2
-      negm |= q < 0 ? 1u << j : 0u;  // marked after the batch (rare)
-#else
       if (q < 0) {
         const int k = ((z + j) >> 3) - gbs;
         if (k < 62) {
@@ -2026,17 +1663,10 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
           nhi = max(nhi, z + j);
         }
       }
-#endif
       // saturated voxels (w = 64 at a tsdf fixed point) keep their values:
       // skipping those stores changes nothing and saves write bandwidth
-#if KFX_INT_EXP != 3  // 3: timing experiment only (wrong values): no tsdf/weight stores
-#if KFX_INT_LEAN & 1
-      mem.st_t(i, (int16_t)q);  // (an unchanged value rewritten: no compare, no branch)
-#else
       if (q != t0[j]) mem.st_t(i, (int16_t)q);
-#endif
       if (new_w != pre_w) mem.st_w(i, (int16_t)new_w);
-#endif
       if (sdf[j] <= thres_color && sdf[j] >= -thres_color) {  // colour band (rare)
         const uint32_t c0 = mem.ld_c(i);
         const uint8_t *px = bgr + 3 * (size_t)(pix[j] >> kPixSh);
@@ -2052,21 +1682,6 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
         if (out != c0) mem.st_c(i, out);
       }
     }
-#if KFX_INT_LEAN & 2
-    if (negm) {  // (rare) the occupancy marks of the negative voxels
-#pragma unroll
-      for (int j = 0; j < kB; ++j)
-        if ((negm >> j) & 1u) {
-          const int k = ((z + j) >> 3) - gbs;
-          if (k < 62) {
-            nbm |= 1ull << k;
-          } else {
-            nlo = min(nlo, z + j);
-            nhi = max(nhi, z + j);
-          }
-        }
-    }
-#endif
   }
   if (!kCount) {  // raycast skip maps
 #pragma unroll
@@ -2093,11 +1708,7 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
     atomicAdd(&counters[2 * sh + 1], (unsigned long long)cc);
     atomicAdd(&counters[32 + sh], (unsigned long long)cv);
     atomicAdd(&counters[48 + sh], (unsigned long long)cg);
-    atomicAdd(&counters[80 + sh], (unsigned long long)cfu);
-    if (lane == 0) {  // per-wave counts (wave-uniform)
-      atomicAdd(&counters[64 + sh], (unsigned long long)cb);
-      atomicAdd(&counters[96 + sh], (unsigned long long)cfb);
-    }
+    if (lane == 0) atomicAdd(&counters[64 + sh], (unsigned long long)cb);  // per-wave count (wave-uniform)
   }
 }
 
@@ -2373,9 +1984,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KFX_RAY_OCC
     // after the candidate sample from the saved state — same samples, same
     // order, same result.
     bool cand = false;
-#if KFX_RAY_PRIO
-    int wave_batches = 0;  // wave-uniform
-#endif
     f3 cvert = {0.f, 0.f, 0.f}, r_nextp = nextp;
     float cts = 0.f;  // the candidate's Ts (slab payload)
     float r_rl = 0.f, r_tprev = 0.f;
@@ -2455,40 +2063,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KFX_RAY_OCC
           // tfar (2 steps of margin over the accumulated rounding)
           pf2 pxy = {nextp.x, nextp.y}, pzr = {nextp.z, ray_len};
           const pf2 sxy = {vstep.x, vstep.y}, szr = {vstep.z, rc.step};
-#ifdef KFX_RAY_NOREPLAY  // timing experiment only (wrong values): jump instead of replay
-          const int nf = 0;
-          pxy = pxy + sxy * pf2{(float)(n - 1), (float)(n - 1)};
-          pzr = pzr + szr * pf2{(float)(n - 1), (float)(n - 1)};
-          if (true) {
-            if (!(pzr.y < tfar)) live = false;
-            pxy = pxy + sxy;
-            pzr = pzr + szr;
-            nextp = {pxy.x, pxy.y, pzr.x};
-            ray_len = pzr.y;
-            nsk += (uint32_t)n;
-            if (!live) break;
-            continue;
-          }
-#else
           const int nf = min(n, max(0, (int)((tfar - ray_len) * rstep) - 2));
-#endif
           int i = 0;
-#if KFX_RAY_SREPLAY  // four scalar add chains (see replay_add)
-          {
-            float px = pxy.x, py = pxy.y, pz = pzr.x, pr = pzr.y;
-            for (; i + 8 <= nf; i += 8) {
-#pragma unroll
-              for (int u = 0; u < 8; ++u) {
-                asm volatile("v_add_f32 %0, %0, %1" : "+v"(px) : "v"(sxy.x));
-                asm volatile("v_add_f32 %0, %0, %1" : "+v"(py) : "v"(sxy.y));
-                asm volatile("v_add_f32 %0, %0, %1" : "+v"(pz) : "v"(szr.x));
-                asm volatile("v_add_f32 %0, %0, %1" : "+v"(pr) : "v"(szr.y));
-              }
-            }
-            pxy = {px, py};
-            pzr = {pz, pr};
-          }
-#else
           for (; i + 8 <= nf; i += 8) {
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
@@ -2496,7 +2072,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KFX_RAY_OCC
               pzr = pzr + szr;
             }
           }
-#endif
           for (; i < nf; ++i) {
             pxy = pxy + sxy;
             pzr = pzr + szr;
@@ -2521,11 +2096,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KFX_RAY_OCC
         }
       }
       if (!__any(live)) break;
-#if KFX_RAY_PRIO
-      // waves still marching after KFX_RAY_PRIO batches are the kernel's tail:
-      // the SIMD arbiter favours them from then on
-      if (++wave_batches == KFX_RAY_PRIO) __builtin_amdgcn_s_setprio(2);
-#endif
       int16_t raw[kR];
       unsigned pm = 0u, nm = 0u, am = 0u, ownm = 0u;
       if (kStats || kTrace) st_batches += live ? 1u : 0u;
@@ -2647,11 +2217,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KFX_RAY_OCC
 #endif
     if (cand) {  // the wave's normal pass
       cand = false;
-#ifdef KFX_RAY_NONORMAL  // timing experiment only (wrong values)
-      const f3 n = {cvert.x, 0.5f, 0.5f};
-#else
       const f3 n = compute_normal<kIdx32 && KFX_RAY_N32>(v, rc, cvert);
-#endif
       if (!isnan(n.x * n.y * n.z)) {
         // Rinv re-read from LDS here (volatile LDS reads: not held in
         // registers through the march; a generic volatile pointer would
@@ -3488,26 +3054,6 @@ IcpPlan make_icp_plan(int levels, const LevelGeom *g, const int *iters, FrameVie
     pl.slots += iters[l];
   }
   pl.nblocks = std::max(pl.nblocks, 1);
-#if KFX_ICP_XCOARSE
-  // coarse levels on the fewest XCD groups whose blocks hold them at their
-  // pixels per lane (KFX_ICP_XCOARSE = 1: level 2 only, 2: levels 2 and 1)
-  const int per_group = (pl.nblocks + 7) / 8;  // blocks of one residue mod 8
-  for (int l = std::max(1, levels - KFX_ICP_XCOARSE); l < levels; ++l) {
-    int ppl = pl.ppl[l], gr = pl.groups[l];
-    int nx = (gr + per_group - 1) / per_group;
-    const int nx_max = l == levels - 1 ? 1 : 2;  // the coarsest level on one XCD, the next on two
-    while (nx > nx_max && ppl < kIcpPix) {  // more pixels per lane until it fits
-      ++ppl;
-      gr = (pl.npix[l] + kIcpThreads * ppl - 1) / (kIcpThreads * ppl);
-      nx = (gr + per_group - 1) / per_group;
-    }
-    if (nx < 8) {
-      pl.ppl[l] = ppl;
-      pl.groups[l] = gr;
-      pl.xgroups[l] = nx;
-    }
-  }
-#endif
   return pl;
 }
 
@@ -3611,12 +3157,8 @@ int integrate_chunks(const VolView &v) {
   const int tiles = v.tiles_x * v.tiles_y;
   if (integrate_mode(v) == 1) return std::max(1, std::min(KFX_INT_NC, v.zn / 32));  // chunks of >= 32 slices
   // z-chunks so that >= KFX_INT_WAVES waves exist (12 per SIMD on 1024 SIMDs)
-  const int waves = KFX_INT_PLAN ? KFX_INT_PWAVES : KFX_INT_WAVES;
-  return std::max(1, std::min(KFX_INT_MAXCHUNK, (waves + tiles - 1) / tiles));
+  return std::max(1, std::min(KFX_INT_MAXCHUNK, (KFX_INT_WAVES + tiles - 1) / tiles));
 }
-
-// k_int_plan is used where a tile has several chunks (the per-chunk replay it removes)
-bool integrate_planned(const VolView &v) { return KFX_INT_PLAN && integrate_chunks(v) > 1 && v.Z < 65535; }
 
 // Longest-first dispatch order of k_integrate's (tile, chunk) items for the
 // next frame (VolView::iadapt): item c of tile t is one of ct(len_t) capped
@@ -3678,21 +3220,8 @@ void launch_integrate(hipStream_t s, VolView v, LevelGeom g0, const float2 *dl0,
   const int nchunk = integrate_chunks(v);
   v.inchunk = nchunk;
   v.iadapt = integrate_mode(v);
-#if !KFX_INT_LPT
   if (!v.iadapt) v.iperm = nullptr, v.iwork = nullptr;  // geometric chunks in block order
-#endif
   if (counters) v.iwork = nullptr;  // the count-only pass leaves the order alone
-#if KFX_INT_LPT
-  // every mode dispatches its items longest first (by the last frame's intervals)
-  if (counters) v.iperm = nullptr;  // the count-only pass keeps block order
-#endif
-  const bool planned = integrate_planned(v) && v.prange && v.pckpt;
-  if (planned) {
-    hipLaunchKernelGGL(k_int_plan, dim3(tiles), dim3(64), 0, s, v, g0, dl0, st, log, vpose, xpose,
-                       v.iwork ? 1 : 0);
-  } else {
-    v.prange = nullptr, v.pckpt = nullptr;
-  }
   dim3 grd(tiles * nchunk);  // one wave (block) per (tile, chunk) item
   const bool idx32 = v.local_voxels() < (1ull << 31);  // 32-bit tsdf/weight byte offsets
 #ifdef KFX_INT_TRACE
@@ -3704,32 +3233,21 @@ void launch_integrate(hipStream_t s, VolView v, LevelGeom g0, const float2 *dl0,
   g_int_trace_waves = (int)grd.x;
   (void)hipMemsetAsync(trace_buf, 0, sizeof(unsigned long long) * 4 * g_int_trace_waves, s);  // waves that exit early write none
   if (!counters) {
-    if (planned)
-      hipLaunchKernelGGL((k_integrate<false, true, true>), grd, dim3(KFX_INT_BLOCK), 0, s, v, g0, dl0, dmap, invl, bgr, st,
-                         log, vpose, xpose, trace_buf);
-    else
-      hipLaunchKernelGGL((k_integrate<false, true, false>), grd, dim3(KFX_INT_BLOCK), 0, s, v, g0, dl0, dmap, invl, bgr, st,
-                         log, vpose, xpose, trace_buf);
+    hipLaunchKernelGGL((k_integrate<false, true>), grd, dim3(KFX_INT_BLOCK), 0, s, v, g0, dl0, dmap, invl, bgr, st,
+                       log, vpose, xpose, trace_buf);
     return;
   }
 #endif
-#define KFX_LAUNCH_INT(C, I, P)                                                                             \
-  hipLaunchKernelGGL((k_integrate<C, I, P>), grd, dim3(KFX_INT_BLOCK), 0, s, v, g0, dl0, dmap, invl, bgr, st, log, vpose, xpose, \
+#define KFX_LAUNCH_INT(C, I)                                                                             \
+  hipLaunchKernelGGL((k_integrate<C, I>), grd, dim3(KFX_INT_BLOCK), 0, s, v, g0, dl0, dmap, invl, bgr, st, log, vpose, xpose, \
                      counters)
-  if (counters) {
-    if (planned) KFX_LAUNCH_INT(true, false, true);
-    else KFX_LAUNCH_INT(true, false, false);
-  } else if (idx32) {
-    if (planned) KFX_LAUNCH_INT(false, true, true);
-    else KFX_LAUNCH_INT(false, true, false);
-  } else {
-    if (planned) KFX_LAUNCH_INT(false, false, true);
-    else KFX_LAUNCH_INT(false, false, false);
-  }
+  if (counters) KFX_LAUNCH_INT(true, false);
+  else if (idx32) KFX_LAUNCH_INT(false, true);
+  else KFX_LAUNCH_INT(false, false);
 #undef KFX_LAUNCH_INT
   if (!counters && v.iwork && v.iperm)
     hipLaunchKernelGGL(k_int_order, dim3(1), dim3(1024), 0, s, v.iwork, v.iperm, tiles, nchunk, v.zn, v.iadapt,
-                       planned ? KFX_INT_PCHUNKR : KFX_INT_CHUNKR);
+                       KFX_INT_CHUNKR);
 }
 
 #ifdef KFX_RAY_TRACE

@@ -461,8 +461,7 @@ class KinectFusion:
         """Work of the last frame's integrate: updated / coloured / visited / gathered voxels."""
         a = (C.c_int64 * 8)()
         _check(lib().kfx_integrate_stats(self._h, a), "kfx_integrate_stats")
-        return dict(zip(["updated", "colored", "visited", "gathered", "wave_batches", "cert_updated",
-                         "cert_batches"], a[:7]))
+        return dict(zip(["updated", "colored", "visited", "gathered", "wave_batches"], a[:5]))
 
     def raycast_stats(self) -> dict:
         """Work of the last frame's raycast (re-run, nothing written)."""

@@ -55,3 +55,19 @@ def test_create_rejects_bad_arguments(kfx_lib):
     good = Intrinsics(320, 240, 262.5, 262.5, 159.5, 119.5)
     assert kfx_lib.lib().kfx_create(C.byref(good), C.byref(p2), 0, C.byref(h)) == -1
     assert b"multiples of 8" in kfx_lib.lib().kfx_last_error()
+
+
+def test_product_build_refuses_experiment_macros():
+    """make ARCH=gfx950 with -DKFX_* macros is refused for the product library
+    (experiments build into lib/var_<name>), and the shipped kernel source holds
+    none of the dropped experiment switches."""
+    import subprocess
+    pkg = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "slam-kinectfusion_amd")
+    r = subprocess.run(["make", "-n", "-C", pkg, "ARCH=gfx950", "EXTRA=-DKFX_INT_CERT=1"],
+                       capture_output=True, text=True)
+    assert r.returncode != 0 and "var_" in (r.stdout + r.stderr)
+    src = open(os.path.join(pkg, "csrc", "kfx_kernels.hip")).read()
+    for m in ("KFX_INT_ZCLASS", "KFX_INT_CERT", "KFX_INT_DEDUP", "KFX_INT_LEAN", "KFX_INT_PLAN", "KFX_INT_PRIO",
+              "KFX_RAY_PRIO", "KFX_ICP_XCOARSE", "KFX_INT_EXP", "KFX_PLAN_EXP", "KFX_RAY_NOREPLAY",
+              "KFX_RAY_NONORMAL", "wrong values"):
+        assert m not in src, m
