@@ -725,21 +725,6 @@ VolView make_vol(const kfx_params &p, int rank, int world, const int *cuts = nul
   }
   v.trunc = p.volu_trun_dist;
   v.inv_trunc = 1.f / v.trunc;
-  // tsdf fixed point T* of the saturated free-space update (w = 64, ts = 1),
-  // iterated with the kernel's exact operations (tsdfhelper, tsdf_volume.cu:76-81)
-  v.tsat = 1 << 20;  // none
-  int t = 32767;
-  for (int it = 0; it < 64; ++it) {
-    const float pre_t = (float)t * 0.0000305185f;
-    const float new_t = std::fma(pre_t, 64.f, 1.f) / 65.f;
-    int q = (int)(new_t * 32767.f);
-    q = std::max(-32767, std::min(32767, q));
-    if (q == t) {
-      v.tsat = t;
-      break;
-    }
-    t = q;
-  }
   return v;
 }
 

@@ -103,7 +103,6 @@ struct VolView {
   float range[3];  // volume_range
   float trunc;
   float inv_trunc;  // RN(1/trunc), for the exact FMA division (kfx_kernels.hip div_rn)
-  int tsat;         // tsdf fixed point of a weight-64, ts = 1 update (integrate skip), or 1<<20
   size_t slice;    // voxels per z slice (= X*Y)
   // Dilated occupancy of negative tsdf (raycast empty-space skipping, DESIGN.md
   // §4): bit set <=> some voxel within one brick of this brick may hold a

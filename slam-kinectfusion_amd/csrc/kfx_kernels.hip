@@ -54,9 +54,6 @@
 #ifndef KFX_FF_MIN
 #define KFX_FF_MIN 768  // fast-forward replays of at least this many adds (shorter ones: the adds; A/B r3m: 384 costs C2 +8 %)
 #endif
-#ifndef KFX_INT_PXY
-#define KFX_INT_PXY 0  // integrate fast projection: packed {x, y} of one voxel (A/B)
-#endif
 #ifndef KFX_INT_WAVES
 #define KFX_INT_WAVES 12288  // integrate: target wave count (z-chunks per column tile; C2: 3 chunks of 4096 tiles)
 #endif
@@ -1506,6 +1503,10 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
   // the next frame's dispatch order (k_int_order) from this interval length
   if (!kCount && chunk == 0 && lane == 0 && v.iwork) v.iwork[tile] = wh >= wl ? (unsigned)(wh - wl + 1) : 0u;
   if (wh < wl || !int_chunk(v, KFX_INT_CHUNKR, chunk, nchunk, wl, wh, za, zb)) return;  // wave-uniform
+  // (uniform by construction: tell the compiler, so that the z loop and the
+  // replay run on the scalar unit)
+  za = __builtin_amdgcn_readfirstlane(za);
+  zb = __builtin_amdgcn_readfirstlane(zb);
   z = 1;
   vc = replay(vc, zs, z, za);
   z = max(z, za);
@@ -1554,29 +1555,19 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
       for (int j = 0; j < kB; j += 2) {
         const pf2 pz = {p[j].z, p[j + 1].z};
         const pf2 yv = rcp_rn2(pz);
-#if KFX_INT_PXY
-        // one voxel's {x, y} per packed op: the intrinsics are the pairs
-        // {fx, fy}, {cx, cy} (4 SGPRs shared with the IEEE path, not 8 more)
-        pf2 uu, vv;
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-          const pf2 q = div_rn2(pf2{p[j + k].x, p[j + k].y}, pf2{pz[k], pz[k]}, pf2{yv[k], yv[k]}) *
-                            pf2{g.fx, g.fy} + pf2{g.cx, g.cy};
-          uu[k] = q.x;
-          vv[k] = q.y;
-        }
-#else
         const pf2 px = {p[j].x, p[j + 1].x}, py = {p[j].y, p[j + 1].y};
         const pf2 uu = div_rn2(px, pz, yv) * pf2{g.fx, g.fx} + pf2{g.cx, g.cx};
         const pf2 vv = div_rn2(py, pz, yv) * pf2{g.fy, g.fy} + pf2{g.cy, g.cy};
-#endif
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
-          // uu, vv are finite here (|vc| components in {0} u [2^-40, 2^40]);
-          // the conversion saturates out-of-range values, so one unsigned
-          // compare per axis is the float range test [0, w) of the rounded
-          // value; 24-bit multiply (w, h < 2^24)
-          const int iu = (int)rintf(uu[k]), iv = (int)rintf(vv[k]);
+          // uu, vv are finite here (|vc| components in {0} u [2^-40, 2^40]).
+          // rintf by the 1.5 * 2^23 bias: for |u| < 2^22 the biased sum has
+          // ulp 1 and its integer (ties to even: the bias is even) is
+          // rintf(u); u >= 2^22 unbiases to >= 2^22, u <= -2^22 to a negative
+          // value, so one unsigned compare per axis is still the range test
+          // [0, w) of rintf(u); 24-bit multiply (w, h < 2^24)
+          const int iu = (int)(__float_as_uint(uu[k] + 12582912.f) - 0x4B400000u);
+          const int iv = (int)(__float_as_uint(vv[k] + 12582912.f) - 0x4B400000u);
           ok[j + k] = (z + j + k >= la) & (z + j + k <= lb) & (pz[k] > 0) & ((unsigned)iu < (unsigned)g.w) & ((unsigned)iv < (unsigned)g.h);
           pix[j + k] = ok[j + k] ? __umul24((unsigned)iv, kPixB * (unsigned)g.w) + ((unsigned)iu << kPixSh) : kOob;
         }
@@ -1601,7 +1592,9 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
     if (fast) {
 #pragma unroll
       for (int j = 0; j < kB; j += 2) {
-        const pf2 sd = -(pf2{d[j].y, d[j + 1].y} * sqrt_rn2(pf2{n2[j], n2[j + 1]}) - pf2{d[j].x, d[j + 1].x});
+        // d - il |vc| = -(il |vc| - d) exactly (RN is odd-symmetric); only the
+        // sign of a zero sdf can differ, and no result depends on it
+        const pf2 sd = pf2{d[j].x, d[j + 1].x} - pf2{d[j].y, d[j + 1].y} * sqrt_rn2(pf2{n2[j], n2[j + 1]});
         sdf[j] = sd.x;
         sdf[j + 1] = sd.y;
       }
@@ -1640,20 +1633,30 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
       w0[j] = mem.ld_w(i);
     }
     iz += (Idx)kB * slice;
+    // The update arithmetic of all kB voxels, two voxels per packed op and
+    // without branches (voxels that do not pass compute values nobody
+    // stores).  A saturated voxel (w = 64 at the tsdf fixed point T* of a
+    // ts = 1 update, sdf >= trunc) needs no test: its update reproduces the
+    // stored values, so the changed-value tests below skip its stores.
+    int qv[kB];
+#pragma unroll
+    for (int j = 0; j < kB; j += 2) {
+      const pf2 tq = div_rn2(pf2{sdf[j], sdf[j + 1]}, pf2{trunc, trunc}, pf2{v.inv_trunc, v.inv_trunc});
+      const pf2 ts = {fminf(1.f, tq.x), fminf(1.f, tq.y)};
+      const pf2 pt = pf2{(float)t0[j], (float)t0[j + 1]} * pf2{kDivShortMax, kDivShortMax};
+      const pf2 pw = {(float)w0[j], (float)w0[j + 1]};
+      const pf2 nt = div_rn2(pfma(pt, pw, ts), pw + pf2{1.f, 1.f}, pf2{rtab[w0[j] + 1], rtab[w0[j + 1] + 1]}) *
+                     pf2{(float)kShortMax, (float)kShortMax};
+#pragma unroll
+      for (int k = 0; k < 2; ++k) qv[j + k] = max(-kShortMax, min(kShortMax, (int)nt[k]));
+    }
 #pragma unroll
     for (int j = 0; j < kB; ++j) {
-      // saturated free space (w = 64 at the tsdf fixed point T* of a ts = 1
-      // update, sdf >= trunc so ts = 1 and no colour band): the update is
-      // the identity — skip it (same stores skipped as below)
-      if (!ok[j] || (w0[j] == kMaxWeight && t0[j] == v.tsat && sdf[j] >= trunc)) continue;
+      if (!ok[j]) continue;
       const Idx i = vi[j];
       const int pre_w = w0[j];
-      const float ts = fminf(1.f, div_rn(sdf[j], trunc, v.inv_trunc));
-      const float pre_t = (float)t0[j] * kDivShortMax;
       const int new_w = min(pre_w + 1, kMaxWeight);
-      const float new_t = div_rn(fmaf(pre_t, (float)pre_w, ts), (float)(pre_w + 1), rtab[pre_w + 1]);
-      int q = (int)(new_t * (float)kShortMax);
-      q = max(-kShortMax, min(kShortMax, q));
+      const int q = qv[j];
       if (q < 0) {
         const int k = ((z + j) >> 3) - gbs;
         if (k < 62) {

@@ -3,6 +3,7 @@
 # one-shot job files.  Jobs run in order; each GPU step has its own time limit
 # and the first failure ends the call (no retries):
 #   tests[=EXPR]      pytest -m gpu (-k EXPR)            -> gpurun_out/tests.log
+#   vtests=VAR:EXPR   pytest -m gpu -k EXPR on the variant lib/var_VAR
 #   smoke             __graft_entry__.smoke()
 #   bench[=ARGS]      bench.py (ARGS comma-separated; default: the driver's
 #                     --steps 20 --warmup 5)              -> gpurun_out/bench.json
@@ -37,6 +38,14 @@ for job in "$@"; do
       rc=$?
       tail -n 3 gpurun_out/tests.log
       [ $rc -eq 0 ] || { grep -E "FAILED|Error" gpurun_out/tests.log | head -20; exit $rc; } ;;
+    vtests)
+      V=${val%%:*}; E=${val#*:}
+      echo "=== vtests $V"
+      KFX_LIB_PATH=$PWD/slam-kinectfusion_amd/lib/var_$V/libkfx.so timeout -k 10 900 python3 -u -m pytest -x -q \
+        --timeout 300 --timeout-method thread -m gpu tests -k "$E" > gpurun_out/vtests_$V.log 2>&1
+      rc=$?
+      tail -n 2 gpurun_out/vtests_$V.log
+      [ $rc -eq 0 ] || { grep -E "FAILED|Error" gpurun_out/vtests_$V.log | head -20; exit $rc; } ;;
     smoke)
       step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)
