@@ -14,6 +14,7 @@
 #include <opencv2/core/affine.hpp>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <fstream>
 #include <iostream>
@@ -117,7 +118,12 @@ class kinectfusion {
   ~kinectfusion() { release(); }
 
   // kinectfusion.cpp:78-127.  Depth is CV_32FC1 millimetres (depth_sensor.cpp:191) or CV_16UC1.
+  // A tracked frame prints the reference's "Frame:N||Time:Xms" line
+  // (kinectfusion.cpp:122-123: wall time of the whole call) and keeps it in
+  // frame_time; the bootstrap frame and a dropped frame print nothing else.
   void pipeline(cv::Mat cmap_, cv::Mat dmap_) {
+    const auto start_time = std::chrono::system_clock::now();
+    const int count = frame_count;
     cv::Mat c = cmap_.isContinuous() ? cmap_ : cmap_.clone();
     cv::Mat d = dmap_.isContinuous() ? dmap_ : dmap_.clone();
     int rc;
@@ -128,6 +134,11 @@ class kinectfusion {
     if (rc == KFX_TRACKING_LOST) std::cout << "tracking fail!" << std::endl;  // kinectfusion.cpp:99
     else if (rc != KFX_OK) throw std::runtime_error(kfx_last_error());
     sync_host_state();
+    if (rc == KFX_OK && count > 1) {
+      const std::chrono::duration<double, std::milli> ms = std::chrono::system_clock::now() - start_time;
+      frame_time = std::to_string(ms.count());
+      std::cout << "Frame:" << count << "||Time:" << ms.count() << "ms" << std::endl;
+    }
   }
   void reset() {
     kfx_reset(ctx_);
@@ -168,10 +179,20 @@ class kinectfusion {
   std::vector<cv::Affine3f> pose_record;
 
  private:
+  // pose_record mirrors the device log: a tracked frame appends one pose (only
+  // that pose is read), the bootstrap frame none; a reset (the log shrank)
+  // re-reads the whole record.
   void sync_host_state() {
     kfx_get_frame_count(ctx_, &frame_count);
     int n = 0;
     kfx_get_pose_record(ctx_, nullptr, 0, &n);
+    if (n == (int)pose_record.size()) return;
+    if (n == (int)pose_record.size() + 1) {
+      kfx_pose p;
+      if (kfx_get_cur_camera_pose(ctx_, &p) != KFX_OK) throw std::runtime_error(kfx_last_error());
+      pose_record.push_back(from_kfx(p));
+      return;
+    }
     std::vector<kfx_pose> ps(n);
     kfx_get_pose_record(ctx_, ps.data(), n, &n);
     pose_record.clear();

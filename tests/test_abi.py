@@ -71,3 +71,24 @@ def test_product_build_refuses_experiment_macros():
               "KFX_RAY_PRIO", "KFX_ICP_XCOARSE", "KFX_INT_EXP", "KFX_PLAN_EXP", "KFX_RAY_NOREPLAY",
               "KFX_RAY_NONORMAL", "wrong values"):
         assert m not in src, m
+
+
+def test_adapter_header_compiles_and_links(tmp_path):
+    """adapter/kinectfusion.h (the reference's kf::kinectfusion over the C-ABI)
+    compiled with a main.cpp-like driver against stand-ins for the few OpenCV
+    core types it uses (OpenCV is not in this image) and linked to libkfx.so.
+    Without a GPU the program reports the missing device and exits 2."""
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    stub = os.path.join(root, "tests", "adapter_stub")
+    lib = os.path.join(root, "slam-kinectfusion_amd", "lib")
+    exe = str(tmp_path / "main_like")
+    r = subprocess.run(["g++", "-std=c++17", "-Wall", "-Werror", "-I", stub,
+                        "-I", os.path.join(root, "slam-kinectfusion_amd", "adapter"),
+                        os.path.join(stub, "main_like.cpp"), "-o", exe, "-L", lib, "-lkfx",
+                        f"-Wl,-rpath,{lib}"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    import torch
+    if not torch.cuda.is_available():
+        p = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+        assert p.returncode == 2 and "kinectfusion:" in p.stderr

@@ -11,6 +11,7 @@
 #   prof[=ARGS]       tools/prof.sh (rocprofv3 stats + PMC passes)
 #   slab=c4|c5        tools/slab_record.py (8 slabs on one GPU)
 #   ab=ROUNDS:V1:V2   tools/ab_quick.sh ROUNDS V1 V2 ... (alternating variants)
+#   pmcv=V1:V2        SQ instruction counters of k_integrate per variant (tools/pmc_var.sh)
 # e.g.  gpurun -- bash tools/gpu.sh tests bench quick=--config,c5
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}" || exit 1
@@ -66,6 +67,9 @@ for job in "$@"; do
       tail -n 5 gpurun_out/slab_$val.log ;;
     ab)
       step ab 1200 bash tools/ab_quick.sh $(echo "$val" | tr ':' ' ') ;;
+    pmcv)
+      mkdir -p gpurun_out/pmcv
+      step pmcv 900 bash tools/pmc_var.sh "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_LDS" $(echo "$val" | tr ':' ' ') ;;
     *)
       echo "unknown job $job"; exit 2 ;;
   esac
