@@ -184,6 +184,8 @@ struct kfx_ctx {
   hipStream_t cstream = nullptr;
   ncclComm_t comm = nullptr;      // RCCL communicator over the slab ranks (one process per GPU)
   hipEvent_t xev[5]{};            // extraction pass events (kfx_get_extract_ms)
+  int extract_passes = 0;         // the last extraction: 1 (single pass) or 2 (count + emit)
+  int extract_mode = 1;           // kfx_set_extract_passes: 1 single pass when a buffer is given, 2 always two
   float extract_ms[3]{};          // last extraction: count pass, scan, emit pass
   bool ext_open = false;          // kfx_slab_frame_local done, kfx_slab_frame_finish due
   hipEvent_t *ext_pending = nullptr;  // that frame's timing sample
@@ -1826,12 +1828,75 @@ static int extract_events(kfx_ctx *c) {
   return KFX_OK;
 }
 
+int kfx_set_extract_passes(kfx_ctx *c, int passes) {
+  int r = check_ctx(c);
+  if (r) return r;
+  if (passes != 1 && passes != 2) return set_err(KFX_ERR_ARG, "extract passes are 1 or 2");
+  c->extract_mode = passes;
+  return KFX_OK;
+}
+
 int kfx_get_extract_ms(kfx_ctx *c, float out_ms[3]) {
   int r = check_ctx(c);
   if (r) return r;
   if (!out_ms) return set_err(KFX_ERR_ARG, "null out");
   for (int i = 0; i < 3; ++i) out_ms[i] = c->extract_ms[i];
   return KFX_OK;
+}
+
+// Single-pass extraction into the caller's buffer (k_extract1: one read of
+// the volume; the two-pass count / scan / emit path below is taken when the
+// caller asks for the count only, when the device buffer cannot be allocated,
+// or when the look-back watchdog fired).  per = floats per item (3 per point,
+// 9 per triangle).  Returns 1 when it produced the result.
+static int extract_single_pass(kfx_ctx *c, const uint8_t *tab, int zlo, int zhi, float *host, int64_t cap,
+                               int per, int64_t *total_out) {
+  if (cap <= 0 || cap > (int64_t)1 << 40 || c->extract_mode == 2) return 0;
+  const size_t nb = extract1_blocks(c->vol, zlo, zhi);
+  if (nb == 0) return 0;
+  char *ws = nullptr;
+  float *dout = nullptr;
+  const size_t wsb = nb * 8 + 64;
+  if (hipMalloc(&ws, wsb) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  if (hipMalloc(&dout, (size_t)cap * per * sizeof(float)) != hipSuccess) {
+    (void)hipGetLastError();
+    (void)hipFree(ws);
+    return 0;
+  }
+  unsigned long long *state = (unsigned long long *)ws;
+  unsigned long long *dtot = state + nb;
+  unsigned *derr = (unsigned *)(dtot + 1);
+  int done = 0;
+  hipError_t e = hipMemsetAsync(ws, 0, wsb, c->stream);
+  if (e == hipSuccess && extract_events(c) == KFX_OK) {
+    (void)hipEventRecord(c->xev[0], c->stream);
+    launch_extract1(c->stream, c->vol, to_dev(c->p.volu_pose), zlo, zhi, tab, state, dout,
+                    (unsigned long long)cap, dtot, derr);
+    (void)hipEventRecord(c->xev[1], c->stream);
+    e = hipGetLastError();
+    unsigned long long h[2] = {0, 0};
+    if (e == hipSuccess) e = hipMemcpyAsync(h, dtot, 16, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    const unsigned err = (unsigned)h[1];
+    if (e == hipSuccess && err == 0) {
+      const int64_t n = std::min<int64_t>((int64_t)h[0], cap);
+      if (n > 0) e = hipMemcpy(host, dout, (size_t)n * per * sizeof(float), hipMemcpyDeviceToHost);
+      if (e == hipSuccess) {
+        (void)hipEventElapsedTime(&c->extract_ms[0], c->xev[0], c->xev[1]);
+        c->extract_ms[1] = c->extract_ms[2] = 0.f;
+        c->extract_passes = 1;
+        *total_out = (int64_t)h[0];
+        done = 1;
+      }
+    }
+  }
+  (void)hipGetLastError();
+  (void)hipFree(dout);
+  (void)hipFree(ws);
+  return done;
 }
 
 int kfx_extract_points(kfx_ctx *c, float *xyz, int64_t cap, int64_t *n_points) {
@@ -1843,6 +1908,11 @@ int kfx_extract_points(kfx_ctx *c, float *xyz, int64_t cap, int64_t *n_points) {
   const int zlo = std::max(0, c->vol.own0), zhi = std::min(c->vol.own1, c->vol.Z - 1);
   const size_t waves = extract_waves(c->vol, zlo, zhi);
   int64_t total = 0;
+  if (waves > 0 && extract_single_pass(c, nullptr, zlo, zhi, xyz, cap, 3, &total)) {
+    if (n_points) *n_points = total;
+    return KFX_OK;
+  }
+  c->extract_passes = 2;
   if (waves > 0) {
     const size_t nb = scan_blocks(waves);
     char *ws = nullptr;
@@ -1968,6 +2038,11 @@ int kfx_extract_mesh(kfx_ctx *c, float *tri_xyz, int64_t cap, int64_t *n_tris) {
   const int zlo = std::max(0, c->vol.own0), zhi = std::min(c->vol.own1, c->vol.Z - 1);
   const size_t waves = extract_waves(c->vol, zlo, zhi);
   int64_t total = 0;
+  if (waves > 0 && extract_single_pass(c, c->mc_tab, zlo, zhi, tri_xyz, cap, 9, &total)) {
+    if (n_tris) *n_tris = total;
+    return KFX_OK;
+  }
+  c->extract_passes = 2;
   if (waves > 0) {
     const size_t nb = scan_blocks(waves);
     char *ws = nullptr;

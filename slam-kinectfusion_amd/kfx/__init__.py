@@ -35,7 +35,7 @@ EXPORTS = [
     "kfx_stage_icp", "kfx_stage_integrate", "kfx_stage_raycast", "kfx_set_profiling", "kfx_get_stage_ms",
     "kfx_integrate_counts", "kfx_integrate_stats", "kfx_raycast_stats", "kfx_download_columns", "kfx_pipeline_async", "kfx_pipeline_async_u16", "kfx_register_host_buffer", "kfx_unregister_host_buffer", "kfx_slab_mask_payload", "kfx_slab_expand", "kfx_set_icp_allreduce", "kfx_create_slab", "kfx_create_slab_cuts", "kfx_slice_work", "kfx_slice_work_parts", "kfx_slab_balance", "kfx_slab_info", "kfx_comm_get_unique_id", "kfx_comm_init",
     "kfx_pipeline_group", "kfx_slab_frame_local", "kfx_slab_frame_finish", "kfx_render", "kfx_volume_checksum", "kfx_extract_points", "kfx_write_ply", "kfx_save_pointcloud",
-    "kfx_extract_mesh", "kfx_write_ply_mesh", "kfx_get_extract_ms",
+    "kfx_extract_mesh", "kfx_write_ply_mesh", "kfx_get_extract_ms", "kfx_set_extract_passes",
     "kfx_dataset_open", "kfx_dataset_info", "kfx_dataset_read", "kfx_dataset_close", "kfx_png_info",
     "kfx_png_read_bgr8", "kfx_png_read_depth", "kfx_parse_intr",
 ]
@@ -128,6 +128,7 @@ def lib():
         "kfx_save_pointcloud": ([vp, C.c_char_p, C.c_int64], i),
         "kfx_extract_mesh": ([vp, P(f), C.c_int64, P(C.c_int64)], i),
         "kfx_get_extract_ms": ([vp, P(f)], i),
+        "kfx_set_extract_passes": ([vp, i], i),
         "kfx_write_ply_mesh": ([C.c_char_p, P(f), C.c_int64], i),
         "kfx_dataset_open": ([C.c_char_p, P(vp)], i),
         "kfx_dataset_info": ([vp, P(Intrinsics), P(i), P(i)], i),
@@ -485,27 +486,37 @@ class KinectFusion:
 
     def extract_mesh(self, cap: int = 50_000_000) -> np.ndarray:
         """Marching-cubes triangles, (N, 3, 3) float32 world coordinates (canonical order)."""
+        # one call into a cap-sized buffer (the library's single-pass path;
+        # np.empty pages are touched only where triangles are written)
         n = C.c_int64()
-        _check(lib().kfx_extract_mesh(self._h, None, 0, C.byref(n)), "kfx_extract_mesh")
-        m = min(n.value, cap)
-        out = np.zeros((m, 3, 3), np.float32)
-        if m:
-            _check(lib().kfx_extract_mesh(self._h, fptr(out), m, C.byref(n)), "kfx_extract_mesh")
-        return out
+        out = np.empty((max(cap, 0), 3, 3), np.float32)
+        _check(lib().kfx_extract_mesh(self._h, fptr(out) if cap > 0 else None, max(cap, 0), C.byref(n)),
+               "kfx_extract_mesh")
+        return out[:min(n.value, max(cap, 0))]
 
     # ---- point cloud (kinectfusion::extracePointcloud / savePointcloud) ---
     def extract_points(self, cap: int = 10_000_000) -> np.ndarray:
         """(N, 3) float32 zero-crossing points in world coordinates (canonical order)."""
         n = C.c_int64()
-        _check(lib().kfx_extract_points(self._h, None, 0, C.byref(n)), "kfx_extract_points")
-        m = min(n.value, cap)
-        out = np.zeros((m, 3), np.float32)
-        if m:
-            _check(lib().kfx_extract_points(self._h, fptr(out), m, C.byref(n)), "kfx_extract_points")
-        return out
+        out = np.empty((max(cap, 0), 3), np.float32)
+        _check(lib().kfx_extract_points(self._h, fptr(out) if cap > 0 else None, max(cap, 0), C.byref(n)),
+               "kfx_extract_points")
+        return out[:min(n.value, max(cap, 0))]
+
+    def extract_count(self, mesh: bool = False) -> int:
+        """Points (or triangles) the volume holds, without extracting them (count pass only)."""
+        n = C.c_int64()
+        fn = lib().kfx_extract_mesh if mesh else lib().kfx_extract_points
+        _check(fn(self._h, None, 0, C.byref(n)), "kfx_extract_mesh" if mesh else "kfx_extract_points")
+        return n.value
+
+    def set_extract_passes(self, passes: int):
+        """1: single-pass extraction (default); 2: count + scan + emit passes."""
+        _check(lib().kfx_set_extract_passes(self._h, int(passes)), "kfx_set_extract_passes")
 
     def extract_ms(self) -> dict:
-        """Device ms of the last extract_points / extract_mesh: count pass, scan, emit pass."""
+        """Device ms of the last extract_points / extract_mesh: count pass, scan, emit pass
+        (a single-pass extraction reports its one pass as count, scan = emit = 0)."""
         a = (C.c_float * 3)()
         _check(lib().kfx_get_extract_ms(self._h, a), "kfx_get_extract_ms")
         return {"count": a[0], "scan": a[1], "emit": a[2]}

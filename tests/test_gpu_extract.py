@@ -98,3 +98,27 @@ def test_mesh_matches_oracle(fused, tmp_path):
                         "property float z", "element face 3", "property list uchar int vertex_indices",
                         "end_header", "%g %g %g" % tuple(float(v) for v in o[0, 0])]
     assert txt[-1] == "3 6 7 8"
+
+
+@pytest.mark.parametrize("mesh", [False, True])
+def test_single_pass_equals_two_pass(mesh, fused):
+    """The single-pass extraction (count, decoupled look-back offsets, emit in
+    one volume read) gives the two-pass result (count pass, offset scan, emit
+    pass) bit for bit, full and capped, and the count-only call's total."""
+    kf, p, _ = fused
+    fn = kf.extract_mesh if mesh else kf.extract_points
+    one = fn(cap=50_000_000)
+    ms1 = kf.extract_ms()
+    assert ms1["count"] > 0 and ms1["scan"] == 0 and ms1["emit"] == 0  # one pass ran
+    capped = fn(cap=1234)
+    kf.set_extract_passes(2)
+    try:
+        two = fn(cap=50_000_000)
+        ms2 = kf.extract_ms()
+        assert ms2["emit"] > 0
+        two_capped = fn(cap=1234)
+    finally:
+        kf.set_extract_passes(1)
+    assert len(one) == kf.extract_count(mesh) > 1000
+    assert np.array_equal(one.view(np.uint32), two.view(np.uint32))
+    assert np.array_equal(capped.view(np.uint32), two_capped.view(np.uint32)) and len(capped) == 1234

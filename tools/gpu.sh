@@ -11,6 +11,7 @@
 #   prof[=ARGS]       tools/prof.sh (rocprofv3 stats + PMC passes)
 #   slab=c4|c5        tools/slab_record.py (8 slabs on one GPU)
 #   ab=ROUNDS:V1:V2   tools/ab_quick.sh ROUNDS V1 V2 ... (alternating variants)
+#   py=SCRIPT:ARG     python3 tools/SCRIPT ARG (e.g. py=icp_trace.py:hd720)
 #   pmcv=V1:V2        SQ instruction counters of k_integrate per variant (tools/pmc_var.sh)
 # e.g.  gpurun -- bash tools/gpu.sh tests bench quick=--config,c5
 set -o pipefail
@@ -65,6 +66,10 @@ for job in "$@"; do
     slab)
       step slab 900 python3 tools/slab_record.py "$val" --out gpurun_out/slab_$val.json > gpurun_out/slab_$val.log 2>&1
       tail -n 5 gpurun_out/slab_$val.log ;;
+    py)  # py=SCRIPT:ARG  a tools/ python script on the GPU
+      S=${val%%:*}; A=${val#*:}; [ "$A" = "$val" ] && A=""
+      step py 600 python3 tools/$S $A > gpurun_out/py_${S%.py}.log 2>&1
+      tail -n 40 gpurun_out/py_${S%.py}.log ;;
     ab)
       step ab 1200 bash tools/ab_quick.sh $(echo "$val" | tr ':' ' ') ;;
     pmcv)

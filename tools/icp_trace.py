@@ -1,5 +1,7 @@
 #!/usr/bin/env python3
-"""Phase timing of the persistent ICP kernel on a VGA 512^3 run (GPU box)."""
+"""Phase timing of the persistent ICP kernel on a VGA 512^3 run (GPU box);
+`icp_trace.py hd720`: 1280x720 frames (C5's size) on a 512^3 volume of C5's
+4.096 m extent."""
 import os
 import sys
 
@@ -11,11 +13,13 @@ import kfx  # noqa: E402
 from kfx import synth  # noqa: E402
 from kfx.abi import default_params  # noqa: E402
 
-intr = synth.Intrinsics.vga()
-kf = kfx.KinectFusion(intr, default_params())
+hd = len(sys.argv) > 1 and sys.argv[1] == "hd720"
+intr = synth.Intrinsics.hd720() if hd else synth.Intrinsics.vga()
+L = 4.096 if hd else 2.048
+kf = kfx.KinectFusion(intr, default_params(dims=512, range_m=L))
 # the benchmark's regime: frames staged in HBM, overlapped launches (the
 # next frame's preprocess runs beside this frame's ICP), 25 frames
-bgr, dep, _ = synth.sequence(25, intr)
+bgr, dep, _ = synth.sequence(25, intr, L=L)
 kf.stage_frames(bgr, dep.astype(np.float32))
 for k in range(len(dep)):
     kf.pipeline_staged(k)
