@@ -56,7 +56,6 @@ struct IcpPlan {
   LevelGeom g[kMaxLevels];
   int xe[kMaxLevels], npix[kMaxLevels], groups[kMaxLevels], iters[kMaxLevels];
   int ppl[kMaxLevels];  // pixels per lane at each level
-  int xgroups[kMaxLevels];  // 8, or the block residues mod 8 (XCD groups) taking part at that level
   const float *cv[kMaxLevels], *cn[kMaxLevels], *pv[kMaxLevels], *pn[kMaxLevels];
   float dist2_max, sine2_max;  // sqrt_le_bound of the distance / sine thresholds
   // 1: nblocks (co-resident) is below some level's groups; block b also takes

@@ -536,6 +536,9 @@ constexpr int kIcpPix = KFX_ICP_PIX;
 #ifndef KFX_ICP_SLEEP
 #define KFX_ICP_SLEEP 1  // ICP release poll: s_sleep units (64 clocks) between polls (0: busy poll)
 #endif
+#ifndef KFX_ICP_MINB
+#define KFX_ICP_MINB 2  // persistent ICP: blocks per CU the register budget is sized for (co-resident grid)
+#endif
 #ifndef KFX_ICP_THREADS
 #define KFX_ICP_THREADS 256  // ICP: threads per block
 #endif
@@ -559,10 +562,12 @@ __device__ __forceinline__ void icp_lane(const LevelGeom &g, const DevPose &P,
                                          const bool (&ok0)[kIcpPix], int ppl,
                                          const float *__restrict__ pv,
                                          const float *__restrict__ pn, float dist2_max,
-                                         float sine2_max, double (&acc)[27]) {
+                                         float sine2_max, double (&acc)[27], bool zero = true) {
   const f3 t = {P.t[0], P.t[1], P.t[2]};
+  if (zero) {  // (zero = false: add to the sums already in acc)
 #pragma unroll
-  for (int k = 0; k < 27; ++k) acc[k] = 0.0;
+    for (int k = 0; k < 27; ++k) acc[k] = 0.0;
+  }
   f3 vcur[kIcpPix];
   int j[kIcpPix];
   bool ok[kIcpPix];
@@ -816,7 +821,7 @@ __global__ __launch_bounds__(kIcpThreads) void k_icp_acc(LevelGeom g, int xe, in
 // sums stay integers below 2^53 (<= 16 groups per block, IcpPlan docs), so the
 // fp64 adds remain exact and the int64 totals are the oracle's.
 template <bool kStride>
-__global__ __launch_bounds__(kIcpThreads, 2) void k_icp_track(IcpPlan pl, DevState *__restrict__ st,
+__global__ __launch_bounds__(kIcpThreads, KFX_ICP_MINB) void k_icp_track(IcpPlan pl, DevState *__restrict__ st,
                                                    IcpSync *__restrict__ sy, int begin) {
   DevPose P;
   if (begin) {
@@ -837,43 +842,44 @@ __global__ __launch_bounds__(kIcpThreads, 2) void k_icp_track(IcpPlan pl, DevSta
   int slot = 0;
   for (int l = pl.levels - 1; l >= 0 && !fail; --l) {
     const LevelGeom g = pl.g[l];
-    // blocks dealt round-robin over the 8 XCDs: with xgroups < 8 only the
-    // blocks of that many residues mod 8 (as many XCDs, under round-robin
-    // placement — speed only, the protocol is agent-scope either way) work
-    const int nx = pl.xgroups[l];
-    const int prank = nx >= 8 ? (int)blockIdx.x : (int)(blockIdx.x / 8) * nx + (int)(blockIdx.x % 8);
-    const bool mine = (nx >= 8 || (int)(blockIdx.x % 8) < nx) && prank < pl.groups[l];
-    // (level-uniform) more groups than blocks: identity group order, strided
-    const bool stride = kStride && nx >= 8 && pl.groups[l] > (int)gridDim.x;
+    const int prank = (int)blockIdx.x;
+    const bool mine = prank < pl.groups[l];
+    // kStride (some level has more groups than blocks): every level takes its
+    // groups b, b + gridDim.x, ... in identity order and re-reads their
+    // current-frame pixels each iteration (no register-held pixels: one
+    // lane-phase code path, the register budget of the plain kernel)
+    constexpr bool stride = kStride;
     f3 n0[kIcpPix], v0[kIcpPix];
     bool ok[kIcpPix];
-    if (mine)
-      icp_load_cur(g, pl.xe[l], pl.npix[l],
-                   nx < 8 ? prank : (stride ? (int)blockIdx.x : (KFX_ICP_XCD ? xcd_remap(blockIdx.x, pl.groups[l]) : (int)blockIdx.x)),
+    if (mine && !stride)
+      icp_load_cur(g, pl.xe[l], pl.npix[l], KFX_ICP_XCD ? xcd_remap(blockIdx.x, pl.groups[l]) : (int)blockIdx.x,
                    pl.ppl[l], pl.cv[l], pl.cn[l], n0, v0, ok);
     for (int it = 0; it < pl.iters[l] && !fail; ++it, ++slot) {
       unsigned long long *sh = sy->sums + (size_t)slot * kIcpShards * 27;
-      target += stride ? gridDim.x : pl.groups[l];  // arrivals: the blocks with a group
+      target += min(pl.groups[l], (int)gridDim.x);  // arrivals: the blocks with a group
       const bool tr = threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x - 1);
       if (tr && blockIdx.x == 0) sy->trace[slot][0] = wall_clock64();
 #ifdef KFX_ICP_BLOCK_TRACE
       if (threadIdx.x == 0 && blockIdx.x < 512) sy->blk[slot][blockIdx.x][0] = wall_clock64();
 #endif
       if (mine) {
-        double acc[27];
-        icp_lane(g, P, n0, v0, ok, pl.ppl[l], pl.pv[l], pl.pn[l], pl.dist2_max, pl.sine2_max, acc);
-        if (stride)
-          for (int gx = (int)blockIdx.x + (int)gridDim.x; gx < pl.groups[l]; gx += (int)gridDim.x) {
-            f3 n1[kIcpPix], v1[kIcpPix];
-            bool ok1[kIcpPix];
-            double a1[27];
-            icp_load_cur(g, pl.xe[l], pl.npix[l], gx, pl.ppl[l], pl.cv[l], pl.cn[l], n1, v1, ok1);
-            icp_lane(g, P, n1, v1, ok1, pl.ppl[l], pl.pv[l], pl.pn[l], pl.dist2_max, pl.sine2_max, a1);
-#pragma unroll
-            for (int i = 0; i < 27; ++i) acc[i] += a1[i];
+        long long bsum = 0;
+        if (stride) {
+          // groups blockIdx.x, + gridDim.x, ...: each group's block sums are
+          // added as int64 (exact), so no lane sums stay live across groups
+          for (int gx = (int)blockIdx.x; gx < pl.groups[l]; gx += (int)gridDim.x) {
+            double acc[27];
+            icp_load_cur(g, pl.xe[l], pl.npix[l], gx, pl.ppl[l], pl.cv[l], pl.cn[l], n0, v0, ok);
+            icp_lane(g, P, n0, v0, ok, pl.ppl[l], pl.pv[l], pl.pn[l], pl.dist2_max, pl.sine2_max, acc);
+            if (tr && blockIdx.x == 0) sy->trace[slot][8] = wall_clock64() + (acc[3] == -1.5 ? 1 : 0);
+            bsum += icp_block_reduce(red, acc);
           }
-        if (tr && blockIdx.x == 0) sy->trace[slot][8] = wall_clock64() + (acc[3] == -1.5 ? 1 : 0);
-        const long long bsum = icp_block_reduce(red, acc);
+        } else {
+          double acc[27];
+          icp_lane(g, P, n0, v0, ok, pl.ppl[l], pl.pv[l], pl.pn[l], pl.dist2_max, pl.sine2_max, acc);
+          if (tr && blockIdx.x == 0) sy->trace[slot][8] = wall_clock64() + (acc[3] == -1.5 ? 1 : 0);
+          bsum = icp_block_reduce(red, acc);
+        }
         if (tr && blockIdx.x == 0) sy->trace[slot][9] = wall_clock64() + (bsum == -7 ? 1 : 0);
         if (threadIdx.x < 64) {
           if (threadIdx.x < 27)
@@ -3158,7 +3164,6 @@ IcpPlan make_icp_plan(int levels, const LevelGeom *g, const int *iters, FrameVie
     // CU (256), so coarse levels spread over more waves (shorter lane phase)
     pl.ppl[l] = std::max(1, std::min(kIcpPix, (pl.npix[l] + KFX_ICP_PPLCAP * kIcpThreads - 1) / (KFX_ICP_PPLCAP * kIcpThreads)));
     pl.groups[l] = std::max(1, (pl.npix[l] + kIcpThreads * pl.ppl[l] - 1) / (kIcpThreads * pl.ppl[l]));
-    pl.xgroups[l] = 8;
     pl.iters[l] = iters[l];
     pl.cv[l] = cur.v[l];
     pl.cn[l] = cur.n[l];
@@ -3186,8 +3191,6 @@ bool icp_persistent_ok(IcpPlan &pl, int device) {
     return false;
   const int cap = per_cu_s * cus;
   if (cap <= 0 || (pl.nblocks + cap - 1) / cap > kIcpStrideMax) return false;
-  for (int l = 0; l < pl.levels; ++l)
-    if (pl.xgroups[l] < 8) return false;  // (XCD-group levels index by residue, not strided)
   pl.nblocks = cap;
   pl.stride = 1;
   return true;
