@@ -13,7 +13,7 @@ and raycast): factor = counter value per dispatch / bytes the stream moved
 must be calibrated on a known byte count).  The SQ pass (pmc/SQ) gives the
 issue figures of integrate and raycast (VALU issue fraction, wave-cycle split).
 Output: <dir>/traffic.json, and profiles/$PMC_RECORD (default
-r03_integrate_pmc.json) when --commit is given: bench.py attaches it as
+r04_integrate_pmc.json) when --commit is given: bench.py attaches it as
 roofline.traffic only to a run that loaded the library it names by sha256.
 """
 import collections
@@ -105,7 +105,7 @@ def main():
                 ks = [k for k in sq if k.startswith(pre)]
                 if ks:
                     rec[name] = sq_issue(sq[ks[0]])
-            name = os.environ.get("PMC_RECORD", "r03_integrate_pmc.json")
+            name = os.environ.get("PMC_RECORD", "r04_integrate_pmc.json")
             json.dump(rec, open(os.path.join(REPO, "profiles", name), "w"), indent=1)
             # a copy beside the counters (profiles/ does not come back from the GPU box)
             json.dump(rec, open(os.path.join(root, name), "w"), indent=1)
