@@ -377,23 +377,25 @@ def extract_record(kf, n):
     """Surface extraction off the per-frame path (C5 names the
     marching-cubes extract): kfx_extract_points (FullScan6 zero crossings,
     tsdf_volume.cu:307-481) and kfx_extract_mesh on the volume the timed frames
-    built; device ms of the count pass, the offset scan and the emit pass
-    (HIP events).  Roofline: each pass of the reference's full scan reads every
-    voxel's int16 tsdf + u8 weight (3 B; neighbours come from cache), the emit
-    pass also writes 12 B per point / 36 B per triangle.  The kernels skip the
-    waves whose brick the occupancy map proves empty, so `achieved` is the
+    built; device ms of the volume pass, the offset scan and the pool copy
+    (passes = 1: the volume is read once) or the emit pass (passes = 2), HIP
+    events.  Roofline on the reference's bytes: its FullScan6 reads every
+    voxel's int16 tsdf + u8 weight once (3 B; neighbours come from cache) and
+    writes 12 B per point (36 B per triangle for the mesh).  The kernels skip
+    the waves whose brick the occupancy map proves empty, so `achieved` is the
     full-scan-equivalent rate."""
     vox = n * n * (n - 1)  # z = 0 .. Z-2 (the +z neighbour must exist)
     out = {"voxels_scanned": vox, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-           "bytes_basis": "2 full-volume passes of 3 B/voxel + outputs (the reference's scan); "
+           "bytes_basis": "one full-volume pass of 3 B/voxel + the outputs (the reference's FullScan6); "
                           "clear bricks are skipped, so achieved is the full-scan-equivalent rate"}
     for name, fn, per in (("points", kf.extract_points, 12), ("mesh", kf.extract_mesh, 36)):
         items = fn(cap=50_000_000)
         ms = kf.extract_ms()
-        b = 2 * 3 * vox + per * len(items)
+        b = 3 * vox + per * len(items)
         t = ms["count"] + ms["scan"] + ms["emit"]
-        out[name] = {"items": int(len(items)), "count_ms": round(ms["count"], 4), "scan_ms": round(ms["scan"], 4),
-                     "emit_ms": round(ms["emit"], 4), "algorithmic_bytes": int(b),
+        out[name] = {"items": int(len(items)), "passes": ms["passes"], "count_ms": round(ms["count"], 4),
+                     "scan_ms": round(ms["scan"], 4), "copy_or_emit_ms": round(ms["emit"], 4),
+                     "total_ms": round(t, 4), "algorithmic_bytes": int(b),
                      "achieved": round(b / (t * 1e-3) / 1e9, 1) if t > 0 else None,
                      "frac": round(b / (t * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if t > 0 else None}
         del items

@@ -270,16 +270,20 @@ int kfx_download_columns(kfx_ctx *ctx, const int32_t *cols, int n, int16_t *tsdf
                          uint32_t *rgb);
 
 /* ---- point cloud ------------------------------------------ */
-/* Device ms of the last kfx_extract_points / kfx_extract_mesh call: the count
- * pass, the offset scan and the emit pass (0 if nothing was emitted).  A call
- * with a buffer (cap > 0) normally runs ONE pass over the volume (count, a
- * decoupled look-back for the offsets, emit): out_ms[0] is that pass and
- * out_ms[1] = out_ms[2] = 0.  cap = 0 (count only) runs the count pass. */
+/* Device ms of the last kfx_extract_points / kfx_extract_mesh call, three
+ * phases.  A call with a buffer (cap > 0) normally reads the volume ONCE:
+ * [0] the pass that counts every wave's items and writes them into an
+ * unordered pool, [1] the offset scan, [2] the pool-to-canonical-order copy
+ * (kfx_get_extract_passes = 1).  The two-pass path (count only, cap = 0;
+ * kfx_set_extract_passes(2); or more items than cap, when the pool cannot hold
+ * them all): [0] the count pass, [1] the scan, [2] the emit pass, which reads
+ * the volume again (passes = 2; 0 if nothing was emitted). */
 int kfx_get_extract_ms(kfx_ctx *ctx, float out_ms[3]);
-/* 1 (default): kfx_extract_points / kfx_extract_mesh with a buffer run the
- * single pass; 2: always the count pass, the offset scan and the emit pass
- * (the fallback the single pass takes itself if its look-back stalls).  The
- * output is identical. */
+/* Volume passes of the last extraction: 1 or 2 (see above). */
+int kfx_get_extract_passes(kfx_ctx *ctx, int *passes);
+/* 1 (default): kfx_extract_points / kfx_extract_mesh with a buffer read the
+ * volume once; 2: always the count pass, the offset scan and the emit pass.
+ * The output is identical. */
 int kfx_set_extract_passes(kfx_ctx *ctx, int passes);
 /* TSDFVolume::fetchPointCloud buffer size (tsdf_volume.cpp:67) */
 #define KFX_DEFAULT_CLOUD_POINTS 10000000

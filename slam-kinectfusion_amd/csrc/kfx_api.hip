@@ -1836,6 +1836,14 @@ int kfx_set_extract_passes(kfx_ctx *c, int passes) {
   return KFX_OK;
 }
 
+int kfx_get_extract_passes(kfx_ctx *c, int *passes) {
+  int r = check_ctx(c);
+  if (r) return r;
+  if (!passes) return set_err(KFX_ERR_ARG, "null out");
+  *passes = c->extract_passes;
+  return KFX_OK;
+}
+
 int kfx_get_extract_ms(kfx_ctx *c, float out_ms[3]) {
   int r = check_ctx(c);
   if (r) return r;
@@ -1844,57 +1852,82 @@ int kfx_get_extract_ms(kfx_ctx *c, float out_ms[3]) {
   return KFX_OK;
 }
 
-// Single-pass extraction into the caller's buffer (k_extract1: one read of
-// the volume; the two-pass count / scan / emit path below is taken when the
-// caller asks for the count only, when the device buffer cannot be allocated,
-// or when the look-back watchdog fired).  per = floats per item (3 per point,
-// 9 per triangle).  Returns 1 when it produced the result.
+// Extraction into the caller's buffer with ONE read of the volume
+// (k_extract_pool: count + items into an unordered pool; the offset scan;
+// k_extract_copy: pool -> canonical order).  If the pool (cap items) cannot
+// hold every item, the counts are still complete and the emit pass of the
+// two-pass path writes the first cap items instead.  Not taken (returns 0)
+// for a count-only call (cap = 0), with kfx_set_extract_passes(2), or when
+// the buffers cannot be allocated: the caller then runs the two-pass path.
+// per = floats per item (3 per point, 9 per triangle).
 static int extract_single_pass(kfx_ctx *c, const uint8_t *tab, int zlo, int zhi, float *host, int64_t cap,
                                int per, int64_t *total_out) {
-  if (cap <= 0 || cap > (int64_t)1 << 40 || c->extract_mode == 2) return 0;
-  const size_t nb = extract1_blocks(c->vol, zlo, zhi);
-  if (nb == 0) return 0;
+  if (cap <= 0 || cap > (int64_t)1 << 36 || c->extract_mode == 2) return 0;
+  const size_t waves = extract_waves(c->vol, zlo, zhi);
+  if (waves == 0) return 0;
+  const size_t nb = scan_blocks(waves);
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  const size_t o_off = al(waves * 4), o_bsum = o_off + al(waves * 8), o_misc = o_bsum + al(nb * 8),
+               o_at = o_misc + 256, o_list = o_at + al(waves * 8), wsb = o_list + al(waves * 4);
   char *ws = nullptr;
-  float *dout = nullptr;
-  const size_t wsb = nb * 8 + 64;
-  if (hipMalloc(&ws, wsb) != hipSuccess) {
+  float *pool = nullptr, *dout = nullptr;
+  const size_t ibytes = (size_t)cap * per * sizeof(float);
+  if (hipMalloc(&ws, wsb) != hipSuccess || hipMalloc(&pool, ibytes) != hipSuccess ||
+      hipMalloc(&dout, ibytes) != hipSuccess) {
     (void)hipGetLastError();
+    if (ws) (void)hipFree(ws);
+    if (pool) (void)hipFree(pool);
     return 0;
   }
-  if (hipMalloc(&dout, (size_t)cap * per * sizeof(float)) != hipSuccess) {
-    (void)hipGetLastError();
-    (void)hipFree(ws);
-    return 0;
-  }
-  unsigned long long *state = (unsigned long long *)ws;
-  unsigned long long *dtot = state + nb;
-  unsigned *derr = (unsigned *)(dtot + 1);
+  unsigned *counts = (unsigned *)ws;
+  unsigned long long *offsets = (unsigned long long *)(ws + o_off);
+  unsigned long long *bsum = (unsigned long long *)(ws + o_bsum);
+  unsigned long long *misc = (unsigned long long *)(ws + o_misc);  // {total, ctr, overflow}
+  unsigned long long *pool_at = (unsigned long long *)(ws + o_at);
+  unsigned *list = (unsigned *)(ws + o_list);
+  const DevPose vp = to_dev(c->p.volu_pose);
   int done = 0;
-  hipError_t e = hipMemsetAsync(ws, 0, wsb, c->stream);
+  hipError_t e = hipMemsetAsync(misc, 0, 256, c->stream);
   if (e == hipSuccess && extract_events(c) == KFX_OK) {
     (void)hipEventRecord(c->xev[0], c->stream);
-    launch_extract1(c->stream, c->vol, to_dev(c->p.volu_pose), zlo, zhi, tab, state, dout,
-                    (unsigned long long)cap, dtot, derr);
+    launch_extract_pool(c->stream, c->vol, vp, zlo, zhi, tab, counts, misc + 1, pool_at, list, pool,
+                        (unsigned long long)cap, (unsigned *)(misc + 2));
     (void)hipEventRecord(c->xev[1], c->stream);
+    launch_scan(c->stream, counts, offsets, bsum, waves, misc);
+    (void)hipEventRecord(c->xev[2], c->stream);
     e = hipGetLastError();
-    unsigned long long h[2] = {0, 0};
-    if (e == hipSuccess) e = hipMemcpyAsync(h, dtot, 16, hipMemcpyDeviceToHost, c->stream);
+    unsigned long long h[3] = {0, 0, 0};
+    if (e == hipSuccess) e = hipMemcpyAsync(h, misc, 24, hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-    const unsigned err = (unsigned)h[1];
-    if (e == hipSuccess && err == 0) {
-      const int64_t n = std::min<int64_t>((int64_t)h[0], cap);
-      if (n > 0) e = hipMemcpy(host, dout, (size_t)n * per * sizeof(float), hipMemcpyDeviceToHost);
-      if (e == hipSuccess) {
-        (void)hipEventElapsedTime(&c->extract_ms[0], c->xev[0], c->xev[1]);
-        c->extract_ms[1] = c->extract_ms[2] = 0.f;
-        c->extract_passes = 1;
-        *total_out = (int64_t)h[0];
-        done = 1;
-      }
+    const int64_t total = (int64_t)h[0], n = std::min<int64_t>(total, cap);
+    const bool ovf = (unsigned)h[2] != 0;
+    if (e == hipSuccess && n > 0) {
+      (void)hipEventRecord(c->xev[3], c->stream);
+      if (!ovf)
+        launch_extract_copy(c->stream, list, (unsigned)(h[1] >> 40), counts, pool_at, offsets, pool, dout,
+                            (unsigned long long)n, per);
+      else if (tab)
+        launch_mesh(c->stream, c->vol, vp, zlo, zhi, tab, counts, offsets, dout, (unsigned long long)n);
+      else
+        launch_extract(c->stream, c->vol, vp, zlo, zhi, counts, offsets, dout, (unsigned long long)n);
+      (void)hipEventRecord(c->xev[4], c->stream);
+      e = hipGetLastError();
+      if (e == hipSuccess) e = hipMemcpyAsync(host, dout, (size_t)n * per * sizeof(float), hipMemcpyDeviceToHost, c->stream);
+      if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    }
+    if (e == hipSuccess) {
+      (void)hipEventElapsedTime(&c->extract_ms[0], c->xev[0], c->xev[1]);
+      (void)hipEventElapsedTime(&c->extract_ms[1], c->xev[1], c->xev[2]);
+      c->extract_ms[2] = 0.f;
+      if (n > 0) (void)hipEventElapsedTime(&c->extract_ms[2], c->xev[3], c->xev[4]);
+      c->extract_passes = ovf && n > 0 ? 2 : 1;
+      *total_out = total;
+      done = 1;
     }
   }
   (void)hipGetLastError();
   (void)hipFree(dout);
+  (void)hipFree(pool);
   (void)hipFree(ws);
   return done;
 }

@@ -272,12 +272,14 @@ void launch_extract(hipStream_t s, const VolView &v, DevPose vpose, int zlo, int
 void launch_mesh(hipStream_t s, const VolView &v, DevPose vpose, int zlo, int zhi, const uint8_t *tab,
                  unsigned *counts, const unsigned long long *offsets, float *out, unsigned long long cap);
 size_t scan_blocks(size_t n);  // bsum entries launch_scan needs (<= 65536)
-// single-pass extraction (k_extract1): tab = null for points, the marching-cubes
-// table for triangles; state = extract1_blocks() zeroed u64 words
-size_t extract1_blocks(const VolView &v, int zlo, int zhi);
-void launch_extract1(hipStream_t s, const VolView &v, DevPose vpose, int zlo, int zhi, const uint8_t *tab,
-                     unsigned long long *state, float *out, unsigned long long cap, unsigned long long *total,
-                     unsigned *err);
+// one-read extraction (k_extract_pool + scan + k_extract_copy): tab = null
+// for points, the marching-cubes table for triangles
+void launch_extract_pool(hipStream_t s, const VolView &v, DevPose vpose, int zlo, int zhi, const uint8_t *tab,
+                         unsigned *counts, unsigned long long *ctr, unsigned long long *pool_at, unsigned *list,
+                         float *pool, unsigned long long pool_cap, unsigned *overflow);
+void launch_extract_copy(hipStream_t s, const unsigned *list, unsigned nlist, const unsigned *counts,
+                         const unsigned long long *pool_at, const unsigned long long *offsets, const float *pool,
+                         float *out, unsigned long long cap, int per);
 void launch_scan(hipStream_t s, const unsigned *counts, unsigned long long *offsets,
                  unsigned long long *bsum, size_t n, unsigned long long *total);
 void launch_export_records(hipStream_t s, VolView v, int z0, int nz, uint64_t *dst);

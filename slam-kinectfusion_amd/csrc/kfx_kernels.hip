@@ -2617,8 +2617,9 @@ __device__ __forceinline__ unsigned extract_wave(const VolView &v, const DevPose
       const unsigned long long r = base + (unsigned long long)(__popcll(b1 & below) +
                                                                __popcll(b2 & below) +
                                                                __popcll(b3 & below));
-      for (int l = 0; l < n; ++l)
-        if (r + l < cap) st3(out, (size_t)(r + l), pts[l]);
+#pragma unroll
+      for (int l = 0; l < 3; ++l)  // (unrolled: pts stays in registers)
+        if (l < n && r + l < cap) st3(out, (size_t)(r + l), pts[l]);
     }
     const unsigned wt = (unsigned)(__popcll(b1) + __popcll(b2) + __popcll(b3));
     base += wt;
@@ -2751,94 +2752,80 @@ __global__ __launch_bounds__(256) void k_mesh(VolView v, DevPose aff, int zlo, i
   if (!kEmit && lane == 0) counts[wave] = total;
 }
 
-// Single-pass extraction (points or marching cubes): count, offsets and emit
-// in ONE read of the volume.  A block = 4 consecutive canonical waves (4
-// tiles of one 8-slice chunk).  It counts, publishes its aggregate, finds the
-// exclusive prefix of every block before it by a decoupled look-back, then
-// publishes its inclusive prefix and emits (re-reading the bricks it just
-// read, from cache).  Blocks are dispatched in index order, so every block a
-// look-back waits for has started and completes without waiting on a later
-// one.  state[b] (zeroed by the host): 0 = nothing yet, kLbAgg | count,
-// kLbIncl | inclusive prefix.  Wave 0 looks back 64 blocks per round trip.
-// A wait longer than the watchdog sets *err (the host then takes the
-// two-pass path); total = the last block's inclusive prefix.
-constexpr unsigned long long kLbAgg = 1ull << 62, kLbIncl = 1ull << 63, kLbVal = (1ull << 62) - 1ull;
-constexpr unsigned long long kLookbackWatchdogTicks = 50000000ull;  // >= 0.5 s of s_memrealtime
+// Extraction with ONE read of the volume (points or marching cubes).
+// Pass A (k_extract_pool): each canonical wave counts its brick's items and,
+// if it has any, reserves that many slots of a pool with one 64-bit atomic
+// (high bits: the wave's entry in the list of non-empty waves, low bits: the
+// pool offset) and writes its items there in its own canonical order (from
+// the bricks it just read: cache hits).  The reserved slots are unordered
+// across waves.  Then the offset scan of the per-wave counts (canonical
+// order) and pass C (k_extract_copy): one wave per listed wave copies its
+// items from the pool to their canonical position.  A pool too small for
+// every item (the caller's cap) sets *overflow; the counts are still complete,
+// and the host then runs the emit pass of the two-pass path instead.
+constexpr int kPoolListShift = 40;
+constexpr unsigned long long kPoolMask = (1ull << kPoolListShift) - 1ull;
 template <bool kMesh>
-__global__ __launch_bounds__(256) void k_extract1(VolView v, DevPose aff, int zlo, int zhi,
-                                                  const uint8_t *__restrict__ tab, unsigned long long *state,
-                                                  float *out, unsigned long long cap,
-                                                  unsigned long long *total, unsigned *err) {
-  __shared__ unsigned wcnt[4];
-  __shared__ unsigned long long s_excl;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+__global__ __launch_bounds__(256) void k_extract_pool(VolView v, DevPose aff, int zlo, int zhi,
+                                                      const uint8_t *__restrict__ tab, unsigned *counts,
+                                                      unsigned long long *ctr, unsigned long long *pool_at,
+                                                      unsigned *list, float *pool, unsigned long long pool_cap,
+                                                      unsigned *overflow) {
+  const int lane = threadIdx.x & 63;
   const int ntiles = v.tiles_x * v.tiles_y;
-  const int tile = blockIdx.x * 4 + w;
-  const size_t b = (size_t)blockIdx.y * gridDim.x + blockIdx.x;  // canonical block order
-  const size_t nblocks = (size_t)gridDim.x * gridDim.y;
-  const int c0 = (zlo / kExtractZ) * kExtractZ + (int)blockIdx.y * kExtractZ;
-  const int z0 = max(zlo, c0), z1 = min(zhi, c0 + kExtractZ);
-  const bool act = tile < ntiles && !(KFX_EXTRACT_SKIP && brick_clear(v, tile, c0));  // wave-uniform
+  const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (tile >= ntiles) return;
+  const size_t wave = (size_t)blockIdx.y * ntiles + tile;
   const int x = (tile % v.tiles_x) * 8 + (lane & 7);
   const int y = (tile / v.tiles_x) * 8 + (lane >> 3);
-  unsigned cnt = 0;
-  if (act)
-    cnt = kMesh ? mesh_wave<false>(v, aff, tab, x, y, z0, z1, 0ull, out, 0ull)
-                : extract_wave<false>(v, aff, x, y, z0, z1, 0ull, out, 0ull);
-  if (lane == 0) wcnt[w] = cnt;
-  __syncthreads();
-  if (w == 0) {  // wave 0: publish, look back, publish
-    const unsigned long long agg = (unsigned long long)wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
-    unsigned long long excl = 0;
-    if (b == 0) {
-      if (lane == 0) __hip_atomic_store(&state[0], kLbIncl | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      if (lane == 0) __hip_atomic_store(&state[b], kLbAgg | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      // window: lane k reads block p - k; the nearest inclusive prefix ends it
-      long long p = (long long)b - 1;
-      const unsigned long long t0 = wall_clock64();
-      bool done = false;
-      while (!done) {
-        const long long q = p - lane;
-        const unsigned long long sv =
-            q >= 0 ? __hip_atomic_load(&state[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kLbIncl;
-        const unsigned long long inc = __ballot((sv & kLbIncl) != 0ull);
-        const unsigned long long none = __ballot((sv & (kLbIncl | kLbAgg)) == 0ull);
-        const int first_inc = inc ? __ffsll((long long)inc) - 1 : 64;  // nearest inclusive lane
-        const unsigned long long need = first_inc == 64 ? ~0ull : ((2ull << first_inc) - 1ull);
-        if (none & need) {  // a block in the window has not published yet: poll again
-          if (wall_clock64() - t0 > kLookbackWatchdogTicks) {
-            if (lane == 0) atomicOr(err, 1u);
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-          continue;
-        }
-        unsigned long long part = (lane <= first_inc) ? (sv & kLbVal) : 0ull;
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) part += (unsigned long long)__shfl_xor((long long)part, off);
-        excl += part;
-        done = first_inc < 64;
-        p -= 64;
-      }
-      if (lane == 0)
-        __hip_atomic_store(&state[b], kLbIncl | ((excl + agg) & kLbVal), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (lane == 0) {
-      s_excl = excl;
-      if (b == nblocks - 1) *total = excl + agg;
-    }
+  const int c0 = (zlo / kExtractZ) * kExtractZ + (int)blockIdx.y * kExtractZ;
+  const int z0 = max(zlo, c0), z1 = min(zhi, c0 + kExtractZ);
+  if (KFX_EXTRACT_SKIP && brick_clear(v, tile, c0)) {  // wave-uniform
+    if (lane == 0) counts[wave] = 0;
+    return;
   }
-  __syncthreads();
-  if (act && cnt) {
-    unsigned long long base = s_excl;
-    for (int k = 0; k < w; ++k) base += wcnt[k];
-    if (kMesh)
-      (void)mesh_wave<true>(v, aff, tab, x, y, z0, z1, base, out, cap);
-    else
-      (void)extract_wave<true>(v, aff, x, y, z0, z1, base, out, cap);
+  const unsigned n = kMesh ? mesh_wave<false>(v, aff, tab, x, y, z0, z1, 0ull, pool, 0ull)
+                           : extract_wave<false>(v, aff, x, y, z0, z1, 0ull, pool, 0ull);
+  if (lane == 0) counts[wave] = n;
+  if (n == 0) return;  // wave-uniform
+  unsigned long long old = 0;
+  if (lane == 0) old = atomicAdd(ctr, (1ull << kPoolListShift) | (unsigned long long)n);
+  old = __shfl(old, 0);
+  const unsigned long long base = old & kPoolMask;
+  if (lane == 0) {
+    list[old >> kPoolListShift] = (unsigned)wave;
+    pool_at[wave] = base;
   }
+  if (base + n > pool_cap) {
+    if (lane == 0) atomicOr(overflow, 1u);
+    return;
+  }
+  // the items again from the bricks just read (cache hits; staging them in
+  // LDS during the count measured slower: occupancy)
+  if (kMesh) {
+    (void)mesh_wave<true>(v, aff, tab, x, y, z0, z1, base, pool, pool_cap);
+  } else {
+    (void)extract_wave<true>(v, aff, x, y, z0, z1, base, pool, pool_cap);
+  }
+}
+// Pass C: listed wave i's items from the pool to offsets[wave] (first cap
+// items of the canonical order only); per = floats per item.
+__global__ __launch_bounds__(256) void k_extract_copy(const unsigned *__restrict__ list, unsigned nlist,
+                                                      const unsigned *__restrict__ counts,
+                                                      const unsigned long long *__restrict__ pool_at,
+                                                      const unsigned long long *__restrict__ offsets,
+                                                      const float *__restrict__ pool, float *out,
+                                                      unsigned long long cap, int per) {
+  const unsigned i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= nlist) return;
+  const int lane = threadIdx.x & 63;
+  const unsigned w = list[i];
+  const unsigned long long o = offsets[w];
+  if (o >= cap) return;
+  const unsigned long long n = min((unsigned long long)counts[w], cap - o);
+  const float *src = pool + pool_at[w] * per;
+  float *dst = out + o * per;
+  for (unsigned long long k = lane; k < n * per; k += 64) dst[k] = src[k];
 }
 
 // Exclusive scan of n u32 counts into u64 offsets (one 1024-thread block per
@@ -3524,19 +3511,25 @@ void launch_mesh(hipStream_t s, const VolView &v, DevPose vpose, int zlo, int zh
     hipLaunchKernelGGL(k_mesh<false>, grd, dim3(256), 0, s, v, vpose, zlo, zhi, tab, counts, offsets, out, cap);
 }
 size_t scan_blocks(size_t n) { return (n + 4095) / 4096; }
-size_t extract1_blocks(const VolView &v, int zlo, int zhi) {
-  return (size_t)((v.tiles_x * v.tiles_y + 3) / 4) * (size_t)extract_chunks(zlo, zhi);
-}
-void launch_extract1(hipStream_t s, const VolView &v, DevPose vpose, int zlo, int zhi, const uint8_t *tab,
-                     unsigned long long *state, float *out, unsigned long long cap, unsigned long long *total,
-                     unsigned *err) {
+void launch_extract_pool(hipStream_t s, const VolView &v, DevPose vpose, int zlo, int zhi, const uint8_t *tab,
+                         unsigned *counts, unsigned long long *ctr, unsigned long long *pool_at, unsigned *list,
+                         float *pool, unsigned long long pool_cap, unsigned *overflow) {
   const int nc = extract_chunks(zlo, zhi);
   if (nc == 0) return;
   dim3 grd((v.tiles_x * v.tiles_y + 3) / 4, nc);
   if (tab)
-    hipLaunchKernelGGL(k_extract1<true>, grd, dim3(256), 0, s, v, vpose, zlo, zhi, tab, state, out, cap, total, err);
+    hipLaunchKernelGGL(k_extract_pool<true>, grd, dim3(256), 0, s, v, vpose, zlo, zhi, tab, counts, ctr, pool_at,
+                       list, pool, pool_cap, overflow);
   else
-    hipLaunchKernelGGL(k_extract1<false>, grd, dim3(256), 0, s, v, vpose, zlo, zhi, tab, state, out, cap, total, err);
+    hipLaunchKernelGGL(k_extract_pool<false>, grd, dim3(256), 0, s, v, vpose, zlo, zhi, tab, counts, ctr, pool_at,
+                       list, pool, pool_cap, overflow);
+}
+void launch_extract_copy(hipStream_t s, const unsigned *list, unsigned nlist, const unsigned *counts,
+                         const unsigned long long *pool_at, const unsigned long long *offsets, const float *pool,
+                         float *out, unsigned long long cap, int per) {
+  if (nlist == 0) return;
+  hipLaunchKernelGGL(k_extract_copy, dim3((nlist + 3) / 4), dim3(256), 0, s, list, nlist, counts, pool_at, offsets,
+                     pool, out, cap, per);
 }
 void launch_scan(hipStream_t s, const unsigned *counts, unsigned long long *offsets,
                  unsigned long long *bsum, size_t n, unsigned long long *total) {

@@ -35,7 +35,7 @@ EXPORTS = [
     "kfx_stage_icp", "kfx_stage_integrate", "kfx_stage_raycast", "kfx_set_profiling", "kfx_get_stage_ms",
     "kfx_integrate_counts", "kfx_integrate_stats", "kfx_raycast_stats", "kfx_download_columns", "kfx_pipeline_async", "kfx_pipeline_async_u16", "kfx_register_host_buffer", "kfx_unregister_host_buffer", "kfx_slab_mask_payload", "kfx_slab_expand", "kfx_set_icp_allreduce", "kfx_create_slab", "kfx_create_slab_cuts", "kfx_slice_work", "kfx_slice_work_parts", "kfx_slab_balance", "kfx_slab_info", "kfx_comm_get_unique_id", "kfx_comm_init",
     "kfx_pipeline_group", "kfx_slab_frame_local", "kfx_slab_frame_finish", "kfx_render", "kfx_volume_checksum", "kfx_extract_points", "kfx_write_ply", "kfx_save_pointcloud",
-    "kfx_extract_mesh", "kfx_write_ply_mesh", "kfx_get_extract_ms", "kfx_set_extract_passes",
+    "kfx_extract_mesh", "kfx_write_ply_mesh", "kfx_get_extract_ms", "kfx_set_extract_passes", "kfx_get_extract_passes",
     "kfx_dataset_open", "kfx_dataset_info", "kfx_dataset_read", "kfx_dataset_close", "kfx_png_info",
     "kfx_png_read_bgr8", "kfx_png_read_depth", "kfx_parse_intr",
 ]
@@ -129,6 +129,7 @@ def lib():
         "kfx_extract_mesh": ([vp, P(f), C.c_int64, P(C.c_int64)], i),
         "kfx_get_extract_ms": ([vp, P(f)], i),
         "kfx_set_extract_passes": ([vp, i], i),
+        "kfx_get_extract_passes": ([vp, P(i)], i),
         "kfx_write_ply_mesh": ([C.c_char_p, P(f), C.c_int64], i),
         "kfx_dataset_open": ([C.c_char_p, P(vp)], i),
         "kfx_dataset_info": ([vp, P(Intrinsics), P(i), P(i)], i),
@@ -515,11 +516,13 @@ class KinectFusion:
         _check(lib().kfx_set_extract_passes(self._h, int(passes)), "kfx_set_extract_passes")
 
     def extract_ms(self) -> dict:
-        """Device ms of the last extract_points / extract_mesh: count pass, scan, emit pass
-        (a single-pass extraction reports its one pass as count, scan = emit = 0)."""
+        """Device ms of the last extract_points / extract_mesh: the volume pass, the offset
+        scan, and the pool copy (one volume read, passes = 1) or the emit pass (passes = 2)."""
         a = (C.c_float * 3)()
         _check(lib().kfx_get_extract_ms(self._h, a), "kfx_get_extract_ms")
-        return {"count": a[0], "scan": a[1], "emit": a[2]}
+        n = C.c_int()
+        _check(lib().kfx_get_extract_passes(self._h, C.byref(n)), "kfx_get_extract_passes")
+        return {"count": a[0], "scan": a[1], "emit": a[2], "passes": n.value}
 
     def save_pointcloud(self, path: str, cap: int = 0):
         _check(lib().kfx_save_pointcloud(self._h, path.encode(), cap), "kfx_save_pointcloud")

@@ -102,20 +102,21 @@ def test_mesh_matches_oracle(fused, tmp_path):
 
 @pytest.mark.parametrize("mesh", [False, True])
 def test_single_pass_equals_two_pass(mesh, fused):
-    """The single-pass extraction (count, decoupled look-back offsets, emit in
-    one volume read) gives the two-pass result (count pass, offset scan, emit
-    pass) bit for bit, full and capped, and the count-only call's total."""
+    """The one-read extraction (count + items into a pool, offset scan, pool
+    copy in canonical order) gives the two-pass result (count pass, offset
+    scan, emit pass) bit for bit, full and capped (a cap below the total
+    overflows the pool and takes the emit pass), and the count-only total."""
     kf, p, _ = fused
     fn = kf.extract_mesh if mesh else kf.extract_points
     one = fn(cap=50_000_000)
-    ms1 = kf.extract_ms()
-    assert ms1["count"] > 0 and ms1["scan"] == 0 and ms1["emit"] == 0  # one pass ran
-    capped = fn(cap=1234)
+    assert kf.extract_ms()["passes"] == 1  # one volume read (pool + copy)
+    capped = fn(cap=1234)  # fewer slots than items: the pool overflows, the emit pass writes
+    assert kf.extract_ms()["passes"] == 2
     kf.set_extract_passes(2)
     try:
         two = fn(cap=50_000_000)
         ms2 = kf.extract_ms()
-        assert ms2["emit"] > 0
+        assert ms2["emit"] > 0 and ms2["passes"] == 2
         two_capped = fn(cap=1234)
     finally:
         kf.set_extract_passes(1)
