@@ -524,6 +524,9 @@ constexpr int kIcpPix = KFX_ICP_PIX;
 #ifndef KFX_EXTRACT_SKIP
 #define KFX_EXTRACT_SKIP 1  // point / mesh extraction: waves of clear bricks read nothing
 #endif
+#ifndef KFX_XSWEEP_WAVES
+#define KFX_XSWEEP_WAVES 65536  // extraction: units per wave grow (up to 64) while this many waves remain
+#endif
 #ifndef KFX_RAY_SLAB_SKIP
 #define KFX_RAY_SLAB_SKIP 1  // slab raycast: rays jump over the samples before the stored slices
 #endif
@@ -2628,30 +2631,6 @@ __device__ __forceinline__ unsigned extract_wave(const VolView &v, const DevPose
   return total;
 }
 
-template <bool kEmit>
-__global__ __launch_bounds__(256) void k_extract(VolView v, DevPose aff, int zlo, int zhi,
-                                                 unsigned *counts, const unsigned long long *offsets,
-                                                 float *out, unsigned long long cap) {
-  const int lane = threadIdx.x & 63;
-  const int ntiles = v.tiles_x * v.tiles_y;
-  const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (tile >= ntiles) return;
-  const size_t wave = (size_t)blockIdx.y * ntiles + tile;
-  const int x = (tile % v.tiles_x) * 8 + (lane & 7);
-  const int y = (tile / v.tiles_x) * 8 + (lane >> 3);
-  // chunks are aligned to global multiples of kExtractZ (slab boundaries are
-  // too), so concatenating slabs in rank order reproduces the single volume
-  const int c0 = (zlo / kExtractZ) * kExtractZ + (int)blockIdx.y * kExtractZ;
-  const int z0 = max(zlo, c0), z1 = min(zhi, c0 + kExtractZ);
-  static_assert(kExtractZ == 8, "one brick per wave");
-  if (KFX_EXTRACT_SKIP && brick_clear(v, tile, c0)) {  // wave-uniform
-    if (!kEmit && lane == 0) counts[wave] = 0;
-    return;
-  }
-  const unsigned total = extract_wave<kEmit>(v, aff, x, y, z0, z1, kEmit ? offsets[wave] : 0ull, out, cap);
-  if (!kEmit && lane == 0) counts[wave] = total;
-}
-
 // Marching cubes (§8 f5; C5 asks for a mesh, the reference has none).  Cube
 // (x, y, z) = the 8 voxels (x+dx, y+dy, z+dz); all 8 must have weight > 0;
 // corner c = dx | dy<<1 | dz<<2 is inside when its tsdf < 0.  `tab` (256 x
@@ -2730,28 +2709,6 @@ __device__ __forceinline__ unsigned mesh_wave(const VolView &v, const DevPose &a
   return total;
 }
 
-template <bool kEmit>
-__global__ __launch_bounds__(256) void k_mesh(VolView v, DevPose aff, int zlo, int zhi,
-                                              const uint8_t *__restrict__ tab, unsigned *counts,
-                                              const unsigned long long *offsets, float *out,
-                                              unsigned long long cap) {
-  const int lane = threadIdx.x & 63;
-  const int ntiles = v.tiles_x * v.tiles_y;
-  const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (tile >= ntiles) return;
-  const size_t wave = (size_t)blockIdx.y * ntiles + tile;
-  const int x = (tile % v.tiles_x) * 8 + (lane & 7);
-  const int y = (tile / v.tiles_x) * 8 + (lane >> 3);
-  const int c0 = (zlo / kExtractZ) * kExtractZ + (int)blockIdx.y * kExtractZ;
-  const int z0 = max(zlo, c0), z1 = min(zhi, c0 + kExtractZ);
-  if (KFX_EXTRACT_SKIP && brick_clear(v, tile, c0)) {  // wave-uniform
-    if (!kEmit && (threadIdx.x & 63) == 0) counts[wave] = 0;
-    return;
-  }
-  const unsigned total = mesh_wave<kEmit>(v, aff, tab, x, y, z0, z1, kEmit ? offsets[wave] : 0ull, out, cap);
-  if (!kEmit && lane == 0) counts[wave] = total;
-}
-
 // Extraction with ONE read of the volume (points or marching cubes).
 // Pass A (k_extract_pool): each canonical wave counts its brick's items and,
 // if it has any, reserves that many slots of a pool with one 64-bit atomic
@@ -2765,47 +2722,75 @@ __global__ __launch_bounds__(256) void k_mesh(VolView v, DevPose aff, int zlo, i
 // and the host then runs the emit pass of the two-pass path instead.
 constexpr int kPoolListShift = 40;
 constexpr unsigned long long kPoolMask = (1ull << kPoolListShift) - 1ull;
-template <bool kMesh>
-__global__ __launch_bounds__(256) void k_extract_pool(VolView v, DevPose aff, int zlo, int zhi,
-                                                      const uint8_t *__restrict__ tab, unsigned *counts,
-                                                      unsigned long long *ctr, unsigned long long *pool_at,
-                                                      unsigned *list, float *pool, unsigned long long pool_cap,
-                                                      unsigned *overflow) {
+enum XMode { kXCount = 0, kXEmit = 1, kXPool = 2 };
+// The extraction passes.  A unit = one tile x one 8-slice chunk (the
+// canonical order's (chunk, tile)); each wave sweeps 64 consecutive units of
+// one chunk (K = 1..64, xsweep_units): lane l tests unit T0 + l's brick in
+// the occupancy map, a clear brick's unit has no items (count 0, no voxel
+// read), and the others are processed one after another by the whole wave
+// (lane = column).  At 2048^3 (16.8 M units, mostly clear) a wave per unit
+// is launch-bound (count pass 8.3 ms; 64 units per wave: 6.8 ms for count +
+// pool emit); small volumes keep enough waves with a small K.
+// kXCount: counts[unit]; kXEmit: items at offsets[unit] (first cap only);
+// kXPool: counts[unit] and the items into the pool (above).
+template <int kMode, bool kMesh>
+__global__ __launch_bounds__(256) void k_xsweep(VolView v, DevPose aff, int zlo, int zhi,
+                                                const uint8_t *__restrict__ tab, unsigned *counts,
+                                                const unsigned long long *offsets, float *out,
+                                                unsigned long long cap, unsigned long long *ctr,
+                                                unsigned long long *pool_at, unsigned *list, unsigned *overflow,
+                                                int K) {
   const int lane = threadIdx.x & 63;
   const int ntiles = v.tiles_x * v.tiles_y;
-  const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (tile >= ntiles) return;
-  const size_t wave = (size_t)blockIdx.y * ntiles + tile;
-  const int x = (tile % v.tiles_x) * 8 + (lane & 7);
-  const int y = (tile / v.tiles_x) * 8 + (lane >> 3);
+  const int T0 = (int)(blockIdx.x * 4 + (threadIdx.x >> 6)) * K;
+  if (T0 >= ntiles) return;
+  // chunks are aligned to global multiples of kExtractZ (slab boundaries are
+  // too), so concatenating slabs in rank order reproduces the single volume
   const int c0 = (zlo / kExtractZ) * kExtractZ + (int)blockIdx.y * kExtractZ;
   const int z0 = max(zlo, c0), z1 = min(zhi, c0 + kExtractZ);
-  if (KFX_EXTRACT_SKIP && brick_clear(v, tile, c0)) {  // wave-uniform
-    if (lane == 0) counts[wave] = 0;
-    return;
-  }
-  const unsigned n = kMesh ? mesh_wave<false>(v, aff, tab, x, y, z0, z1, 0ull, pool, 0ull)
-                           : extract_wave<false>(v, aff, x, y, z0, z1, 0ull, pool, 0ull);
-  if (lane == 0) counts[wave] = n;
-  if (n == 0) return;  // wave-uniform
-  unsigned long long old = 0;
-  if (lane == 0) old = atomicAdd(ctr, (1ull << kPoolListShift) | (unsigned long long)n);
-  old = __shfl(old, 0);
-  const unsigned long long base = old & kPoolMask;
-  if (lane == 0) {
-    list[old >> kPoolListShift] = (unsigned)wave;
-    pool_at[wave] = base;
-  }
-  if (base + n > pool_cap) {
-    if (lane == 0) atomicOr(overflow, 1u);
-    return;
-  }
-  // the items again from the bricks just read (cache hits; staging them in
-  // LDS during the count measured slower: occupancy)
-  if (kMesh) {
-    (void)mesh_wave<true>(v, aff, tab, x, y, z0, z1, base, pool, pool_cap);
-  } else {
-    (void)extract_wave<true>(v, aff, x, y, z0, z1, base, pool, pool_cap);
+  static_assert(kExtractZ == 8, "one brick per unit");
+  const size_t ubase = (size_t)blockIdx.y * ntiles;  // unit index = ubase + tile
+  const int tl = T0 + lane;
+  const bool mine = lane < K && tl < ntiles;
+  const bool have = mine && !(KFX_EXTRACT_SKIP && brick_clear(v, tl, c0));
+  if (kMode != kXEmit && mine && !have) counts[ubase + tl] = 0u;
+  unsigned long long work = __ballot(have);
+  while (work) {  // wave-uniform
+    const int t = __ffsll((long long)work) - 1;
+    work &= work - 1ull;
+    const int tile = T0 + t;
+    const size_t unit = ubase + tile;
+    const int x = (tile % v.tiles_x) * 8 + (lane & 7);
+    const int y = (tile / v.tiles_x) * 8 + (lane >> 3);
+    if (kMode == kXEmit) {
+      if (kMesh)
+        (void)mesh_wave<true>(v, aff, tab, x, y, z0, z1, offsets[unit], out, cap);
+      else
+        (void)extract_wave<true>(v, aff, x, y, z0, z1, offsets[unit], out, cap);
+      continue;
+    }
+    const unsigned n = kMesh ? mesh_wave<false>(v, aff, tab, x, y, z0, z1, 0ull, out, 0ull)
+                             : extract_wave<false>(v, aff, x, y, z0, z1, 0ull, out, 0ull);
+    if (lane == 0) counts[unit] = n;
+    if (kMode != kXPool || n == 0) continue;
+    unsigned long long old = 0;
+    if (lane == 0) old = atomicAdd(ctr, (1ull << kPoolListShift) | (unsigned long long)n);
+    old = __shfl(old, 0);
+    const unsigned long long base = old & kPoolMask;
+    if (lane == 0) {
+      list[old >> kPoolListShift] = (unsigned)unit;
+      pool_at[unit] = base;
+    }
+    if (base + n > cap) {  // (cap = the pool's size here)
+      if (lane == 0) atomicOr(overflow, 1u);
+      continue;
+    }
+    // the items again from the brick just read (cache hits; staging them in
+    // LDS during the count measured slower: occupancy)
+    if (kMesh)
+      (void)mesh_wave<true>(v, aff, tab, x, y, z0, z1, base, out, cap);
+    else
+      (void)extract_wave<true>(v, aff, x, y, z0, z1, base, out, cap);
   }
 }
 // Pass C: listed wave i's items from the pool to offsets[wave] (first cap
@@ -3485,44 +3470,45 @@ static int extract_chunks(int zlo, int zhi) {
 size_t extract_waves(const VolView &v, int zlo, int zhi) {
   return (size_t)v.tiles_x * v.tiles_y * (size_t)extract_chunks(zlo, zhi);
 }
+template <int kMode>
+static void launch_xsweep(hipStream_t s, const VolView &v, DevPose vpose, int zlo, int zhi, const uint8_t *tab,
+                          unsigned *counts, const unsigned long long *offsets, float *out, unsigned long long cap,
+                          unsigned long long *ctr, unsigned long long *pool_at, unsigned *list, unsigned *overflow) {
+  const int nc = extract_chunks(zlo, zhi);
+  if (nc == 0) return;
+  const int tiles = v.tiles_x * v.tiles_y;
+  // units per wave: as many as keep >= 64 K waves (at least 1, at most 64)
+  const size_t units = (size_t)tiles * nc;
+  int K = 1;
+  while (K < 64 && units / (size_t)(2 * K) >= (size_t)KFX_XSWEEP_WAVES) K *= 2;
+  dim3 grd((tiles + 4 * K - 1) / (4 * K), nc);  // 4 waves of K units per block
+  if (tab)
+    hipLaunchKernelGGL((k_xsweep<kMode, true>), grd, dim3(256), 0, s, v, vpose, zlo, zhi, tab, counts, offsets, out,
+                       cap, ctr, pool_at, list, overflow, K);
+  else
+    hipLaunchKernelGGL((k_xsweep<kMode, false>), grd, dim3(256), 0, s, v, vpose, zlo, zhi, tab, counts, offsets, out,
+                       cap, ctr, pool_at, list, overflow, K);
+}
 void launch_extract(hipStream_t s, const VolView &v, DevPose vpose, int zlo, int zhi,
                     unsigned *counts, const unsigned long long *offsets, float *out,
                     unsigned long long cap) {
-  const int nc = extract_chunks(zlo, zhi);
-  if (nc == 0) return;
-  const int tiles = v.tiles_x * v.tiles_y;
-  dim3 grd((tiles + 3) / 4, nc);
   if (offsets)
-    hipLaunchKernelGGL(k_extract<true>, grd, dim3(256), 0, s, v, vpose, zlo, zhi, counts, offsets,
-                       out, cap);
+    launch_xsweep<kXEmit>(s, v, vpose, zlo, zhi, nullptr, counts, offsets, out, cap, nullptr, nullptr, nullptr, nullptr);
   else
-    hipLaunchKernelGGL(k_extract<false>, grd, dim3(256), 0, s, v, vpose, zlo, zhi, counts, offsets,
-                       out, cap);
+    launch_xsweep<kXCount>(s, v, vpose, zlo, zhi, nullptr, counts, nullptr, nullptr, 0, nullptr, nullptr, nullptr, nullptr);
 }
 void launch_mesh(hipStream_t s, const VolView &v, DevPose vpose, int zlo, int zhi, const uint8_t *tab,
                  unsigned *counts, const unsigned long long *offsets, float *out, unsigned long long cap) {
-  const int nc = extract_chunks(zlo, zhi);
-  if (nc == 0) return;
-  const int tiles = v.tiles_x * v.tiles_y;
-  dim3 grd((tiles + 3) / 4, nc);
   if (offsets)
-    hipLaunchKernelGGL(k_mesh<true>, grd, dim3(256), 0, s, v, vpose, zlo, zhi, tab, counts, offsets, out, cap);
+    launch_xsweep<kXEmit>(s, v, vpose, zlo, zhi, tab, counts, offsets, out, cap, nullptr, nullptr, nullptr, nullptr);
   else
-    hipLaunchKernelGGL(k_mesh<false>, grd, dim3(256), 0, s, v, vpose, zlo, zhi, tab, counts, offsets, out, cap);
+    launch_xsweep<kXCount>(s, v, vpose, zlo, zhi, tab, counts, nullptr, nullptr, 0, nullptr, nullptr, nullptr, nullptr);
 }
 size_t scan_blocks(size_t n) { return (n + 4095) / 4096; }
 void launch_extract_pool(hipStream_t s, const VolView &v, DevPose vpose, int zlo, int zhi, const uint8_t *tab,
                          unsigned *counts, unsigned long long *ctr, unsigned long long *pool_at, unsigned *list,
                          float *pool, unsigned long long pool_cap, unsigned *overflow) {
-  const int nc = extract_chunks(zlo, zhi);
-  if (nc == 0) return;
-  dim3 grd((v.tiles_x * v.tiles_y + 3) / 4, nc);
-  if (tab)
-    hipLaunchKernelGGL(k_extract_pool<true>, grd, dim3(256), 0, s, v, vpose, zlo, zhi, tab, counts, ctr, pool_at,
-                       list, pool, pool_cap, overflow);
-  else
-    hipLaunchKernelGGL(k_extract_pool<false>, grd, dim3(256), 0, s, v, vpose, zlo, zhi, tab, counts, ctr, pool_at,
-                       list, pool, pool_cap, overflow);
+  launch_xsweep<kXPool>(s, v, vpose, zlo, zhi, tab, counts, nullptr, pool, pool_cap, ctr, pool_at, list, overflow);
 }
 void launch_extract_copy(hipStream_t s, const unsigned *list, unsigned nlist, const unsigned *counts,
                          const unsigned long long *pool_at, const unsigned long long *offsets, const float *pool,
