@@ -388,6 +388,15 @@ int kfx_slice_work(kfx_ctx *ctx, const uint8_t *bgr, const float *depth_mm, int6
 int kfx_slice_work_parts(kfx_ctx *ctx, const uint8_t *bgr, const float *depth_mm, int64_t *cover,
                          int64_t *updated);
 int kfx_slab_balance(const int64_t *slice_work, int Z, int world, int *cuts);
+/* Bounded slab raycast: a slab that combines with others over
+ * a communicator or in a kfx_pipeline_group marches each ray only up to the
+ * previous frame's model distance along it (+ 16 voxels + 2 %), records where
+ * it stopped, and after the all-reduce of [keys | stop points] re-marches the
+ * pixels no slab resolved below that point (an exact second pass), so slabs
+ * behind the visible surface skip the occluded space.  mode 0: off (every
+ * ray marched to its end); 1: on (default); 2: on without the margin (test:
+ * most pixels take the second pass).  Results are identical in every mode. */
+int kfx_set_slab_bound(kfx_ctx *ctx, int mode);
 /* stored slices [zb, zb+zn), owned slices [own0, own1) */
 int kfx_slab_info(kfx_ctx *ctx, int *zb, int *zn, int *own0, int *own1);
 /* One process per GPU: rank 0 creates the id, every rank passes it to

@@ -82,8 +82,9 @@ constexpr int kInitialPoseCap = 1 << 16;
 }  // namespace
 
 // per-frame stage events: [0] start, [1] preprocess done, [2] ICP done,
-// [3] integrate done, [4] frame done, [5] local raycast done, [6] combine starts
-constexpr int kStageEvents = 7;
+// [3] integrate done, [4] frame done, [5] local raycast done, [6] combine starts,
+// [7] / [8] a group combine's shared part (reductions, masks, resume) starts / ends
+constexpr int kStageEvents = 9;
 
 struct kfx_ctx {
   int device = 0;
@@ -162,8 +163,14 @@ struct kfx_ctx {
   int rank = 0, world = 1;
   uint8_t *render = nullptr;      // kfx_render output (allocated on first use)
   uint8_t *mc_tab = nullptr;      // marching-cubes table (uploaded on first use)
-  uint32_t *key_local = nullptr;  // per-pixel sample index of this slab's decisive event
-  uint32_t *key_min = nullptr;    // all-reduce MIN of key_local over the slabs
+  // per pixel: [key | pend | Ts | nx | ny | nz] planes (k_raycast<kSlab>): the
+  // sample index of this slab's decisive event, the first sample a bounded
+  // march left unexamined, and the hit payload
+  uint32_t *key_local = nullptr;
+  uint32_t *key_min = nullptr;    // all-reduce MIN of the [key | pend] planes over the slabs
+  int slab_bound = 1;             // kfx_set_slab_bound: 0 off, 1 on, 2 on without margin (tests)
+  bool group_combine = false;     // kfx_pipeline_group member (in-process combine), this call only
+  bool pass1_bounded = false;     // the frame's slab raycast was bounded: the combine runs pass 2
   // kfx_pipeline_async: host frames copied into a pinned ring slot, uploaded on
   // the copy stream while earlier frames run (slot reuse ordered by events)
   static constexpr int kRing = 4;
@@ -293,12 +300,15 @@ void enqueue_pre(kfx_ctx *c, FrameInput in, hipEvent_t *ev);
 void enqueue_local(kfx_ctx *c, FrameInput in, hipEvent_t *ev);
 int enqueue_track(kfx_ctx *c, FrameInput in, hipEvent_t *ev, bool begin);
 int enqueue_combine(kfx_ctx *c);
+void enqueue_slab_resume(kfx_ctx *c, hipStream_t s);
 
 int enqueue_frame(kfx_ctx *c, FrameInput in, hipEvent_t *ev) {
   enqueue_pre(c, in, ev);
   int r = enqueue_track(c, in, ev, false);
   if (ev) (void)hipEventRecord(ev[5], c->stream);
   if (ev) (void)hipEventRecord(ev[6], c->stream);
+  if (ev) (void)hipEventRecord(ev[7], c->stream);  // (no shared part: [7] = [8])
+  if (ev) (void)hipEventRecord(ev[8], c->stream);
   if (!r && c->slab) r = enqueue_combine(c);
   if (ev) (void)hipEventRecord(ev[4], c->stream);
   return r;
@@ -312,15 +322,21 @@ int enqueue_frame(kfx_ctx *c, FrameInput in, hipEvent_t *ev) {
   } while (0)
 
 // Cross-slab raycast combine: all-reduce MIN of the per-pixel
-// event keys, each slab clears the payload {Ts, nout} of the pixels it lost,
+// event keys (with the pend plane when the slabs' marches were bounded, and
+// then the resume pass for the pixels no slab resolved, and a MIN of the keys
+// again), each slab clears the payload {Ts, nout} of the pixels it lost,
 // all-reduce MAX of the payload bits (16 B per pixel instead of the 24 B of
 // vmap|nmap), every rank rebuilds the level-0 maps from it, then the pyramid.
 int enqueue_combine(kfx_ctx *c) {
   hipStream_t s = c->stream;
   const size_t np = (size_t)c->g[0].w * c->g[0].h;
-  uint32_t *pay = c->key_local + np;  // [Ts | nx | ny | nz] planes after the keys
+  uint32_t *pay = c->key_local + 2 * np;  // [Ts | nx | ny | nz] planes after [keys | pend]
   if (c->world > 1 || c->comm) {
     if (!c->comm) return set_err(KFX_ERR_STATE, "slab context without a communicator (kfx_comm_init, or kfx_pipeline_group)");
+    if (c->pass1_bounded) {
+      NCCLCHK(ncclAllReduce(c->key_local, c->key_min, 2 * np, ncclUint32, ncclMin, c->comm, s));
+      enqueue_slab_resume(c, s);
+    }
     NCCLCHK(ncclAllReduce(c->key_local, c->key_min, np, ncclUint32, ncclMin, c->comm, s));
     launch_slab_mask(s, c->key_local, c->key_min, (int)np);
     NCCLCHK(ncclAllReduce(pay, pay, 4 * np, ncclUint32, ncclMax, c->comm, s));
@@ -375,6 +391,28 @@ int enqueue_icp_sharded(kfx_ctx *c, bool begin) {
   return KFX_OK;
 }
 
+// The slab raycast's first pass is bounded by the previous frame's model
+// (SlabPass) when the frame's combine can run the resume pass: several slabs
+// combined over a communicator or in-process (kfx_pipeline_group)
+SlabPass slab_pass1(kfx_ctx *c) {
+  SlabPass sp;
+  c->pass1_bounded = c->slab && c->slab_bound && c->world > 1 && (c->comm || c->group_combine);
+  if (c->pass1_bounded) {
+    sp.pass = 1;
+    sp.bound_abs = c->slab_bound == 2 ? 0.f : 16.f * c->vol.vs[0];  // 16 voxels
+    sp.bound_rel = c->slab_bound == 2 ? 0.f : 0.02f;
+  }
+  return sp;
+}
+// pass 2: the pixels this slab left pending below the reduced [key | pend]
+void enqueue_slab_resume(kfx_ctx *c, hipStream_t s) {
+  SlabPass sp;
+  sp.pass = 2;
+  sp.kmin = c->key_min;
+  launch_raycast(s, c->vol, c->L, c->g, c->cur, c->prev, c->st, c->pose_log, to_dev(c->p.volu_pose), nullptr,
+                 c->key_local, nullptr, sp);
+}
+
 // integrate + raycast of the frame whose maps are in the current set
 void enqueue_map(kfx_ctx *c, FrameInput in, hipEvent_t *ev) {
   hipStream_t s = c->stream;
@@ -382,7 +420,7 @@ void enqueue_map(kfx_ctx *c, FrameInput in, hipEvent_t *ev) {
                    to_dev(c->p.volu_pose), nullptr, nullptr);
   if (ev) (void)hipEventRecord(ev[3], s);
   launch_raycast(s, c->vol, c->L, c->g, c->cur, c->prev, c->st, c->pose_log,
-                 to_dev(c->p.volu_pose), nullptr, c->slab ? c->key_local : nullptr);
+                 to_dev(c->p.volu_pose), nullptr, c->slab ? c->key_local : nullptr, nullptr, slab_pass1(c));
 }
 
 // The persistent ICP launch, if this context uses it.  False when it does not,
@@ -455,6 +493,8 @@ int enqueue_main_overlap(kfx_ctx *c, FrameInput in, hipEvent_t *ev) {
   int r = enqueue_track(c, in, ev, true);
   if (ev) HIPCHK(hipEventRecord(ev[5], c->stream));
   if (ev) HIPCHK(hipEventRecord(ev[6], c->stream));
+  if (ev) HIPCHK(hipEventRecord(ev[7], c->stream));
+  if (ev) HIPCHK(hipEventRecord(ev[8], c->stream));
   if (!r && c->slab) r = enqueue_combine(c);
   if (ev) HIPCHK(hipEventRecord(ev[4], c->stream));
   return r;
@@ -956,8 +996,8 @@ static int create_impl(const kfx_intrinsics *intr, const kfx_params *params, int
   }
   const size_t np0 = (size_t)intr->width * intr->height;
   if (slab) {
-    if ((r = dalloc(c, (void **)&c->key_local, np0 * 4 * 5))) return fail(r);  // keys + payload
-    if ((r = dalloc(c, (void **)&c->key_min, np0 * 4))) return fail(r);
+    if ((r = dalloc(c, (void **)&c->key_local, np0 * 4 * 6))) return fail(r);  // keys, pend + payload
+    if ((r = dalloc(c, (void **)&c->key_min, np0 * 4 * 2))) return fail(r);
   }
   if ((r = dalloc(c, (void **)&c->raw0_u16, np0 * 2))) return fail(r);
   if ((r = dalloc(c, (void **)&c->bgr, np0 * 3))) return fail(r);
@@ -1264,13 +1304,15 @@ int kfx_get_kernel_timing_ex(kfx_ctx *c, float out_ms[4], int *n_samples) {
   // sample events: [2] ICP done, [3] integrate done, [5] local raycast done,
   // [6] combine starts (group members: after the other members' local phases),
   // [4] frame done; [1] the frame's tracking starts
-  static const int kFrom[4] = {1, 2, 3, 6}, kTo[4] = {2, 3, 5, 4};
+  // [7]..[8] the shared part of a group combine (elapsed 0 elsewhere), added
+  // to the member's own combine [6]..[4]
+  static const int kFrom[5] = {1, 2, 3, 6, 7}, kTo[5] = {2, 3, 5, 4, 8};
   double acc[4] = {0, 0, 0, 0};
   for (size_t k = 0; k < c->tnext; ++k) {
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < 5; ++i) {
       float ms = 0.f;
       HIPCHK(hipEventElapsedTime(&ms, c->tsets[kStageEvents * k + kFrom[i]], c->tsets[kStageEvents * k + kTo[i]]));
-      acc[i] += ms;
+      acc[i < 4 ? i : 3] += ms;
     }
   }
   for (int i = 0; i < 4; ++i) out_ms[i] = c->tnext ? (float)(acc[i] / (double)c->tnext) : 0.f;
@@ -1828,6 +1870,14 @@ static int extract_events(kfx_ctx *c) {
   return KFX_OK;
 }
 
+int kfx_set_slab_bound(kfx_ctx *c, int mode) {
+  int r = check_ctx(c);
+  if (r) return r;
+  if (mode < 0 || mode > 2) return set_err(KFX_ERR_ARG, "slab bound modes are 0, 1, 2");
+  c->slab_bound = mode;
+  return KFX_OK;
+}
+
 int kfx_set_extract_passes(kfx_ctx *c, int passes) {
   int r = check_ctx(c);
   if (r) return r;
@@ -2257,13 +2307,14 @@ int kfx_pipeline_group(kfx_ctx **cs, int n, const uint8_t *bgr, const float *dep
   }
   int r;
   const bool sharded = cs[0]->icp_sharded && n > 1;
-  struct ChainScope {  // group_chain holds for this call only (every exit)
+  struct ChainScope {  // group_chain / group_combine hold for this call only (every exit)
     kfx_ctx **cs;
     int n;
     ~ChainScope() {
-      for (int k = 0; k < n; ++k) cs[k]->group_chain = false;
+      for (int k = 0; k < n; ++k) cs[k]->group_chain = cs[k]->group_combine = false;
     }
   } chain_scope{cs, n};
+  for (int k = 0; k < n; ++k) cs[k]->group_combine = n > 1;
   hipEvent_t *tev[kMaxGroup] = {};  // members' timing samples (replicated ICP only)
   for (int k = 0; k < n; ++k) {  // local phase: preprocess, ICP, integrate, slab raycast
     kfx_ctx *c = cs[k];
@@ -2324,36 +2375,44 @@ int kfx_pipeline_group(kfx_ctx **cs, int n, const uint8_t *bgr, const float *dep
     HIPCHK(hipStreamSynchronize(cs[k]->stream));
   }
   // combine, with the reductions of the collective path run by one kernel over
-  // every member's buffer
+  // every member's buffer.  The shared part (reductions, resume passes,
+  // masks) runs on member 0's stream; each member's timed combine is that
+  // part ([7]..[8]) plus its own expand + pyramid ([6]..[4]) — what one rank
+  // of the RCCL path spends, without the members queuing behind each other.
   uint32_t *kin[kMaxGroup], *kout[kMaxGroup], *pay[kMaxGroup];
   for (int k = 0; k < n; ++k) {
     kin[k] = cs[k]->key_local;
     kout[k] = cs[k]->key_min;
-    pay[k] = cs[k]->key_local + np;
+    pay[k] = cs[k]->key_local + 2 * np;
   }
   kfx_ctx *c0 = cs[0];
   if ((r = check_ctx(c0))) return r;
-  for (int k = 0; k < n; ++k)  // every member's combine starts with the shared reductions
-    if (tev[k]) HIPCHK(hipEventRecord(tev[k][6], c0->stream));
-  launch_group_reduce(c0->stream, kin, n, kout, n, np, false);
-  HIPCHK(hipGetLastError());
-  HIPCHK(hipStreamSynchronize(c0->stream));
-  for (int k = 0; k < n; ++k) {
-    if ((r = check_ctx(cs[k]))) return r;
-    launch_slab_mask(cs[k]->stream, cs[k]->key_local, cs[k]->key_min, (int)np);
-    HIPCHK(hipStreamSynchronize(cs[k]->stream));
+  hipStream_t s0 = c0->stream;
+  for (int k = 0; k < n; ++k)
+    if (tev[k]) HIPCHK(hipEventRecord(tev[k][7], s0));
+  if (c0->pass1_bounded) {  // [key | pend] MIN, then the resume passes
+    launch_group_reduce(s0, kin, n, kout, n, 2 * np, false);
+    for (int k = 0; k < n; ++k) enqueue_slab_resume(cs[k], s0);
   }
-  if ((r = check_ctx(c0))) return r;
-  launch_group_reduce(c0->stream, pay, n, pay, n, 4 * np, true);
-  HIPCHK(hipStreamSynchronize(c0->stream));
+  launch_group_reduce(s0, kin, n, kout, n, np, false);
+  for (int k = 0; k < n; ++k) launch_slab_mask(s0, cs[k]->key_local, cs[k]->key_min, (int)np);
+  launch_group_reduce(s0, pay, n, pay, n, 4 * np, true);
+  for (int k = 0; k < n; ++k)
+    if (tev[k]) HIPCHK(hipEventRecord(tev[k][8], s0));
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(s0));
   int status = KFX_OK;
   for (int k = 0; k < n; ++k) {
     kfx_ctx *c = cs[k];
     if ((r = check_ctx(c))) return r;
-    launch_slab_expand(c->stream, c->g[0], c->key_local + np, c->cur, c->prev, c->st, c->pose_log,
+    if (tev[k]) HIPCHK(hipEventRecord(tev[k][6], c->stream));
+    launch_slab_expand(c->stream, c->g[0], c->key_local + 2 * np, c->cur, c->prev, c->st, c->pose_log,
                        to_dev(c->p.volu_pose));
     launch_resize(c->stream, c->L, c->g, c->cur, c->prev, c->st, nullptr);
-    if (tev[k]) HIPCHK(hipEventRecord(tev[k][4], c->stream));  // combine = in-process reductions + expand + resize
+    if (tev[k]) {  // timed members run alone (as on a GPU of their own)
+      HIPCHK(hipEventRecord(tev[k][4], c->stream));
+      HIPCHK(hipStreamSynchronize(c->stream));
+    }
     HIPCHK(hipGetLastError());
     c->pending += 1;
     const int s = finish_frame(c);
@@ -2382,9 +2441,11 @@ int kfx_slab_frame_local(kfx_ctx *c, const uint8_t *bgr, const float *depth_mm, 
   enqueue_local(c, {c->raw[0], nullptr, c->bgr}, tev);
   if (tev) HIPCHK(hipEventRecord(tev[5], c->stream));
   if (tev) HIPCHK(hipEventRecord(tev[6], c->stream));  // re-recorded when the combine starts
+  if (tev) HIPCHK(hipEventRecord(tev[7], c->stream));  // (no shared part on the device: [7] = [8])
+  if (tev) HIPCHK(hipEventRecord(tev[8], c->stream));
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(keys, c->key_local, np * 4, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipMemcpyAsync(payload, c->key_local + np, 4 * np * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipMemcpyAsync(payload, c->key_local + 2 * np, 4 * np * 4, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   c->ext_pending = tev;
   c->ext_open = true;
@@ -2398,8 +2459,10 @@ int kfx_slab_frame_finish(kfx_ctx *c, const uint32_t *payload) {
   if (!c->ext_open) return set_err(KFX_ERR_STATE, "kfx_slab_frame_finish without kfx_slab_frame_local");
   c->ext_open = false;
   const size_t np = (size_t)c->intr.width * c->intr.height;
-  uint32_t *pay = c->key_local + np;
+  uint32_t *pay = c->key_local + 2 * np;
   if (c->ext_pending) HIPCHK(hipEventRecord(c->ext_pending[6], c->stream));
+  if (c->ext_pending) HIPCHK(hipEventRecord(c->ext_pending[7], c->stream));
+  if (c->ext_pending) HIPCHK(hipEventRecord(c->ext_pending[8], c->stream));
   HIPCHK(hipMemcpyAsync(pay, payload, 4 * np * 4, hipMemcpyHostToDevice, c->stream));
   launch_slab_expand(c->stream, c->g[0], pay, c->cur, c->prev, c->st, c->pose_log, to_dev(c->p.volu_pose));
   launch_resize(c->stream, c->L, c->g, c->cur, c->prev, c->st, nullptr);

@@ -228,12 +228,24 @@ void launch_integrate(hipStream_t s, VolView v, LevelGeom g0, const float2 *dl0,
                       const float *invl, const uint8_t *bgr, DevState *st, DevPose *log, DevPose vpose,
                       const float *xpose,
                       unsigned long long *counters /* non-null: count-only, 32 words */);
+// Z-slab raycast passes: pass 0 marches every ray to its end;
+// pass 1 stops at the previous frame's model distance along the ray (+
+// bound_abs metres + bound_rel of the distance) and records the first sample
+// it did not examine (pend plane); pass 2 re-marches, unbounded, the pixels
+// whose pend lies below kmin (the MIN-reduced [keys | pend] of pass 1)
+struct SlabPass {
+  int pass = 0;
+  const uint32_t *kmin = nullptr;
+  float bound_abs = 0.f, bound_rel = 0.f;
+};
 // raycast of level 0 + resizePointsNormals of levels >= 1 in one launch; with
-// keys != null the slab variant (owned events only, key per pixel, no resize)
+// keys != null the slab variant (owned events only, key per pixel, no resize;
+// planes [key | pend | Ts | nx | ny | nz])
 // stats (non-null): the statistics variant (6 counters added, nothing stored)
 void launch_raycast(hipStream_t s, VolView v, int levels, const LevelGeom *g, FrameView cur,
                     FrameView prev, const DevState *st, const DevPose *log, DevPose vpose,
-                    const float *xpose, uint32_t *keys, unsigned long long *stats = nullptr);
+                    const float *xpose, uint32_t *keys, unsigned long long *stats = nullptr,
+                    const SlabPass &sp = SlabPass{});
 // the reference raycast's distinct voxels read (out[0]) and reads (out[1]),
 // count-only (bits: one bit per stored voxel, workspace)
 void launch_raycast_touch(hipStream_t s, VolView v, LevelGeom g0, const DevState *st, const DevPose *log,

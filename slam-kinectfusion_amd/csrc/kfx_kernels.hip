@@ -1834,6 +1834,12 @@ struct RayArgs {
   LevelGeom g[kMaxLevels];
   int levels;
   unsigned long long *stats;  // k_raycast<.., kStats>: 6 counters
+  // kSlab: 0 unbounded march; 1 bounded by the previous frame's model
+  // distance (+ margin); 2 resume: re-march unbounded the pixels whose pass-1
+  // bound left them unresolved (kmin: the MIN-reduced [keys | pend] planes)
+  int slab_pass;
+  const uint32_t *kmin;
+  float bound_abs, bound_rel;  // pass-1 margin: metres, fraction of the distance
 };
 
 __device__ void resize_tile(const RayArgs &ra, int kind, int tx0, int ty0, int lx, int ly, f3 vout,
@@ -1917,7 +1923,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KFX_RAY_OCC
   const int kind = s_kind;
   f3 vout = {0.f, 0.f, 0.f}, nout = {0.f, 0.f, 0.f};
   uint32_t key = kind == 0 ? 0u : UINT_MAX;  // kSlab: sample index of the decisive event
+  uint32_t pend = UINT_MAX;  // kSlab pass 1: first sample not examined (march stopped at the bound)
   float hts = 0.f;                             // kSlab: Ts of the hit written to the maps
+  // act: this pixel is marched and written.  Resume pass (kSlab, pass 2):
+  // only the pixels this slab left pending below the earliest event any slab
+  // found (MIN-reduced [keys | pend] planes: kmin[o] > own pend) march again,
+  // unbounded; the others keep their pass-1 results
+  bool act = inimg;
+  if (kSlab && ra.slab_pass == 2) {
+    const size_t np = (size_t)g.w * g.h;
+    act = inimg && keys[np + o] != UINT_MAX && keys[np + o] < ra.kmin[o];
+    if (!__any(act)) return;  // (k_raycast has no barrier after its setup)
+  }
   if (kind == 0 && inimg) {  // frame 1: the measured maps become the model maps
     vout = ld3(cur.v[0], o);
     nout = ld3(cur.n[0], o);
@@ -1936,7 +1953,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KFX_RAY_OCC
     const float tnear = fmaxf(fmaxf(tmin.x, tmin.y), fmaxf(tmin.x, tmin.z));
     const float tfar = fminf(fminf(tmax.x, tmax.y), fminf(tmax.x, tmax.z));
     float ray_len = fmaxf(tnear, 0.f);
-    bool live = inimg && ray_len < tfar;
+    bool live = act && ray_len < tfar;
+    // pass 1: samples up to kb only (the previous frame's model distance
+    // along this pixel's ray, + margin; no model point: unbounded)
+    uint32_t kb = UINT_MAX;
+    if (kSlab && ra.slab_pass == 1 && live) {
+      const f3 pv = ld3(prev.v[0], o);
+      const float dprev = sqrtf(dot(pv, pv));
+      if (dprev > 0.f) {
+        const float kf = (dprev * (1.f + ra.bound_rel) + ra.bound_abs - ray_len) / rc.step + 1.f;
+        kb = kf < 1.f ? 1u : (kf < 4.0e9f ? (uint32_t)kf : UINT_MAX);
+      }
+    }
     const f3 vstep = mulc(dir, rc.vs);
     ray_len += rc.step;
     f3 nextp = add(org, scl(dir, ray_len));
@@ -2021,6 +2049,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KFX_RAY_OCC
 #endif
     while (__any(live || cand)) {
     while (__any(live)) {
+      if (kSlab && live && kbase > kb) {  // pass-1 bound: samples < kbase examined, no owned event
+        live = false;
+        pend = kbase;
+      }
       if (can_skip && live && sprev >= 0) {
         uint32_t nsk = 0;
         for (;;) {
@@ -2105,6 +2137,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KFX_RAY_OCC
           kbase += nsk;
           tprev = voxel2tsdf(v, rc, nextp);
           sprev = isnan(tprev) ? 0 : (tprev > 0.f ? 1 : (tprev < 0.f ? -1 : 0));
+        }
+        if (kSlab && live && kbase > kb) {  // the skipped samples held no event
+          live = false;
+          pend = kbase;
         }
       }
       if (!__any(live)) break;
@@ -2287,14 +2323,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KFX_RAY_OCC
     }
     return;
   }
-  if (inimg) {
-    if (kSlab) {  // key + payload {Ts, nout} (kfx_internal.h slab combine)
+  if (act) {
+    if (kSlab) {  // key, pend + payload {Ts, nout} (kfx_internal.h slab combine)
       const size_t np = (size_t)g.w * g.h;
       keys[o] = key;
-      keys[np + o] = __float_as_uint(hts);
-      keys[2 * np + o] = __float_as_uint(nout.x);
-      keys[3 * np + o] = __float_as_uint(nout.y);
-      keys[4 * np + o] = __float_as_uint(nout.z);
+      keys[np + o] = pend;
+      keys[2 * np + o] = __float_as_uint(hts);
+      keys[3 * np + o] = __float_as_uint(nout.x);
+      keys[4 * np + o] = __float_as_uint(nout.y);
+      keys[5 * np + o] = __float_as_uint(nout.z);
     } else {
       st3(prev.v[0], o, vout);
       st3(prev.n[0], o, nout);
@@ -2487,7 +2524,7 @@ __global__ __launch_bounds__(256) void k_resize(RayArgs ra, FrameView cur, Frame
 // winner's (kfx_internal.h slab_mask_px).
 __global__ void k_slab_mask(const uint32_t *__restrict__ keys, const uint32_t *__restrict__ key_min, int n) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) slab_mask_px(keys, key_min, const_cast<uint32_t *>(keys) + n, (size_t)n, (size_t)i);
+  if (i < n) slab_mask_px(keys, key_min, const_cast<uint32_t *>(keys) + 2 * (size_t)n, (size_t)n, (size_t)i);
 }
 // Step 4: the level-0 model maps from the combined payload (frame kind as in
 // k_raycast: frame 1 copies the measured maps, a reset frame writes zeros).
@@ -3355,7 +3392,7 @@ namespace kfx {
 #endif
 void launch_raycast(hipStream_t s, VolView v, int levels, const LevelGeom *g, FrameView cur,
                     FrameView prev, const DevState *st, const DevPose *log, DevPose vpose,
-                    const float *xpose, uint32_t *keys, unsigned long long *stats) {
+                    const float *xpose, uint32_t *keys, unsigned long long *stats, const SlabPass &sp) {
   const bool want_stats = stats != nullptr;
 #ifdef KFX_RAY_TRACE
   if (!stats) {
@@ -3374,6 +3411,10 @@ void launch_raycast(hipStream_t s, VolView v, int levels, const LevelGeom *g, Fr
   RayArgs ra{};
   ra.levels = levels;
   ra.stats = stats;
+  ra.slab_pass = keys ? sp.pass : 0;
+  ra.kmin = sp.kmin;
+  ra.bound_abs = sp.bound_abs;
+  ra.bound_rel = sp.bound_rel;
   for (int l = 0; l < levels; ++l) ra.g[l] = g[l];
   dim3 grd(((g[0].w + 15) / 16) * ((g[0].h + 15) / 16));
   // 32-bit tsdf byte offsets (24-bit operands of the tile * zn products)

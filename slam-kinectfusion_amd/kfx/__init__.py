@@ -35,7 +35,7 @@ EXPORTS = [
     "kfx_stage_icp", "kfx_stage_integrate", "kfx_stage_raycast", "kfx_set_profiling", "kfx_get_stage_ms",
     "kfx_integrate_counts", "kfx_integrate_stats", "kfx_raycast_stats", "kfx_download_columns", "kfx_pipeline_async", "kfx_pipeline_async_u16", "kfx_register_host_buffer", "kfx_unregister_host_buffer", "kfx_slab_mask_payload", "kfx_slab_expand", "kfx_set_icp_allreduce", "kfx_create_slab", "kfx_create_slab_cuts", "kfx_slice_work", "kfx_slice_work_parts", "kfx_slab_balance", "kfx_slab_info", "kfx_comm_get_unique_id", "kfx_comm_init",
     "kfx_pipeline_group", "kfx_slab_frame_local", "kfx_slab_frame_finish", "kfx_render", "kfx_volume_checksum", "kfx_extract_points", "kfx_write_ply", "kfx_save_pointcloud",
-    "kfx_extract_mesh", "kfx_write_ply_mesh", "kfx_get_extract_ms", "kfx_set_extract_passes", "kfx_get_extract_passes",
+    "kfx_extract_mesh", "kfx_write_ply_mesh", "kfx_get_extract_ms", "kfx_set_extract_passes", "kfx_get_extract_passes", "kfx_set_slab_bound",
     "kfx_dataset_open", "kfx_dataset_info", "kfx_dataset_read", "kfx_dataset_close", "kfx_png_info",
     "kfx_png_read_bgr8", "kfx_png_read_depth", "kfx_parse_intr",
 ]
@@ -129,6 +129,7 @@ def lib():
         "kfx_extract_mesh": ([vp, P(f), C.c_int64, P(C.c_int64)], i),
         "kfx_get_extract_ms": ([vp, P(f)], i),
         "kfx_set_extract_passes": ([vp, i], i),
+        "kfx_set_slab_bound": ([vp, i], i),
         "kfx_get_extract_passes": ([vp, P(i)], i),
         "kfx_write_ply_mesh": ([C.c_char_p, P(f), C.c_int64], i),
         "kfx_dataset_open": ([C.c_char_p, P(vp)], i),
@@ -510,6 +511,11 @@ class KinectFusion:
         fn = lib().kfx_extract_mesh if mesh else lib().kfx_extract_points
         _check(fn(self._h, None, 0, C.byref(n)), "kfx_extract_mesh" if mesh else "kfx_extract_points")
         return n.value
+
+    def set_slab_bound(self, mode: int):
+        """Z-slab raycast bounded by the previous frame's model (1, default), off (0),
+        or bounded without margin (2, tests); results identical."""
+        _check(lib().kfx_set_slab_bound(self._h, int(mode)), "kfx_set_slab_bound")
 
     def set_extract_passes(self, passes: int):
         """1: single-pass extraction (default); 2: count + scan + emit passes."""

@@ -349,3 +349,28 @@ def test_balanced_cuts_group_matches_single_volume(seq_qvga):
     for m in members:
         m.close()
     single.close()
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_slab_bounded_raycast_modes_match_single_volume(mode, seq_qvga):
+    """The bounded slab raycast (kfx_set_slab_bound): each slab marches only up
+    to the previous frame's model distance (+ margin; mode 2: no margin, so
+    every pixel whose surface moved away takes the exact second pass), then
+    the pixels no slab resolved are re-marched.  The frame order jumps (frame
+    3 -> 7 -> 4) so that many pixels see surfaces farther than the frame
+    before.  Every mode gives the single volume's poses, maps and voxels."""
+    bgr, dep, _ = seq_qvga
+    order = [0, 1, 2, 3, 7, 4, 5, 6]
+    bgr, dep = bgr[order], dep[order]
+    intr = synth.Intrinsics.qvga()
+    p = default_params(dims=128, range_m=L_VOL)
+    single, st = _single(intr, p, bgr, dep)
+    members = [KinectFusion(Intrinsics.from_any(intr), p, slab=(r, 4)) for r in range(4)]
+    for m in members:
+        m.set_slab_bound(mode)
+    gst = [pipeline_group(members, bgr[k], dep[k].astype(np.float32)) for k in range(len(dep))]
+    assert gst == st
+    _compare(single, members)
+    for m in members:
+        m.close()
+    single.close()

@@ -46,7 +46,7 @@ def main():
     rec = {"config": a.config, "width": W, "height": H, "volume_dims": n, "volume_range_m": L, "world": a.world,
            "frames_timed": a.frames, "warmup": a.warmup, "lib_sha256": None,
            "method": "8 slab contexts on one GPU (kfx_pipeline_group); timed members run alone, one after "
-                     "another; HIP events on each member's stream; combine = in-process reductions + expand + "
+                     "another; HIP events on each member's stream; combine = shared in-process reductions, masks, resume passes + own expand + "
                      "pyramid (not RCCL)"}
     import hashlib
     rec["lib_sha256"] = hashlib.sha256(open(kfx.LIB_PATH, "rb").read()).hexdigest()
@@ -67,8 +67,10 @@ def main():
     sp = single.pose_record
     single.close()
 
-    def group(cuts):
+    def group(cuts, bound=1):
         members = [kfx.KinectFusion(I, p, slab=(r, a.world), cuts=cuts) for r in range(a.world)]
+        for m in members:
+            m.set_slab_bound(bound)
         for i in order[:a.warmup]:
             kfx.pipeline_group(members, bgr[i], dep[i])
         for m in members:
@@ -92,7 +94,12 @@ def main():
         up = np.array([s["integrate_updated"] for s in slabs], dtype=np.float64)
         # per-rank critical path of one frame at N GPUs (replicated ICP, RCCL not included)
         crit = [s["icp_ms"] + s["integrate_ms"] + s["raycast_local_ms"] for s in slabs]
-        return {"cuts": cuts, "slabs": slabs, "group_wall_ms_per_frame": 1e3 * t_group / a.frames,
+        crit_c = [c + s["combine_ms"] for c, s in zip(crit, slabs)]
+        rc = np.array([s["raycast_local_ms"] for s in slabs])
+        return {"cuts": cuts, "slab_bound": bound, "slabs": slabs,
+                "group_wall_ms_per_frame": 1e3 * t_group / a.frames,
+                "max_slab_over_single_raycast": float(rc.max() / rec["single"]["raycast_ms"]),
+                "max_rank_icp_integrate_raycast_combine_ms": float(max(crit_c)),
                 "integrate_imbalance_max_over_mean": float(it.max() / it.mean()),
                 "updated_imbalance_max_over_mean": float(up.max() / up.mean()),
                 "max_slab_over_single_integrate": float(it.max() / rec["single"]["integrate_ms"]),
@@ -111,6 +118,8 @@ def main():
     rec["slice_updated_first_frame"] = [int(x) for x in upd]
     rec["equal_cuts"] = group(None)
     rec["balanced_cuts"] = group(kfx.slab_balance(work, a.world))
+    # the same cuts with every slab ray marched to its end (no bound, no resume pass)
+    rec["balanced_cuts_unbounded"] = group(kfx.slab_balance(work, a.world), bound=0)
     # integrate ms of a slab against its stored slices' estimated parts:
     # ms ~ a * cover + b * updated + c (least squares over both cut sets)
     rows, ys = [], []
@@ -134,6 +143,9 @@ def main():
     print(json.dumps({"config": rec["config"], "ideal": rec["ideal"],
                       **{f"{k}:{q}": rec[k][q] for k in ("equal_cuts", "balanced_cuts")
                          for q in ("integrate_imbalance_max_over_mean", "max_slab_over_single_integrate")},
+                      **{f"{k}:{q}": rec[k][q] for k in ("balanced_cuts", "balanced_cuts_unbounded")
+                         for q in ("max_slab_over_single_raycast", "max_rank_icp_integrate_raycast_combine_ms")},
+                      "single_icp_integrate_raycast_ms": rec["single_icp_integrate_raycast_ms"],
                       "cost_fit": rec["cost_fit"]}))
 
 
