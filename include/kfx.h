@@ -394,8 +394,11 @@ int kfx_slab_balance(const int64_t *slice_work, int Z, int world, int *cuts);
  * it stopped, and after the all-reduce of [keys | stop points] re-marches the
  * pixels no slab resolved below that point (an exact second pass), so slabs
  * behind the visible surface skip the occluded space.  mode 0: off (every
- * ray marched to its end); 1: on (default); 2: on without the margin (test:
- * most pixels take the second pass).  Results are identical in every mode. */
+ * ray marched to its end; the default: on the benchmark scenes the slowest
+ * slab holds the surfaces most rays end on, so the bound did not lower it and
+ * the second pass cost more); 1: on; 2: on without the margin
+ * (test: most pixels take the second pass).  Results are identical in every
+ * mode. */
 int kfx_set_slab_bound(kfx_ctx *ctx, int mode);
 /* stored slices [zb, zb+zn), owned slices [own0, own1) */
 int kfx_slab_info(kfx_ctx *ctx, int *zb, int *zn, int *own0, int *own1);

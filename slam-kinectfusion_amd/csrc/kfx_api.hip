@@ -168,7 +168,7 @@ struct kfx_ctx {
   // march left unexamined, and the hit payload
   uint32_t *key_local = nullptr;
   uint32_t *key_min = nullptr;    // all-reduce MIN of the [key | pend] planes over the slabs
-  int slab_bound = 1;             // kfx_set_slab_bound: 0 off, 1 on, 2 on without margin (tests)
+  int slab_bound = 0;             // kfx_set_slab_bound: 0 off (default: measured no faster), 1 on, 2 no margin
   bool group_combine = false;     // kfx_pipeline_group member (in-process combine), this call only
   bool pass1_bounded = false;     // the frame's slab raycast was bounded: the combine runs pass 2
   // kfx_pipeline_async: host frames copied into a pinned ring slot, uploaded on

@@ -21,6 +21,9 @@
 #ifndef KFX_RAY_OCC
 #define KFX_RAY_OCC 5  // raycast: waves per SIMD the register budget must allow (4800 waves at VGA: one round at 5)
 #endif
+#ifndef KFX_RAY_SLAB_OCC
+#define KFX_RAY_SLAB_OCC 4  // slab and 64-bit-index raycasts: waves per SIMD (their extra registers spill at 5)
+#endif
 #ifndef KFX_RAY_KR
 #define KFX_RAY_KR 14  // raycast: samples per batch (loads in flight per lane)
 #endif
@@ -1877,7 +1880,7 @@ constexpr bool kTrace = true;
 constexpr bool kTrace = false;
 #endif
 template <bool kIdx32, bool kSlab, bool kStats = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KFX_RAY_OCC))) void k_raycast(VolView v, RayArgs ra, RayConsts rc,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((kSlab || !kIdx32) ? KFX_RAY_SLAB_OCC : KFX_RAY_OCC))) void k_raycast(VolView v, RayArgs ra, RayConsts rc,
                                                     FrameView cur, FrameView prev,
                                                     const DevState *__restrict__ st,
                                                     const DevPose *__restrict__ log, DevPose vpose,

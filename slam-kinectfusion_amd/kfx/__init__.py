@@ -513,7 +513,7 @@ class KinectFusion:
         return n.value
 
     def set_slab_bound(self, mode: int):
-        """Z-slab raycast bounded by the previous frame's model (1, default), off (0),
+        """Z-slab raycast bounded by the previous frame's model (1), off (0, default),
         or bounded without margin (2, tests); results identical."""
         _check(lib().kfx_set_slab_bound(self._h, int(mode)), "kfx_set_slab_bound")
 
