@@ -2100,7 +2100,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((kSlab || !
             if (kStats) st_blocked += 1;
             break;
           }
-          const int n = (int)fminf(lim, rc.skip_cap);
+          int n = (int)fminf(lim, rc.skip_cap);
+          if (kSlab) {
+            // a slab's ray ends 2 slices past its owned range (no owned
+            // sample follows, below): replay no further than about there
+            // (the far slabs' boxes run on to the volume's end otherwise)
+            const float zx = dv.z > 0.f ? ((float)(v.own1 + 3) - cz) * idv.z
+                                        : (dv.z < 0.f ? (cz - (float)(v.own0 - 4)) * idv.z : kInf);
+            n = min(n, max(1, (int)fminf(zx, rc.skip_cap)));
+          }
           if (kStats || kTrace) {
             st_lookups += 1;
             st_skipped += (unsigned)n;
@@ -2135,6 +2143,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((kSlab || !
           ray_len = pzr.y;
           nsk += (uint32_t)n;
           if (!live) break;
+          if (kSlab) {  // past the owned range (as after a batch): no owned sample follows
+            const float zf = nextp.z * rc.vs_inv.z;
+            if ((dir.z >= 0.f && zf > (float)(v.own1 + 2)) || (dir.z <= 0.f && zf < (float)(v.own0 - 3))) {
+              live = false;
+              break;
+            }
+          }
         }
         if (nsk != 0u && live) {
           kbase += nsk;
