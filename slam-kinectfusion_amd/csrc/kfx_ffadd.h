@@ -6,9 +6,10 @@
 // [2^E, 2^(E+1)), every float is an integer multiple X of u = 2^(E-23), so
 // while the exact sum x + s stays in the binade, RN(x + s) = (X + R) u with
 // R = the integer nearest to s / u: the sequence is an arithmetic progression
-// in integers, and m steps of it are (X + m R) u.  Steps that leave the
-// binade, ties (s / u a half-integer: the rounding then depends on X's last
-// bit), values near zero and extreme or non-finite values take plain float
+// in integers, and m steps of it are (X + m R) u.  Ties (s / u a
+// half-integer) round to even: after at most one plain step X is even and
+// every step adds the same even integer, again a progression.  Steps that leave the
+// binade, values near zero and extreme or non-finite values take plain float
 // adds.  Integer and float arithmetic only (a handful of registers: the loop
 // runs in integrate's prologue).  Checked against the plain loop on millions
 // of cases (tests/test_ffadd.py) and bit for bit inside the GPU parity tests.
@@ -40,6 +41,7 @@ KFX_HD inline float ff_pow2f(int e) {  // 2^e as a float, -126 <= e <= 127
 // n repeated x <- RN(x + s) (binary32, round to nearest even), exactly.
 KFX_HD inline float ff_add(float x, float s, int n) {
   const float as = s < 0.f ? -s : s;
+  if (n > 0 && as == 0.f) return x + s;  // adding zero: one add settles -0 and NaN
   while (n > 0) {
     const float ax = x < 0.f ? -x : x;
     // plain step: |x| within four steps of zero (tiny binades: one add each
@@ -56,9 +58,42 @@ KFX_HD inline float ff_add(float x, float s, int n) {
     const float rf = __builtin_rintf(su);
     const float f = su - rf;                                    // exact
     const int R = (int)rf;
+    if (f == 0.5f || f == -0.5f) {
+      // tie: 2 su = Q is odd, so X + Q/2 is a half-integer and rounds to the
+      // even one of X + lo, X + hi (lo = (Q-1)/2, hi = lo + 1).  From an even
+      // X every step adds the same c = the even one of lo, hi; an odd X takes
+      // one plain step first (its result is even).  Step k stays in the
+      // binade's rounding while X + k c + Q/2 lies in [2^23 + 1/2, 2^24 - 1/2]
+      // (a result of 2^24 u = 2^(E+1) is still exact).
+      const int Q = 2 * R + (f > 0.f ? 1 : -1), lo = (Q - 1) / 2, hi = lo + 1;
+      if ((X & 1) == 0) {
+        const int c = (lo & 1) == 0 ? lo : hi;
+        int m;
+        if (c > 0) {  // Q >= 3: the lower bound holds
+          const int num = 0x1000000 - X - hi;
+          m = num >= 0 ? num / c + 1 : 0;
+        } else if (c < 0) {  // Q <= -3: the upper bound holds
+          const int num = X + lo - 0x800000;
+          m = num >= 0 ? num / -c + 1 : 0;
+        } else {  // Q = +-1: X is a fixed point while its sum stays in range
+          if (X + lo >= 0x800000 && X + hi <= 0x1000000) return x;
+          m = 0;
+        }
+        if (m > 0) {
+          if (m > n) m = n;
+          const float xn = (float)(X + m * c) * ff_pow2f(E - 23);  // exact
+          x = x < 0.f ? -xn : xn;
+          n -= m;
+          continue;
+        }
+      }
+      x = x + s;
+      --n;
+      continue;
+    }
     // the sum X + R + f must stay in [2^23, 2^24): X + R in [lb, ub]
     const int lb = 0x800000 + (f < 0.f ? 1 : 0), ub = 0x1000000 - (f < 0.f ? 0 : 1);
-    if (f == 0.5f || f == -0.5f || X + R < lb || X + R > ub) {  // tie, or the step leaves the binade
+    if (X + R < lb || X + R > ub) {  // the step leaves the binade
       x = x + s;
       --n;
       continue;

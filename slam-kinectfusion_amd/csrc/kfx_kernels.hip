@@ -1999,12 +1999,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((kSlab || !
       else if (dcz < 0.f) nf = (czv - ((float)(v.zb + v.zn) + 0.5f)) / -dcz;
       if (nf >= 2.f) {
         const int n0 = (int)fminf(nf, 1.0e7f) - 1;
+        const float rl1 = ff_add(ray_len, rc.step, n0 - 1);
         // the reference tests ray_len < tfar before each of the n0 steps
-        if (!(ff_add(ray_len, rc.step, n0 - 1) < tfar)) {
+        if (!(rl1 < tfar)) {
           live = false;  // the march ends among the skipped samples: no event here
         } else {
           nextp = {ff_add(nextp.x, vstep.x, n0), ff_add(nextp.y, vstep.y, n0), ff_add(nextp.z, vstep.z, n0)};
-          ray_len = ff_add(ray_len, rc.step, n0);
+          ray_len = rl1 + rc.step;
           kbase += (uint32_t)n0;
           tprev = voxel2tsdf(v, rc, nextp);
           sprev = isnan(tprev) ? 0 : (tprev > 0.f ? 1 : (tprev < 0.f ? -1 : 0));

@@ -16,7 +16,7 @@ int main(int argc, char** argv) {
   long bad = 0;
   for (long it = 0; it < cases; ++it) {
     float x, s;
-    switch (it % 9) {
+    switch (it % 11) {
       case 0: x = U(g) * 3.f; s = U(g) * 0.01f; break;                  // camera-space columns
       case 1: x = U(g) * 0.01f; s = U(g) * 0.004f; break;               // crossing zero
       case 2: x = U(g) * 1000.f; s = U(g) * 1e-5f; break;               // fixed points
@@ -28,6 +28,16 @@ int main(int argc, char** argv) {
       case 5: x = U(g) * 1.2f; s = U(g) * 3e-4f; break;
       case 6: x = 1.0f + U(g) * 0.5f; s = 0.004f + U(g) * 1e-4f; break;
       case 7: x = std::ldexp(U(g), (int)(g() % 200) - 100); s = std::ldexp(U(g), (int)(g() % 200) - 100); break;
+      case 8: case 9: {                                                 // steps with trailing-zero mantissas: ties
+        x = U(g) * 4.f;
+        s = U(g) * 0.01f;
+        uint32_t b;
+        std::memcpy(&b, &s, 4);
+        b &= ~((1u << (g() % 21)) - 1u);
+        if (g() % 16 == 0) b &= 0x80000000u;                            // +-0 steps
+        std::memcpy(&s, &b, 4);
+        break;
+      }
       default: x = (g() & 1) ? INFINITY : NAN; s = U(g); break;          // non-finite
     }
     const int n = (int)(g() % 2100);
