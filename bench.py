@@ -89,8 +89,9 @@ def parse():
     ap.add_argument("--replicas", type=int, default=1,
                     help="slab mode at N>1: time independent replica streams first (the fallback line)")
     ap.add_argument("--zslab-timeout", type=float, default=300.0)
-    ap.add_argument("--cuts", choices=["balanced", "equal"], default="balanced",
-                    help="slab mode: Z-slab cuts balanced on the first frame's per-slice work, or equal slice ranges")
+    ap.add_argument("--cuts", choices=["balanced", "first", "equal"], default="balanced",
+                    help="slab mode: Z-slab cuts balanced on the mean per-slice work of 4 frames of the timed "
+                         "run at their poses, on the first frame's alone, or equal slice ranges")
     ap.add_argument("--extract", type=int, default=1,
                     help="N=1: time point extraction and marching cubes on the final volume (0 = skip)")
     ap.add_argument("--c3-frames", type=int, default=20,
@@ -295,12 +296,17 @@ def resolve(a, world):
     return name, W, H, n, L, mode
 
 
-def workload_text(name, W, H, n, L, mode, world, icp_ar):
+CUTS_TEXT = {"balanced": "cuts balanced on the mean per-slice integrate work of 4 frames of the run at their poses",
+             "first": "cuts balanced on the first frame's per-slice integrate work",
+             "equal": "equal slice ranges"}
+
+
+def workload_text(name, W, H, n, L, mode, world, icp_ar, cuts="balanced"):
     t = (f"{name.upper()}: synthetic {W}x{H} depth+BGR, {n}^3 TSDF @ {1000 * L / n:.1f} mm, "
          f"3-level ICP {{10,5,4}}, full pipeline per frame")
     if mode == "slab":
-        t += (f"; one stream, volume Z-slab sharded over {world} GPUs (cuts balanced on the first frame's "
-              f"per-slice integrate work), raycast combined per frame by RCCL "
+        t += (f"; one stream, volume Z-slab sharded over {world} GPUs ("
+              f"{CUTS_TEXT[cuts]}), raycast combined per frame by RCCL "
               f"(MIN keys + MAX {{Ts, normal}} payload), ICP " + ("sharded (27 int64 partials all-reduced per "
                                                                    "iteration)" if icp_ar else "replicated"))
     elif mode == "replicas":
@@ -313,10 +319,15 @@ def run_stream(a, intr, params, frames, D, local, slab=None, icp_ar=False, timin
     Returns the open context and the timed-region record; the caller closes it."""
     import kfx
     from kfx.abi import Intrinsics
-    bgr, dep, order = frames
+    bgr, dep, order, gt = frames
     cuts = None
-    if slab is not None and a.cuts == "balanced":
-        cuts = balanced_cuts(intr, params, bgr[order[0]], dep[order[0]], local, slab[1])
+    if slab is not None and a.cuts != "equal":
+        if a.cuts == "first":
+            calib = [order[0]]
+        else:  # 4 frames spread over the timed run's distinct frames
+            seen = sorted(set(order[a.warmup:a.warmup + a.steps]))
+            calib = [seen[int(round(j * (len(seen) - 1) / 3))] for j in range(4)]
+        cuts = balanced_cuts(intr, params, [(bgr[i], dep[i], gt[i]) for i in calib], local, slab[1])
     kf = kfx.KinectFusion(Intrinsics.from_any(intr), params, device=local, slab=slab, cuts=cuts)
     if slab is not None:
         kf.comm_init(D.bcast_bytes(kfx.comm_unique_id() if slab[0] == 0 else None))
@@ -343,15 +354,17 @@ def run_stream(a, intr, params, frames, D, local, slab=None, icp_ar=False, timin
     return kf, {"elapsed": elapsed, "ktime": ktime, "tracked": tracked}
 
 
-def balanced_cuts(intr, params, bgr0, dep0, local, world):
-    """Work-balanced Z-slab cuts from the first frame (kfx_slice_work on a
-    throw-away 16-slice slab context, kfx_slab_balance): every rank computes
-    the same cuts from the same frame."""
+def balanced_cuts(intr, params, calib, local, world):
+    """Work-balanced Z-slab cuts: the mean per-slice integrate work of the
+    calibration frames [(bgr, depth, camera pose)] (kfx_slice_work_at on a
+    throw-away 16-slice slab context), then kfx_slab_balance.  Every rank
+    computes the same cuts from the same frames.  The poses are the synthetic
+    trajectory's (a live system would use its tracked poses)."""
     import kfx
     from kfx.abi import Intrinsics
     Z = int(params.volu_dims[2])
     probe = kfx.KinectFusion(Intrinsics.from_any(intr), params, device=local, slab=(0, Z // 16))
-    work = probe.slice_work(bgr0, dep0)
+    work = np.mean([probe.slice_work_at(b, d, g)[0] for b, d, g in calib], axis=0).round().astype(np.int64)
     probe.close()
     return kfx.slab_balance(work, world)
 
@@ -447,10 +460,10 @@ def main():
     unique = a.unique if a.unique else (16 if W * H > 640 * 480 else 48)
     # one camera trajectory for every rank: the slab ranks share one stream, and
     # replica streams are independent whatever frames they replay
-    bgr, dep, _ = synth.sequence(unique, intr, L=L, noise=True, traj_seed=7, dropout=0.005)
+    bgr, dep, gt = synth.sequence(unique, intr, L=L, noise=True, traj_seed=7, dropout=0.005)
     dep = dep.astype(np.float32)
     order = synth.ping_pong(unique, a.warmup + a.steps + a.profile_frames)
-    frames = (bgr, dep, order)
+    frames = (bgr, dep, order, gt)
 
     # N>1: the replica streams first (no collective), so that a failing or hung
     # Z-slab stream still leaves a measured line
@@ -512,7 +525,7 @@ def main():
         zt.daemon = True
         zt.start()
         try:
-            out["zslab"] = zslab_record(a, intr, (bgr, dep, order), D, rank, world, local, icp_ar, (W, H, L))
+            out["zslab"] = zslab_record(a, intr, frames, D, rank, world, local, icp_ar, (W, H, L))
         except Exception as e:  # noqa: BLE001 -- recorded, the replica line stands
             out["zslab"] = {"error": f"{type(e).__name__}: {e}"[:300]}
         zt.cancel()
@@ -534,7 +547,7 @@ def main():
         i5 = intrinsics(W5, H5)
         u5 = 16
         bgr5, dep5, _ = synth.sequence(u5, i5, L=L5, noise=True, traj_seed=7, dropout=0.005)
-        f5 = (bgr5, dep5.astype(np.float32), synth.ping_pong(u5, b.warmup + b.steps))
+        f5 = (bgr5, dep5.astype(np.float32), synth.ping_pong(u5, b.warmup + b.steps), None)
         out["c5_record"] = single_record(b, "c5", i5, n5, L5, f5, D, local)
         del bgr5, dep5, f5
     emit(out)
@@ -573,8 +586,8 @@ def zslab_record(a, intr, frames, D, rank, world, local, icp_ar, geom):
     else:
         zintr = intrinsics(W, H)
         unique = 16 if W * H > 640 * 480 else 48
-        bgr, dep, _ = synth.sequence(unique, zintr, L=L, noise=True, traj_seed=7, dropout=0.005)
-        zframes = (bgr, dep.astype(np.float32), synth.ping_pong(unique, a.warmup + a.steps))
+        bgr, dep, gt = synth.sequence(unique, zintr, L=L, noise=True, traj_seed=7, dropout=0.005)
+        zframes = (bgr, dep.astype(np.float32), synth.ping_pong(unique, a.warmup + a.steps), gt)
     kf, r = run_stream(a, zintr, params, zframes, D, local, slab=(rank, world), icp_ar=icp_ar)
     kt = r["ktime"] or {}
     work = kf.integrate_stats()
@@ -586,7 +599,7 @@ def zslab_record(a, intr, frames, D, rank, world, local, icp_ar, geom):
     per_rank = [{"rank": k, "icp_ms": round(x[0], 4), "integrate_ms": round(x[1], 4), "raycast_ms": round(x[2], 4),
                  "combine_ms": round(x[3], 4), "integrate_updated": int(x[4]), "owned_slices": int(x[5]),
                  "stored_slices": int(x[6])} for k, x in enumerate(rows)]
-    return {"workload": workload_text(a.zslab, W, H, n, L, "slab", world, icp_ar),
+    return {"workload": workload_text(a.zslab, W, H, n, L, "slab", world, icp_ar, a.cuts),
             "value": round(a.steps / r["elapsed"], 3), "unit": "frames/s", "scaling": "strong",
             "ms_per_step": round(1000.0 * r["elapsed"] / a.steps, 4), "steps": a.steps, "warmup": a.warmup,
             "tracked_frames": int(r["tracked"]), "per_rank": per_rank,
@@ -739,7 +752,7 @@ def measure_main(a, name, intr, params, frames, D, rank, world, local, mode, icp
     frames_done = a.steps * (world if mode == "replicas" else 1)
     value = frames_done / elapsed
     out = base_line(a, world, value, 1000.0 * elapsed / a.steps, "strong" if mode == "slab" else "weak", {
-        "workload": workload_text(name, W, H, n, L, mode, world, icp_ar),
+        "workload": workload_text(name, W, H, n, L, mode, world, icp_ar, a.cuts),
         "width": W, "height": H, "volume_dims": n, "volume_range_m": L,
         "frames_unique": len(bgr),
         # what the timed frames replay as graphs (kfx_set_graph_mode); the few

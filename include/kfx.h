@@ -369,8 +369,8 @@ int kfx_create_slab(const kfx_intrinsics *intr, const kfx_params *params, int de
  * cuts[world] = Z, multiples of 8, >= 8 slices each; every rank passes the
  * same cuts).  kfx_slice_work gives, per global slice, an estimate of a
  * frame's integrate cost at the first frame's pose (any context, slab or not;
- * from the frame's filtered depth: voxel slots visited, updated voxels
- * weighted more); kfx_slab_balance turns such a
+ * from the frame's filtered depth: voxel slots visited plus 1/40 of the
+ * slice's X*Y stored slots); kfx_slab_balance turns such a
  * histogram into cuts minimising the largest slab's stored-range work (halos
  * included).  Results stay bit-identical to the single volume for any cuts.
  * Side effect: kfx_slice_work(_parts) preprocesses the given frame into the
@@ -382,11 +382,18 @@ int kfx_create_slab(const kfx_intrinsics *intr, const kfx_params *params, int de
 int kfx_create_slab_cuts(const kfx_intrinsics *intr, const kfx_params *params, int device,
                          int rank, int world, const int *cuts, kfx_ctx **out);
 int kfx_slice_work(kfx_ctx *ctx, const uint8_t *bgr, const float *depth_mm, int64_t *work);
-/* The two parts kfx_slice_work weighs, per global slice: cover = the voxel
+/* The two parts kfx_slice_work measures, per global slice (it weighs cover): cover = the voxel
  * slots integrate's waves step through (64 per column tile whose z interval
  * holds the slice), updated = the voxels whose depth test passes. */
 int kfx_slice_work_parts(kfx_ctx *ctx, const uint8_t *bgr, const float *depth_mm, int64_t *cover,
                          int64_t *updated);
+/* kfx_slice_work of a frame seen from cam_pose (camera-to-world, as in the
+ * pose record; null = the identity pose of a first frame), with its parts
+ * (cover / updated may be null).  Averaging several frames of a sequence at
+ * their poses gives cuts for the whole run rather than its first frame
+ * (bench.py --cuts balanced). */
+int kfx_slice_work_at(kfx_ctx *ctx, const uint8_t *bgr, const float *depth_mm, const kfx_pose *cam_pose,
+                      int64_t *work, int64_t *cover, int64_t *updated);
 int kfx_slab_balance(const int64_t *slice_work, int Z, int world, int *cuts);
 /* Bounded slab raycast: a slab that combines with others over
  * a communicator or in a kfx_pipeline_group marches each ray only up to the

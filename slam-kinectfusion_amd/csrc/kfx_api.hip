@@ -219,7 +219,10 @@ int dalloc(kfx_ctx *c, void **p, size_t bytes) {
 #define KFX_PREP_AFTER_ICP 1  // overlapped frames: next preprocess waits for this frame's ICP
 #endif
 #ifndef KFX_UPDATED_COST
-#define KFX_UPDATED_COST 2  // slab balancing: cost of an updated voxel over a visited slot (slice_cost)
+#define KFX_UPDATED_COST 0  // slab balancing: cost of an updated voxel over a visited slot (slice_cost)
+#endif
+#ifndef KFX_SLOT_DIV
+#define KFX_SLOT_DIV 40  // slab balancing: a stored voxel slot costs 1/KFX_SLOT_DIV visited slot (0: none)
 #endif
 #ifndef KFX_VOL_PAD
 #define KFX_VOL_PAD 4096  // weight offset past the 2 MiB-rounded tsdf (bytes)
@@ -874,10 +877,16 @@ int kfx_create_slab_cuts(const kfx_intrinsics *intr, const kfx_params *params, i
 
 // Integrate cost of one slice from kfx_slice_work_parts, in voxel-slot units:
 // every slot a wave steps through, plus kUpdatedCost more per updated voxel
-// (its tsdf / weight / colour read-modify-write).  Fitted to per-slab
-// integrate times (tools/slab_record.py).
+// (its tsdf / weight / colour read-modify-write), plus the slice's X*Y stored
+// slots / kSlotDiv (the waves of column tiles outside the frustum still start
+// and test their range).  Fitted to per-slab integrate times of C4 and C5
+// (tools/slab_record.py): an updated voxel costs no more than a
+// visited one, a stored slot 1/40 of one.
 constexpr int64_t kUpdatedCost = KFX_UPDATED_COST;
-static int64_t slice_cost(int64_t cover, int64_t updated) { return cover + kUpdatedCost * updated; }
+constexpr int64_t kSlotDiv = KFX_SLOT_DIV;
+static int64_t slice_cost(int64_t cover, int64_t updated, int64_t slots) {
+  return cover + kUpdatedCost * updated + (kSlotDiv > 0 ? slots / kSlotDiv : 0);
+}
 
 int kfx_slab_balance(const int64_t *slice_work, int Z, int world, int *cuts) {
   if (!slice_work || !cuts || world < 1 || Z < 8 * world) return set_err(KFX_ERR_ARG, "bad argument");
@@ -2211,10 +2220,27 @@ int kfx_save_pointcloud(kfx_ctx *c, const char *path, int64_t cap) {
 
 // ---- Z-slab sharding -------------------------------------------------------
 
-int kfx_slice_work_parts(kfx_ctx *c, const uint8_t *bgr, const float *depth_mm, int64_t *cover, int64_t *updated) {
+// slice work of a frame with the camera at cam (camera-to-world; null: the
+// first frame's identity pose)
+static int slice_work_parts(kfx_ctx *c, const uint8_t *bgr, const float *depth_mm, const kfx_pose *cam,
+                            int64_t *cover, int64_t *updated) {
   int r = check_ctx(c);
   if (r) return r;
   if (!bgr || !depth_mm || !cover || !updated) return set_err(KFX_ERR_ARG, "null argument");
+  DevPose vol2cam = to_dev(c->p.volu_pose);  // identity camera: vol2cam = volume pose
+  if (cam) {  // inverse(cam) o volume pose, in double
+    const kfx_pose &v = c->p.volu_pose;
+    for (int i = 0; i < 3; ++i) {
+      double t = 0.0;
+      for (int k = 0; k < 3; ++k) t += (double)cam->R[3 * k + i] * ((double)v.t[k] - cam->t[k]);
+      vol2cam.t[i] = (float)t;
+      for (int j = 0; j < 3; ++j) {
+        double a = 0.0;
+        for (int k = 0; k < 3; ++k) a += (double)cam->R[3 * k + i] * v.R[3 * k + j];
+        vol2cam.R[3 * i + j] = (float)a;
+      }
+    }
+  }
   HIPCHK(hipStreamSynchronize(c->pstream));
   HIPCHK(hipStreamSynchronize(c->stream));
   set_par(c, 0);
@@ -2228,8 +2254,7 @@ int kfx_slice_work_parts(kfx_ctx *c, const uint8_t *bgr, const float *depth_mm, 
   HIPCHK(hipMalloc(&hist, sizeof(unsigned long long) * n));
   hipError_t e = hipMemsetAsync(hist, 0, sizeof(unsigned long long) * n, c->stream);
   if (e == hipSuccess) {
-    // the first frame integrates at the identity camera pose: vol2cam = volume pose
-    launch_slice_work(c->stream, c->vol, to_dev(c->p.volu_pose), c->g[0], c->dl0, hist);
+    launch_slice_work(c->stream, c->vol, vol2cam, c->g[0], c->dl0, hist);
     e = hipGetLastError();
   }
   std::vector<unsigned long long> h(n);
@@ -2246,13 +2271,27 @@ int kfx_slice_work_parts(kfx_ctx *c, const uint8_t *bgr, const float *depth_mm, 
   return KFX_OK;
 }
 
-int kfx_slice_work(kfx_ctx *c, const uint8_t *bgr, const float *depth_mm, int64_t *work) {
+int kfx_slice_work_parts(kfx_ctx *c, const uint8_t *bgr, const float *depth_mm, int64_t *cover, int64_t *updated) {
+  return slice_work_parts(c, bgr, depth_mm, nullptr, cover, updated);
+}
+
+int kfx_slice_work_at(kfx_ctx *c, const uint8_t *bgr, const float *depth_mm, const kfx_pose *cam_pose,
+                      int64_t *work, int64_t *cover, int64_t *updated) {
   if (!c || !work) return set_err(KFX_ERR_ARG, "null argument");
-  std::vector<int64_t> cover(c->vol.Z), upd(c->vol.Z);
-  const int r = kfx_slice_work_parts(c, bgr, depth_mm, cover.data(), upd.data());
+  std::vector<int64_t> cv(c->vol.Z), up(c->vol.Z);
+  const int r = slice_work_parts(c, bgr, depth_mm, cam_pose, cv.data(), up.data());
   if (r) return r;
-  for (int z = 0; z < c->vol.Z; ++z) work[z] = slice_cost(cover[z], upd[z]);
+  const int64_t slots = (int64_t)c->vol.X * c->vol.Y;
+  for (int z = 0; z < c->vol.Z; ++z) {
+    work[z] = slice_cost(cv[z], up[z], slots);
+    if (cover) cover[z] = cv[z];
+    if (updated) updated[z] = up[z];
+  }
   return KFX_OK;
+}
+
+int kfx_slice_work(kfx_ctx *c, const uint8_t *bgr, const float *depth_mm, int64_t *work) {
+  return kfx_slice_work_at(c, bgr, depth_mm, nullptr, work, nullptr, nullptr);
 }
 
 int kfx_slab_info(kfx_ctx *c, int *zb, int *zn, int *own0, int *own1) {

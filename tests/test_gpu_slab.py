@@ -331,12 +331,12 @@ def test_balanced_cuts_group_matches_single_volume(seq_qvga):
     # the parts: updated voxels as integrate counts them (the estimate's vc is
     # direct, not accumulated: 1 %), wave slots as its batches of 4 slices
     # (each of a tile's <= 8 z-chunks rounds up to a whole batch); the cost
-    # weighs both
+    # weighs the visited slots and the slice's stored slots
     upd, slots, tiles = ws["updated"], ws["wave_batches"] * 4 * 64, (64 // 8) ** 2
-    assert work[0] == 0 and cover[0] == 0 and np.all(cover >= updated)
+    assert cover[0] == 0 and np.all(cover >= updated)
     assert abs(int(updated.sum()) - upd) <= 0.01 * upd, (int(updated.sum()), upd)
     assert cover.sum() <= slots <= cover.sum() + 8 * tiles * 4 * 64, (int(cover.sum()), slots)
-    assert np.array_equal(work, cover + 2 * updated)
+    assert np.array_equal(work, cover + (64 * 64) // 40)  # cover + the slice's slots / 40 (slice_cost)
     world = 3
     cuts = slab_balance(work, world)
     assert cuts[0] == 0 and cuts[-1] == 64 and all(b - a >= 8 for a, b in zip(cuts, cuts[1:]))
@@ -374,3 +374,31 @@ def test_slab_bounded_raycast_modes_match_single_volume(mode, seq_qvga):
     for m in members:
         m.close()
     single.close()
+
+
+@pytest.mark.gpu
+def test_slice_work_at_pose(seq_qvga):
+    """kfx_slice_work_at: with no pose it is kfx_slice_work; at a later
+    frame's pose its updated count matches that frame's integrate at the same
+    pose (kfx_stage_integrate, counted on the device) within the estimate's
+    1 % (its vc is direct, not accumulated)."""
+    from kfx.abi import Pose
+    bgr, dep, gt = seq_qvga
+    I = Intrinsics.from_any(synth.Intrinsics.qvga())
+    p = default_params(dims=64, range_m=L_VOL)
+    kf = KinectFusion(I, p)
+    d0 = dep[0].astype(np.float32)
+    work0 = kf.slice_work(bgr[0], d0)
+    w, c, u = kf.slice_work_at(bgr[0], d0)
+    assert np.array_equal(w, work0) and np.all(c >= u)
+    wi, ci, ui = kf.slice_work_at(bgr[0], d0, np.eye(4))
+    assert np.array_equal(wi, w) and np.array_equal(ci, c) and np.array_equal(ui, u)
+    k = 5
+    dk = dep[k].astype(np.float32)
+    _, ck, uk = kf.slice_work_at(bgr[k], dk, gt[k])
+    kf.stage_preprocess(bgr[k], dk)
+    vol2cam = O.pose_mul(O.pose_inv(Pose.from_matrix(gt[k])), p.volu_pose)
+    nu, _ = kf.stage_integrate(vol2cam)
+    assert abs(int(uk.sum()) - nu) <= 0.01 * nu, (int(uk.sum()), nu)
+    assert not np.array_equal(uk, u)
+    kf.close()

@@ -39,7 +39,7 @@ def main():
     intr = intrinsics(W, H)
     p = default_params(dims=n, range_m=L)
     unique = 16
-    bgr, dep, _ = synth.sequence(unique, intr, L=L, noise=True, traj_seed=7, dropout=0.005)
+    bgr, dep, gt = synth.sequence(unique, intr, L=L, noise=True, traj_seed=7, dropout=0.005)
     dep = dep.astype(np.float32)
     order = synth.ping_pong(unique, a.warmup + a.frames)
     I = Intrinsics.from_any(intr)
@@ -112,14 +112,22 @@ def main():
     probe = kfx.KinectFusion(I, p, slab=(0, n // 16))
     work = probe.slice_work(bgr[order[0]], dep[order[0]])
     cover, upd = probe.slice_work_parts(bgr[order[0]], dep[order[0]])
+    # the same estimate averaged over 4 frames of the timed run at their
+    # ground-truth poses (bench.py --cuts balanced: cuts for the run)
+    seen = sorted(set(order[a.warmup:a.warmup + a.frames]))
+    calib = [seen[int(round(j * (len(seen) - 1) / 3))] for j in range(4)]
+    cw = np.mean([probe.slice_work_at(bgr[i], dep[i], gt[i])[0] for i in calib], axis=0).round().astype(np.int64)
     probe.close()
+    rec["calibration_frames"] = [int(i) for i in calib]
     rec["slice_work_first_frame"] = [int(x) for x in work]
+    rec["slice_work_calibrated"] = [int(x) for x in cw]
     rec["slice_cover_first_frame"] = [int(x) for x in cover]
     rec["slice_updated_first_frame"] = [int(x) for x in upd]
     rec["equal_cuts"] = group(None)
     rec["balanced_cuts"] = group(kfx.slab_balance(work, a.world))
     # the same cuts with every slab ray marched to its end (no bound, no resume pass)
     rec["balanced_cuts_unbounded"] = group(kfx.slab_balance(work, a.world), bound=0)
+    rec["calibrated_cuts_unbounded"] = group(kfx.slab_balance(cw, a.world), bound=0)
     # integrate ms of a slab against its stored slices' estimated parts:
     # ms ~ a * cover + b * updated + c (least squares over both cut sets)
     rows, ys = [], []
@@ -143,7 +151,8 @@ def main():
     print(json.dumps({"config": rec["config"], "ideal": rec["ideal"],
                       **{f"{k}:{q}": rec[k][q] for k in ("equal_cuts", "balanced_cuts")
                          for q in ("integrate_imbalance_max_over_mean", "max_slab_over_single_integrate")},
-                      **{f"{k}:{q}": rec[k][q] for k in ("balanced_cuts", "balanced_cuts_unbounded")
+                      **{f"{k}:{q}": rec[k][q] for k in ("balanced_cuts", "balanced_cuts_unbounded",
+                                                          "calibrated_cuts_unbounded")
                          for q in ("max_slab_over_single_raycast", "max_rank_icp_integrate_raycast_combine_ms")},
                       "single_icp_integrate_raycast_ms": rec["single_icp_integrate_raycast_ms"],
                       "cost_fit": rec["cost_fit"]}))
