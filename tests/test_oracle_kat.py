@@ -192,6 +192,43 @@ def test_icp_block_solve_matches_numpy(oracle_lib):
         assert np.abs(x - xe).max() <= 1e-9 * np.abs(xe).max(), trial
 
 
+def test_icp_det_threshold_matches_lu(oracle_lib):
+    """The tracking-failure test |det A| < 1e-15 (icp_registration.cpp:35-37,
+    cv::determinant) on the block solve's det P * det S decides as the LU
+    determinant of the same fixed-point A does, for positive semidefinite
+    systems (A = JᵀJ) whose determinant spans 1e-18 .. 1e-12 and for rank-
+    deficient ones; only determinants within 1e-6 of the threshold are not
+    compared (the two products round differently there).  For PSD A a singular
+    rotation block P implies a singular A, so the block form never divides by
+    a zero det P of a trackable system."""
+    rng = np.random.default_rng(5)
+    iu = [(i, j) for i in range(6) for j in range(i, 7)]
+    decided = fails = 0
+    for trial in range(400):
+        Qm, _ = np.linalg.qr(rng.normal(size=(6, 6)))
+        lam = np.exp(rng.normal(size=6) * 1.5)
+        if trial % 8 == 0:
+            lam[rng.integers(6)] = 0.0  # rank-deficient: det 0
+        else:
+            lam *= (10.0 ** rng.uniform(-18, -12) / np.prod(lam)) ** (1 / 6)
+        A = (Qm * lam) @ Qm.T
+        b = rng.normal(size=6) * 1e-3
+        Ab = np.concatenate([A, b[:, None]], 1)
+        sums = np.array([round(Ab[i, j] * 2.0 ** 32) for i, j in iu], np.int64)
+        Aq = np.zeros((6, 6))
+        for k, (i, j) in enumerate(iu):
+            if j < 6:
+                Aq[i, j] = Aq[j, i] = sums[k] / 2.0 ** 32
+        d = np.linalg.det(Aq)
+        st, _, _ = oracle_lib.icp_update(sums, Pose.identity())
+        if abs(abs(d) / 1e-15 - 1) < 1e-6:
+            continue
+        decided += 1
+        fails += st
+        assert st == int(abs(d) < 1e-15 or np.isnan(d)), (trial, d)
+    assert decided >= 390 and 0 < fails < decided
+
+
 def test_icp_singular_fails(oracle_lib):
     st, _, _ = oracle_lib.icp_update(np.zeros(27, np.int64), Pose.identity())
     assert st == 1  # det < 1e-15 -> tracking fail (icp_registration.cpp:35-37)
