@@ -263,16 +263,17 @@ CONFIGS = {  # BASELINE.json configs[1..4]: (width, height, volume dims, volume 
 }
 
 
-def graph_parts(a, mode):
-    """The part of each timed frame replayed as a captured graph."""
-    if a.no_graph:
+def graph_parts(a, mode, effective=None):
+    """The part of each timed frame replayed as a captured graph (effective:
+    kfx_get_graph_mode after the run, lowered where RCCL refused capture)."""
+    if a.no_graph or effective == 0:
         return "none (eager)"
     if a.no_overlap:
         return "whole frame (single stream)"
-    if mode == "slab":
-        return "none (overlapped slab frames launch eagerly)"
-    return ("pyrDown+preprocess graph and ICP+integrate+raycast graph" if a.graph_full else
-            "pyrDown+preprocess graph; ICP, integrate, raycast eager")
+    main = "ICP+integrate+raycast" + ("+RCCL combine" if mode == "slab" else "")
+    if a.graph_full and effective in (None, 2):
+        return f"pyrDown+preprocess graph and {main} graph"
+    return f"pyrDown+preprocess graph; {main} eager" + (" (RCCL refused capture)" if a.graph_full else "")
 
 
 def resolve(a, world):
@@ -351,7 +352,7 @@ def run_stream(a, intr, params, frames, D, local, slab=None, icp_ar=False, timin
         raise SystemExit(f"bench: {a.steps - tracked} of {a.steps} timed frames were not tracked")
     if ktime is not None and not ktime["samples"]:
         ktime = None
-    return kf, {"elapsed": elapsed, "ktime": ktime, "tracked": tracked}
+    return kf, {"elapsed": elapsed, "ktime": ktime, "tracked": tracked, "graph_mode": kf.graph_mode()}
 
 
 def balanced_cuts(intr, params, calib, local, world):
@@ -600,6 +601,7 @@ def zslab_record(a, intr, frames, D, rank, world, local, icp_ar, geom):
                  "combine_ms": round(x[3], 4), "integrate_updated": int(x[4]), "owned_slices": int(x[5]),
                  "stored_slices": int(x[6])} for k, x in enumerate(rows)]
     return {"workload": workload_text(a.zslab, W, H, n, L, "slab", world, icp_ar, a.cuts),
+            "graph": graph_parts(a, "slab", r["graph_mode"]),
             "value": round(a.steps / r["elapsed"], 3), "unit": "frames/s", "scaling": "strong",
             "ms_per_step": round(1000.0 * r["elapsed"] / a.steps, 4), "steps": a.steps, "warmup": a.warmup,
             "tracked_frames": int(r["tracked"]), "per_rank": per_rank,
@@ -620,12 +622,12 @@ def measure_main(a, name, intr, params, frames, D, rank, world, local, mode, icp
     import kfx
     from kfx import synth
     from kfx.abi import default_params
-    bgr, dep, order = frames
+    bgr, dep, order, _ = frames
     W, H = intr.width, intr.height
     n, L = params.volu_dims[0], params.volu_range[0]
     slab = (rank, world) if mode == "slab" else None
     kf, r = run_stream(a, intr, params, frames, D, local, slab=slab, icp_ar=icp_ar)
-    elapsed, ktime, tracked = r["elapsed"], r["ktime"], r["tracked"]
+    elapsed, ktime, tracked, gmode = r["elapsed"], r["ktime"], r["tracked"], r["graph_mode"]
     ms_source = (f"timed region, {ktime['samples']} HIP-event-bracketed frames" if ktime else "profiled frames")
 
     # per-stage device ms on further frames (profiled, eager; single volume)
@@ -757,7 +759,7 @@ def measure_main(a, name, intr, params, frames, D, rank, world, local, mode, icp
         "frames_unique": len(bgr),
         # what the timed frames replay as graphs (kfx_set_graph_mode); the few
         # stage-timing sample frames launch eagerly with their events
-        "graph": graph_parts(a, mode), "overlap": not a.no_overlap,
+        "graph": graph_parts(a, mode, gmode), "overlap": not a.no_overlap,
         "parallelism": (f"zslab x{world}" + (" + icp allreduce" if icp_ar else "") if mode == "slab" else
                         (f"replicas x{world} (independent streams)" if world > 1 else "single")),
         "collective": ("RCCL: raycast combine per frame" + (" + ICP partials per iteration" if icp_ar else "")

@@ -132,9 +132,16 @@ int kfx_unregister_host_buffer(kfx_ctx *ctx, void *ptr);
  * staged / async frames replay their pyrDown + preprocess as a graph and
  * launch ICP, integrate and raycast eagerly; 2 as 1, and overlapped frames
  * also replay ICP + integrate + raycast as a second graph (measured slower,
- * DESIGN.md §3).  Z-slab and group frames always launch eagerly when
- * overlapped.  Results are identical in every mode. */
+ * DESIGN.md §3).  Z-slab contexts capture the same graphs, their RCCL
+ * collectives (slab combine, sharded-ICP all-reduces) as graph nodes; if RCCL
+ * refuses stream capture those frames launch eagerly instead.  Frames of an
+ * in-process group (kfx_pipeline_group) launch eagerly when overlapped.
+ * Results are identical in every mode. */
 int kfx_set_graph_mode(kfx_ctx *ctx, int enabled);
+/* The mode in effect: as set, lowered where a capture was refused (RCCL
+ * refusing capture: 2 -> 1 for overlapped frames, 1 -> 0 for single-stream
+ * frames of a communicator context). */
+int kfx_get_graph_mode(kfx_ctx *ctx, int *mode);
 /* Overlap each staged frame's preprocess with the previous frame's tracking on
  * a second stream, over double-buffered frame maps (default on; staged frames
  * then launch eagerly instead of through graphs).  Results are identical. */

@@ -151,6 +151,7 @@ struct kfx_ctx {
   std::vector<hipGraphExec_t> ov_graph;
   bool ov_graph_full = false;  // also capture ICP/integrate/raycast (kfx_set_graph_mode 2)
   bool cap_ext = false;        // capturing: the ev_icp record becomes an event-record node
+  bool ov_main_refused = false;  // the main graph's capture failed (RCCL refused capture): eager
   const uint8_t *last_bgr = nullptr;              // colour the last frame integrated
   hipEvent_t ev[kStageEvents]{};  // stage events; [5]: local raycast done, [6]: combine starts (slabs)
   float stage_ms[5]{};
@@ -549,11 +550,9 @@ int capture_graph(kfx_ctx *c, hipStream_t s, F &&body, hipGraphExec_t *out) {
   return KFX_OK;
 }
 
-// Overlapped frames replay graphs when they run on one device without slab
-// exchange or group chaining (those keep their eager launches).
-bool ov_graphs_apply(const kfx_ctx *c) {
-  return c->graph_mode && !c->slab && !c->comm && !c->group_chain && !c->icp_sharded;
-}
+// Overlapped frames replay graphs unless they run chained in an in-process
+// group (kfx_pipeline_group: cross-context event waits between the members).
+bool ov_graphs_apply(const kfx_ctx *c) { return c->graph_mode && !c->group_chain; }
 
 // The graphs of an overlapped frame for buffer set p: gx[0] pyrDown +
 // preprocess (replayed on pstream) and, with kfx_set_graph_mode(ctx, 2),
@@ -563,16 +562,27 @@ bool ov_graphs_apply(const kfx_ctx *c) {
 // frame slower than the eager launches of the same three kernels (the graph
 // uploaded beforehand), while the preprocess graph is neutral to slightly
 // faster.
+// Z-slab contexts capture the same graphs: the preprocess graph is local, and
+// the main graph holds the slab combine (and the sharded ICP's all-reduces) as
+// RCCL nodes when RCCL accepts stream capture; if it refuses, the main part of
+// every later frame launches eagerly (kfx_get_graph_mode reports 1).
 int ensure_ov_graphs(kfx_ctx *c, FrameInput in, hipGraphExec_t *gx, int p) {
-  if (gx[0] && (gx[1] || !c->ov_graph_full)) return KFX_OK;
+  const bool main = c->ov_graph_full && !c->ov_main_refused;
+  if (gx[0] && (gx[1] || !main)) return KFX_OK;
   const int keep = c->par;
   set_par(c, p);
   int r = gx[0] ? KFX_OK
                 : capture_graph(c, c->pstream, [&] { enqueue_prep_overlap(c, in); return KFX_OK; }, &gx[0]);
-  if (!r && !gx[1] && c->ov_graph_full) {
+  if (!r && !gx[1] && main) {
     c->cap_ext = true;
     r = capture_graph(c, c->stream, [&] { return enqueue_main_overlap(c, in, nullptr); }, &gx[1]);
     c->cap_ext = false;
+    if (r && (c->comm || c->icp_sharded)) {
+      (void)hipGetLastError();
+      gx[1] = nullptr;
+      c->ov_main_refused = true;
+      r = KFX_OK;
+    }
   }
   set_par(c, keep);
   return r;
@@ -1354,7 +1364,14 @@ int kfx_set_graph_mode(kfx_ctx *c, int enabled) {
     HIPCHK(hipStreamSynchronize(c->pstream));
     destroy_graphs(c);
     c->ov_graph_full = enabled == 2;
+    c->ov_main_refused = false;
   }
+  return KFX_OK;
+}
+
+int kfx_get_graph_mode(kfx_ctx *c, int *mode) {
+  if (!c || !mode) return set_err(KFX_ERR_ARG, "null argument");
+  *mode = !c->graph_mode ? 0 : (c->ov_graph_full && !c->ov_main_refused ? 2 : 1);
   return KFX_OK;
 }
 

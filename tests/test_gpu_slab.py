@@ -135,11 +135,12 @@ def test_slab_group_tracking_failure(seq_qvga):
         m.close()
 
 
-@pytest.mark.parametrize("graph,icp_ar", [(True, False), (False, False), (True, True)])
+@pytest.mark.parametrize("graph,icp_ar", [(1, False), (0, False), (1, True), (2, False), (2, True)])
 def test_slab_rccl_single_rank_matches(graph, icp_ar, seq_qvga):
     """A one-rank RCCL communicator: the collectives of the slab combine run
     (captured into the per-frame graph when RCCL allows it); with icp_ar the
-    19 per-iteration all-reduces of the sharded ICP as well."""
+    19 per-iteration all-reduces of the sharded ICP as well.  Mode 2: the
+    overlapped staged frames capture ICP + integrate + raycast + combine too."""
     bgr, dep, _ = seq_qvga
     intr = synth.Intrinsics.qvga()
     p = default_params(dims=64, range_m=L_VOL)
@@ -162,6 +163,8 @@ def test_slab_rccl_single_rank_matches(graph, icp_ar, seq_qvga):
     m.synchronize()
     single.synchronize()
     _compare(single, [m])
+    print("graph mode set", graph, "in effect", m.graph_mode())
+    assert 0 <= m.graph_mode() <= graph
     km, ks = m.kernel_timing(), single.kernel_timing()
     assert km["samples"] == ks["samples"] == (len(dep) + 1) // 2
     for k in ("icp", "integrate", "raycast_local", "combine"):
