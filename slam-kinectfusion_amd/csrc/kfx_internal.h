@@ -58,9 +58,12 @@ struct IcpPlan {
   int ppl[kMaxLevels];  // pixels per lane at each level
   const float *cv[kMaxLevels], *cn[kMaxLevels], *pv[kMaxLevels], *pn[kMaxLevels];
   float dist2_max, sine2_max;  // sqrt_le_bound of the distance / sine thresholds
-  // 1: nblocks (co-resident) is below some level's groups; block b also takes
-  // groups b + k * nblocks (k_icp_track<true>), at most kIcpStrideMax per block
+  // 1: nblocks (co-resident) is below some level's groups (k_icp_track<true>):
+  // at such a level block b takes the contiguous pixels [b span, (b+1) span)
+  // in passes of up to kIcpPix per lane (span[l] > 0, a multiple of the block
+  // size; groups[l] is then the number of non-empty ranges)
   int stride;
+  int span[kMaxLevels];
 };
 constexpr int kIcpStrideMax = 16;
 

@@ -821,11 +821,12 @@ __global__ __launch_bounds__(kIcpThreads) void k_icp_acc(LevelGeom g, int xe, in
 // derives the begun state itself and block 0's thread 0, the only writer of
 // these fields during the kernel, stores it first
 // kStride: a level may have more pixel groups than the grid has blocks
-// (IcpPlan::stride, 1280x720 level 0); block b then also takes groups b +
-// gridDim, b + 2 gridDim, ... whose current-frame pixels it re-reads every
-// iteration.  Their products join the lane sums before the block reduce: the
-// sums stay integers below 2^53 (<= 16 groups per block, IcpPlan docs), so the
-// fp64 adds remain exact and the int64 totals are the oracle's.
+// (IcpPlan::stride, 1280x720 level 0); block b then takes an equal contiguous
+// range of that level's pixels (IcpPlan::span) in passes of up to kIcpPix per
+// lane, re-reading them every iteration, their products added into the same
+// lane sums (integers below 2^53 for <= 8192 pixels per block, so the fp64
+// adds stay exact and the int64 totals are the oracle's); a longer range
+// takes groups b, b + gridDim, ... with one block reduce per group.
 template <bool kStride>
 __global__ __launch_bounds__(kIcpThreads, KFX_ICP_MINB) void k_icp_track(IcpPlan pl, DevState *__restrict__ st,
                                                    IcpSync *__restrict__ sy, int begin) {
@@ -870,7 +871,22 @@ __global__ __launch_bounds__(kIcpThreads, KFX_ICP_MINB) void k_icp_track(IcpPlan
 #endif
       if (mine) {
         long long bsum = 0;
-        if (stride) {
+        if (stride && pl.span[l] > 0) {
+          // this block's contiguous range, in passes of up to kIcpPix pixels
+          // per lane whose products add into the same lane sums (integers
+          // below 2^53: exact), then one block reduce
+          const int b0 = (int)blockIdx.x * pl.span[l], b1 = min(pl.npix[l], b0 + pl.span[l]);
+          double acc[27];
+#pragma unroll
+          for (int k = 0; k < 27; ++k) acc[k] = 0.0;
+          for (int p0 = b0; p0 < b1; p0 += kIcpPix * kIcpThreads) {
+            const int ppl = min(kIcpPix, (b1 - p0 + kIcpThreads - 1) / kIcpThreads);
+            icp_load_cur(g, pl.xe[l], b1, 0, ppl, pl.cv[l], pl.cn[l], n0, v0, ok, p0);
+            icp_lane(g, P, n0, v0, ok, ppl, pl.pv[l], pl.pn[l], pl.dist2_max, pl.sine2_max, acc, false);
+          }
+          if (tr && blockIdx.x == 0) sy->trace[slot][8] = wall_clock64() + (acc[3] == -1.5 ? 1 : 0);
+          bsum = icp_block_reduce(red, acc);
+        } else if (stride) {
           // groups blockIdx.x, + gridDim.x, ...: each group's block sums are
           // added as int64 (exact), so no lane sums stay live across groups
           for (int gx = (int)blockIdx.x; gx < pl.groups[l]; gx += (int)gridDim.x) {
@@ -3221,6 +3237,19 @@ bool icp_persistent_ok(IcpPlan &pl, int device) {
   if (cap <= 0 || (pl.nblocks + cap - 1) / cap > kIcpStrideMax) return false;
   pl.nblocks = cap;
   pl.stride = 1;
+  // levels with more groups than blocks: equal contiguous ranges (every block
+  // runs ceil(npix / cap) pixels instead of one or two whole groups)
+  for (int l = 0; l < pl.levels; ++l) {
+    pl.span[l] = 0;
+    if (pl.groups[l] <= cap) continue;
+    const int per = (pl.npix[l] + cap - 1) / cap;
+    const int span = (per + kIcpThreads - 1) / kIcpThreads * kIcpThreads;
+    // a block's fp64 sums of 2^-32-scaled products (|product| < 2^7) stay
+    // exact integers below 2^53 for up to 2^14 pixels: keep a margin of 2
+    if (span > 8 * kIcpPix * kIcpThreads) continue;
+    pl.span[l] = span;
+    pl.groups[l] = (pl.npix[l] + span - 1) / span;
+  }
   return true;
 }
 

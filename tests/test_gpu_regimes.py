@@ -248,7 +248,9 @@ def test_2048_single_volume_columns_match_oracle():
 def test_c4_1024_eight_slabs_match_single_volume():
     """C4 (1024^3 @ 2 mm Z-slab sharded 8 ways) as an in-process group on one
     GPU: poses, the combined model maps of every level and the order-free
-    volume checksum equal the single 1024^3 volume's, frame by frame."""
+    volume checksum equal the single 1024^3 volume's, frame by frame; and
+    2000 columns of that single volume equal the oracle restating just those
+    columns at the tracked poses."""
     intr = synth.Intrinsics.vga()
     I = Intrinsics.from_any(intr)
     bgr, dep, _ = synth.sequence(3, intr, noise=True, dropout=0.005)
@@ -270,7 +272,23 @@ def test_c4_1024_eight_slabs_match_single_volume():
     assert (sum(s[0] for s in sums) & ((1 << 64) - 1), sum(s[1] for s in sums)) == ref and ref[1] > 10**6
     for m in members:
         m.close()
+    n = 1024
+    rng = np.random.default_rng(4)
+    cols = np.unique(np.stack([rng.integers(0, n, 2000), rng.integers(0, n, 2000)], 1).astype(np.int32), axis=0)
+    gt_, gw, gc = single.download_columns(cols)
+    poses = single.pose_record
     single.close()
+    vol = O.Volume((n,) * 3, (L_VOL,) * 3)
+    for k in range(3):
+        ds, _, _ = O.preprocess(dep[k].astype(np.float32), I, p)
+        vol2cam = O.pose_mul(O.pose_inv(Pose.from_matrix(poses[k])), p.volu_pose)
+        O.integrate(vol, p.volu_trun_dist, I, vol2cam, ds[0], bgr[k], cols=cols)
+    idx = (cols[:, 0][:, None].astype(np.int64) + n * cols[:, 1][:, None].astype(np.int64)
+           + n * n * np.arange(n, dtype=np.int64)[None, :])
+    assert np.array_equal(gt_, vol.tsdf[idx]), f"tsdf: {(gt_ != vol.tsdf[idx]).sum()} differ"
+    assert np.array_equal(gw, vol.weight[idx])
+    assert np.array_equal(gc, vol.rgb.reshape(-1, 4)[idx])
+    assert (gw > 0).sum() > 50000
 
 
 def test_raycast_uniq_count_matches_oracle():

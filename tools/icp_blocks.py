@@ -2,7 +2,7 @@
 """Per-block ICP phase stamps (debug library built with -DKFX_ICP_BLOCK_TRACE):
 for each iteration, the spread of block lane-phase starts and arrivals (us,
 relative to block 0's start), and which blocks arrive last.
-usage: KFX_LIB_PATH=<debug lib> python3 tools/icp_blocks.py"""
+usage: KFX_LIB_PATH=<debug lib> python3 tools/icp_blocks.py [hd720]"""
 import ctypes as C
 import os
 import sys
@@ -14,11 +14,13 @@ import kfx  # noqa: E402
 from kfx import synth  # noqa: E402
 from kfx.abi import default_params  # noqa: E402
 
-intr = synth.Intrinsics.vga()
-kf = kfx.KinectFusion(intr, default_params())
+hd = len(sys.argv) > 1 and sys.argv[1] == "hd720"
+intr = synth.Intrinsics.hd720() if hd else synth.Intrinsics.vga()
+L = 4.096 if hd else 2.048
+kf = kfx.KinectFusion(intr, default_params(dims=512, range_m=L))
 # the benchmark's regime: frames staged in HBM, overlapped launches (the
 # next frame's preprocess runs beside this frame's ICP), 25 frames
-bgr, dep, _ = synth.sequence(25, intr)
+bgr, dep, _ = synth.sequence(25, intr, L=L)
 kf.stage_frames(bgr, dep.astype(np.float32))
 for k in range(len(dep)):
     kf.pipeline_staged(k)
@@ -34,5 +36,6 @@ for s in range(n):
     lane = ars - sts
     last = np.argsort(-ar[used])[:5]
     print(f"it {s:2d} blocks {used.sum():3d} start spread {sts.min():6.2f}..{sts.max():6.2f}  "
-          f"arrive {ars.min():6.2f}..{ars.max():6.2f}  phase med {np.median(lane):5.2f} max {lane.max():5.2f}  "
+          f"arrive {ars.min():6.2f}..{ars.max():6.2f}  phase med {np.median(lane):5.2f} "
+          f"p90 {np.percentile(lane, 90):5.2f} p99 {np.percentile(lane, 99):5.2f} max {lane.max():5.2f}  "
           f"last {list(np.nonzero(used)[0][last])}")
