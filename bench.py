@@ -320,15 +320,16 @@ def run_stream(a, intr, params, frames, D, local, slab=None, icp_ar=False, timin
     Returns the open context and the timed-region record; the caller closes it."""
     import kfx
     from kfx.abi import Intrinsics
-    bgr, dep, order, gt = frames
+    bgr, dep, order, gt = frames  # gt: the trajectory's poses (slab cut calibration), or None
     cuts = None
     if slab is not None and a.cuts != "equal":
-        if a.cuts == "first":
+        if a.cuts == "first" or gt is None:
             calib = [order[0]]
         else:  # 4 frames spread over the timed run's distinct frames
             seen = sorted(set(order[a.warmup:a.warmup + a.steps]))
             calib = [seen[int(round(j * (len(seen) - 1) / 3))] for j in range(4)]
-        cuts = balanced_cuts(intr, params, [(bgr[i], dep[i], gt[i]) for i in calib], local, slab[1])
+        cuts = balanced_cuts(intr, params, [(bgr[i], dep[i], None if gt is None else gt[i]) for i in calib], local,
+                             slab[1])
     kf = kfx.KinectFusion(Intrinsics.from_any(intr), params, device=local, slab=slab, cuts=cuts)
     if slab is not None:
         kf.comm_init(D.bcast_bytes(kfx.comm_unique_id() if slab[0] == 0 else None))
@@ -536,7 +537,7 @@ def main():
         b = copy.copy(a)
         b.steps = a.c3_frames
         W3, H3, n3, L3 = CONFIGS["c3"]
-        f3 = (bgr, dep, synth.ping_pong(len(bgr), b.warmup + b.steps))
+        f3 = (bgr, dep, synth.ping_pong(len(bgr), b.warmup + b.steps), None)
         out["c3_record"] = single_record(b, "c3", intr, n3, L3, f3, D, local)
     # N=1: the C5 single volume (1280x720, 2048^3 @ 2 mm), the N=1 point of the
     # zslab curve the driver's N>1 runs record

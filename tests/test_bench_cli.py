@@ -101,3 +101,79 @@ def test_imbalance():
     assert b.imbalance([1.0, 1.0]) == 1.0
     assert b.imbalance([3.0, 1.0]) == 1.5
     assert b.imbalance([1.0, float("nan")]) is None
+
+
+class _FakeKF:
+    """Stands in for kfx.KinectFusion in run_stream's plumbing test (no GPU)."""
+    calls = []
+
+    def __init__(self, intr, params, device=0, slab=None, cuts=None):
+        self.slab, self.cuts, self.n = slab, cuts, 1
+        _FakeKF.calls.append(("create", slab, cuts))
+
+    def slice_work_at(self, bgr, dep, pose=None):
+        import numpy as np
+        _FakeKF.calls.append(("work", pose is not None))
+        w = np.arange(64, dtype=np.int64)
+        return w, w, w
+
+    def pipeline_staged(self, i):
+        self.n += 1
+
+    @property
+    def pose_record(self):
+        import numpy as np
+        return np.zeros((self.n, 4, 4))
+
+    def graph_mode(self):
+        return 1
+
+    def kernel_timing(self):
+        return {"samples": 0}
+
+    def synchronize(self):
+        return 0
+
+    def __getattr__(self, name):  # comm_init, set_* , stage_frames, close
+        return lambda *a, **k: None
+
+
+def test_run_stream_plumbing_without_gpu(monkeypatch):
+    """run_stream / balanced_cuts wiring on CPU with a stand-in kfx: frame
+    tuples carry the trajectory's poses (or None), slab cuts come from the mean
+    work of 4 calibration frames at their poses ('balanced'), of the first
+    frame ('first', or no poses), or are equal ('equal')."""
+    import numpy as np
+    b = load_bench()
+    fake = types.ModuleType("kfx")
+    fake.KinectFusion = _FakeKF
+    fake.KFX_OK = 0
+    fake.comm_unique_id = lambda: b""
+    fake.slab_balance = lambda work, world: [0, 32, 64]
+    abi = types.ModuleType("kfx.abi")
+    abi.Intrinsics = types.SimpleNamespace(from_any=lambda x: x)
+    monkeypatch.setitem(sys.modules, "kfx", fake)
+    monkeypatch.setitem(sys.modules, "kfx.abi", abi)
+
+    class D:
+        barrier = staticmethod(lambda: None)
+        max = staticmethod(lambda x: x)
+        bcast_bytes = staticmethod(lambda x: b"")
+
+    params = types.SimpleNamespace(volu_dims=[64, 64, 64])
+    a = types.SimpleNamespace(cuts="balanced", warmup=2, steps=6, no_graph=False, graph_full=False, no_overlap=False,
+                              sample_every=0)
+    n = 8
+    frames = ([None] * n, [None] * n, list(range(n)) + list(range(n)), [np.eye(4)] * n)
+    for cuts, gt, slab, want in (("balanced", True, (0, 2), 4), ("first", True, (0, 2), 1),
+                                 ("balanced", False, (0, 2), 1), ("equal", True, (0, 2), 0),
+                                 ("balanced", True, None, 0)):
+        _FakeKF.calls = []
+        a.cuts = cuts
+        f = frames if gt else frames[:3] + (None,)
+        kf, r = b.run_stream(a, None, params, f, D, 0, slab=slab)
+        works = [c for c in _FakeKF.calls if c[0] == "work"]
+        assert len(works) == want and all(w[1] == gt for w in works), (cuts, gt, slab, _FakeKF.calls)
+        created = [c for c in _FakeKF.calls if c[0] == "create" and c[1] == slab]
+        assert created[-1][2] == ([0, 32, 64] if want else None)
+        assert r["tracked"] == a.steps and r["graph_mode"] == 1
