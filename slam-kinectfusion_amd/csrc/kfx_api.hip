@@ -1335,10 +1335,9 @@ int kfx_get_kernel_timing_ex(kfx_ctx *c, float out_ms[4], int *n_samples) {
     }
   }
   for (int i = 0; i < 4; ++i) out_ms[i] = c->tnext ? (float)(acc[i] / (double)c->tnext) : 0.f;
-  if (!c->slab) {  // a single volume's resize runs after the raycast event pair
-    out_ms[2] += out_ms[3];
-    out_ms[3] = 0.f;
-  }
+  // a single volume has no combine: its raycast (the pyramid resize fused in)
+  // ends at [5], and [6]..[4] only span the remaining event records
+  if (!c->slab) out_ms[3] = 0.f;
   if (n_samples) *n_samples = (int)c->tnext;
   c->tnext = 0;
   return KFX_OK;
