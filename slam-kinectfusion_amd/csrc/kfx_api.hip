@@ -310,11 +310,13 @@ int enqueue_frame(kfx_ctx *c, FrameInput in, hipEvent_t *ev) {
   enqueue_pre(c, in, ev);
   int r = enqueue_track(c, in, ev, false);
   if (ev) (void)hipEventRecord(ev[5], c->stream);
-  if (ev) (void)hipEventRecord(ev[6], c->stream);
-  if (ev) (void)hipEventRecord(ev[7], c->stream);  // (no shared part: [7] = [8])
-  if (ev) (void)hipEventRecord(ev[8], c->stream);
+  if (ev && c->slab) {  // (a single volume's sample ends at [5]: no combine to time)
+    (void)hipEventRecord(ev[6], c->stream);
+    (void)hipEventRecord(ev[7], c->stream);  // (no shared part: [7] = [8])
+    (void)hipEventRecord(ev[8], c->stream);
+  }
   if (!r && c->slab) r = enqueue_combine(c);
-  if (ev) (void)hipEventRecord(ev[4], c->stream);
+  if (ev) (void)hipEventRecord(ev[4], c->stream);  // (the profiled frames' end)
   return r;
 }
 
@@ -496,11 +498,13 @@ int enqueue_main_overlap(kfx_ctx *c, FrameInput in, hipEvent_t *ev) {
   if (ev) HIPCHK(hipEventRecord(ev[1], c->stream));
   int r = enqueue_track(c, in, ev, true);
   if (ev) HIPCHK(hipEventRecord(ev[5], c->stream));
-  if (ev) HIPCHK(hipEventRecord(ev[6], c->stream));
-  if (ev) HIPCHK(hipEventRecord(ev[7], c->stream));
-  if (ev) HIPCHK(hipEventRecord(ev[8], c->stream));
+  if (ev && c->slab) {  // (a single volume's sample ends at [5])
+    HIPCHK(hipEventRecord(ev[6], c->stream));
+    HIPCHK(hipEventRecord(ev[7], c->stream));
+    HIPCHK(hipEventRecord(ev[8], c->stream));
+  }
   if (!r && c->slab) r = enqueue_combine(c);
-  if (ev) HIPCHK(hipEventRecord(ev[4], c->stream));
+  if (ev && c->slab) HIPCHK(hipEventRecord(ev[4], c->stream));
   return r;
 }
 
@@ -1325,19 +1329,20 @@ int kfx_get_kernel_timing_ex(kfx_ctx *c, float out_ms[4], int *n_samples) {
   // [4] frame done; [1] the frame's tracking starts
   // [7]..[8] the shared part of a group combine (elapsed 0 elsewhere), added
   // to the member's own combine [6]..[4]
+  // (a single volume records [1], [2], [3], [5] only: every event record in
+  // a sampled frame costs the run time)
   static const int kFrom[5] = {1, 2, 3, 6, 7}, kTo[5] = {2, 3, 5, 4, 8};
+  const int pairs = c->slab ? 5 : 3;
   double acc[4] = {0, 0, 0, 0};
   for (size_t k = 0; k < c->tnext; ++k) {
-    for (int i = 0; i < 5; ++i) {
+    for (int i = 0; i < pairs; ++i) {
       float ms = 0.f;
       HIPCHK(hipEventElapsedTime(&ms, c->tsets[kStageEvents * k + kFrom[i]], c->tsets[kStageEvents * k + kTo[i]]));
       acc[i < 4 ? i : 3] += ms;
     }
   }
   for (int i = 0; i < 4; ++i) out_ms[i] = c->tnext ? (float)(acc[i] / (double)c->tnext) : 0.f;
-  // a single volume has no combine: its raycast (the pyramid resize fused in)
-  // ends at [5], and [6]..[4] only span the remaining event records
-  if (!c->slab) out_ms[3] = 0.f;
+
   if (n_samples) *n_samples = (int)c->tnext;
   c->tnext = 0;
   return KFX_OK;
@@ -1899,6 +1904,11 @@ int kfx_set_slab_bound(kfx_ctx *c, int mode) {
   int r = check_ctx(c);
   if (r) return r;
   if (mode < 0 || mode > 2) return set_err(KFX_ERR_ARG, "slab bound modes are 0, 1, 2");
+  if (mode != c->slab_bound) {  // captured frames hold the old passes
+    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipStreamSynchronize(c->pstream));
+    destroy_graphs(c);
+  }
   c->slab_bound = mode;
   return KFX_OK;
 }
