@@ -405,3 +405,38 @@ def test_slice_work_at_pose(seq_qvga):
     assert abs(int(uk.sum()) - nu) <= 0.01 * nu, (int(uk.sum()), nu)
     assert not np.array_equal(uk, u)
     kf.close()
+
+
+@pytest.mark.gpu
+def test_slab_bound_switch_with_captured_graphs(seq_qvga):
+    """A one-rank RCCL slab context replaying captured per-frame graphs and
+    overlapped staged frames (graph mode 2) switches the bounded raycast on
+    and off mid-sequence (kfx_set_slab_bound drops the captured graphs): every
+    frame still equals the single volume's."""
+    bgr, dep, _ = seq_qvga
+    intr = synth.Intrinsics.qvga()
+    p = default_params(dims=64, range_m=L_VOL)
+    single, st = _single(intr, p, bgr, dep)
+    m = KinectFusion(Intrinsics.from_any(intr), p, slab=(0, 1))
+    m.comm_init(comm_unique_id())
+    m.set_graph_mode(2)
+    gst = []
+    for k in range(len(dep)):
+        if k in (3, 6):
+            m.set_slab_bound(1 if k == 3 else 0)
+        gst.append(m.pipeline(bgr[k], dep[k].astype(np.float32)))
+    assert gst == st
+    _compare(single, [m])
+    single2, _ = _single(intr, p, bgr, dep)
+    single2.stage_frames(bgr, dep.astype(np.float32))
+    m.stage_frames(bgr, dep.astype(np.float32))
+    for k in range(len(dep)):
+        if k == 4:
+            m.synchronize()
+            m.set_slab_bound(2)
+        m.pipeline_staged(k)
+        single2.pipeline_staged(k)
+    m.synchronize()
+    single2.synchronize()
+    _compare(single2, [m])
+    m.close()
