@@ -178,10 +178,12 @@ int kfx_debug_force_icp_stall(kfx_ctx *ctx);
  * per iteration (19 collectives per frame), then every rank solves the same
  * system — poses identical to the replicated mode. */
 int kfx_set_icp_allreduce(kfx_ctx *ctx, int enabled);
-/* Profiling seam: per ICP iteration of the last persistent-ICP frame, five
- * s_memrealtime stamps (100 MHz): block 0 start, block 0 arrived, block 0
- * released from the barrier, block 0 solved, last block arrived.  Returns the
- * number of iterations written (<= max_iters). */
+/* Profiling seam (trace builds, -DKFX_ICP_TRACE via tools/variants.sh; the
+ * product library returns 0: the stamps' code costs ICP ~3 us per frame):
+ * per ICP iteration of the last persistent-ICP frame, five s_memrealtime
+ * stamps (100 MHz): block 0 start, block 0 arrived, block 0 released from the
+ * barrier, block 0 solved, last block arrived.  Returns the number of
+ * iterations written (<= max_iters). */
 int kfx_get_icp_trace(kfx_ctx *ctx, uint64_t *out, int max_iters);
 
 /* kinectfusion::getCurCameraPose() (kinectfusion.cpp:128-132). */

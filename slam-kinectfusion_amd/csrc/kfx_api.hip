@@ -1410,10 +1410,14 @@ int kfx_get_icp_trace(kfx_ctx *c, uint64_t *out, int max_iters) {
   int r = check_ctx(c);
   if (r) return r;
   if (!out || max_iters < 0) return set_err(KFX_ERR_ARG, "null argument");
+#ifdef KFX_ICP_TRACE
   const int n = std::min(max_iters, c->icp_plan.slots);
   HIPCHK(hipStreamSynchronize(c->stream));
   HIPCHK(hipMemcpy(out, c->icp_sync->trace, sizeof(uint64_t) * 12 * (size_t)n, hipMemcpyDeviceToHost));
   return n;
+#else
+  return 0;  // stamps exist in trace builds only (-DKFX_ICP_TRACE, tools/variants.sh)
+#endif
 }
 
 int kfx_set_profiling(kfx_ctx *c, int enabled) {

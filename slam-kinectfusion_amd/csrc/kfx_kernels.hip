@@ -864,7 +864,11 @@ __global__ __launch_bounds__(kIcpThreads, KFX_ICP_MINB) void k_icp_track(IcpPlan
     for (int it = 0; it < pl.iters[l] && !fail; ++it, ++slot) {
       unsigned long long *sh = sy->sums + (size_t)slot * kIcpShards * 27;
       target += min(pl.groups[l], (int)gridDim.x);  // arrivals: the blocks with a group
+#ifdef KFX_ICP_TRACE
       const bool tr = threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x - 1);
+#else
+      constexpr bool tr = false;  // trace build only: the stamps' code costs ICP ~3 us per frame
+#endif
       if (tr && blockIdx.x == 0) sy->trace[slot][0] = wall_clock64();
 #ifdef KFX_ICP_BLOCK_TRACE
       if (threadIdx.x == 0 && blockIdx.x < 512) sy->blk[slot][blockIdx.x][0] = wall_clock64();

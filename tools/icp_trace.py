@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Phase timing of the persistent ICP kernel on a VGA 512^3 run (GPU box);
+"""Phase timing of the persistent ICP kernel on a VGA 512^3 run (GPU box; a trace
+build: tools/variants.sh trace -DKFX_ICP_TRACE, then KFX_LIB_PATH=.../lib/var_trace/libkfx.so);
 `icp_trace.py hd720`: 1280x720 frames (C5's size) on a 512^3 volume of C5's
 4.096 m extent."""
 import os
