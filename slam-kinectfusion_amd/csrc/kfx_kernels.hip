@@ -1563,13 +1563,19 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
   (void)invl;
   constexpr Idx slice = 64;  // index step per z (tile-column layout)
   Idx iz = (Idx)base + (Idx)(za - v.zb) * slice;  // voxel index of (x, y, z)
-  const bool fast = __all(!live || column_fast(vc, zs, v.Z));  // wave-uniform
+  const bool fastw = __all(!live || column_fast(vc, zs, v.Z));  // wave-uniform
   const float fw = (float)g.w, fh = (float)g.h;
   // Batches of kB voxels: positions, projections, the kB {depth, 1/lambda}
   // gathers, then the kB tsdf/weight loads are issued back to back
   // (memory-level parallelism); each voxel's arithmetic is exactly the
   // reference's (tsdf_volume.cu:56-98).
   constexpr int kB = KFX_INT_KB;
+  // The z loop is instantiated once per path (fast: the packed exact
+  // sequences; else IEEE division and sqrt) and the wave picks one: the fast
+  // loop then carries no code or registers of the other (integrate −2 %,
+  // six alternating pairs, against one loop branching on `fast` per batch).
+  auto zloop = [&](auto fast_c) {
+    constexpr bool fast = decltype(fast_c)::value;
   for (; z <= zb; z += kB) {
     float sdf[kB];
     unsigned pix[kB];
@@ -1581,7 +1587,7 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
       p[j] = vc;
     }
     // projection: ok = in the image in front of the camera (tsdf_volume.cu:56-66)
-    if (fast) {  // the cheap exact sequences, two voxels per packed-FP32 op
+    if constexpr (fast) {  // the cheap exact sequences, two voxels per packed-FP32 op
       static_assert(kB % 2 == 0, "voxel pairs");
 #pragma unroll
       for (int j = 0; j < kB; j += 2) {
@@ -1621,7 +1627,7 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
     for (int j = 0; j < kB; ++j)
       d[j] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rdl, pix[j], 0, 0));
     // sdf and the depth test (tsdf_volume.cu:67-71)
-    if (fast) {
+    if constexpr (fast) {
 #pragma unroll
       for (int j = 0; j < kB; j += 2) {
         // d - il |vc| = -(il |vc| - d) exactly (RN is odd-symmetric); only the
@@ -1718,6 +1724,9 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
       }
     }
   }
+  };
+  if (fastw) zloop(std::true_type{});
+  else zloop(std::false_type{});
   if (!kCount) {  // raycast skip maps
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
