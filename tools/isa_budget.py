@@ -33,22 +33,29 @@ loops = collections.defaultdict(int)
 for b in blocks:
     if b[1]:
         loops[b[1]] += b[2]["buffer_load_dwordx2"]
-main = max(loops, key=loops.get)
-out = [f"k_integrate<false, true> main loop {main}: per basic block (code order)",
-       f"{'block':14s} {'VALU':>5s} {'SALU':>5s} {'VMEM':>5s} {'LDS':>4s}  notable"]
-tot = collections.Counter()
-for name, loop, c in blocks:
-    if loop != main:
-        continue
-    v = sum(n for k, n in c.items() if k.startswith("v_"))
-    sa = sum(n for k, n in c.items() if k.startswith("s_"))
-    vm = sum(n for k, n in c.items() if k.startswith(("buffer_", "global_")))
-    ds = sum(n for k, n in c.items() if k.startswith("ds_"))
-    tot.update({"VALU": v, "SALU": sa, "VMEM": vm, "LDS": ds})
-    note = ", ".join(f"{k} {n}" for k, n in c.most_common() if k.startswith(("v_rcp", "v_rsq", "v_pk_", "buffer_load",
-                                                                                "buffer_store", "v_readlane", "ds_")))[:90]
-    out.append(f"{name:14s} {v:5d} {sa:5d} {vm:5d} {ds:4d}  {note}")
-out.append(f"{'loop total':14s} {tot['VALU']:5d} {tot['SALU']:5d} {tot['VMEM']:5d} {tot['LDS']:4d}  (static: both the fast and the IEEE paths)")
+# the z loops: one per path since round 4 (packed exact / IEEE), each with the
+# batch's depth gathers; the fast one's sqrt is v_rsq_f32 + Newton
+mains = [l for l, n in loops.items() if n > 0]
+out = []
+for main in mains:
+    rsq = sum(n for _, loop, c in blocks if loop == main for k, n in c.items() if k.startswith("v_rsq"))
+    kind = "fast path (packed exact projection, rsq-Newton sqrt)" if rsq else "IEEE path (tiny / huge operands)"
+    out += [f"k_integrate<false, true> z loop {main}, {kind}: per basic block (code order)",
+            f"{'block':14s} {'VALU':>5s} {'SALU':>5s} {'VMEM':>5s} {'LDS':>4s}  notable"]
+    tot = collections.Counter()
+    for name, loop, c in blocks:
+        if loop != main:
+            continue
+        v = sum(n for k, n in c.items() if k.startswith("v_"))
+        sa = sum(n for k, n in c.items() if k.startswith("s_"))
+        vm = sum(n for k, n in c.items() if k.startswith(("buffer_", "global_")))
+        ds = sum(n for k, n in c.items() if k.startswith("ds_"))
+        tot.update({"VALU": v, "SALU": sa, "VMEM": vm, "LDS": ds})
+        note = ", ".join(f"{k} {n}" for k, n in c.most_common() if k.startswith(("v_rcp", "v_rsq", "v_pk_", "buffer_load",
+                                                                                    "buffer_store", "v_readlane", "ds_")))[:90]
+        out.append(f"{name:14s} {v:5d} {sa:5d} {vm:5d} {ds:4d}  {note}")
+    out.append(f"{'loop total':14s} {tot['VALU']:5d} {tot['SALU']:5d} {tot['VMEM']:5d} {tot['LDS']:4d}  (static)")
+    out.append("")
 text_out = "\n".join(out)
 print(text_out)
 if len(sys.argv) > 1:
