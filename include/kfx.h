@@ -172,6 +172,11 @@ int kfx_set_icp_persistent(kfx_ctx *ctx, int enabled);
 /* Test hook: the next tracked frame's persistent-ICP barrier never completes
  * (its watchdog fires after 0.2 s). */
 int kfx_debug_force_icp_stall(kfx_ctx *ctx);
+/* Test hook: on != 0 routes integrate and raycast through the 64-bit-index
+ * kernels (the path a volume of >= 2^31 stored voxels takes, A9:
+ * device_utils.cuh:31, tsdf_volume.cpp:24) at any volume size, so the oracle
+ * can pin them at sizes it runs.  Results are identical either way. */
+int kfx_debug_force_index64(kfx_ctx *ctx, int on);
 /* Slab contexts (SURVEY.md §8e alternative): instead of every rank running
  * the whole ICP (default), rank r accumulates the 27 products over its band
  * of each level's rows and the exact int64 partials are all-reduced (SUM)
@@ -414,7 +419,12 @@ int kfx_slab_balance(const int64_t *slice_work, int Z, int world, int *cuts);
  * slab holds the surfaces most rays end on, so the bound did not lower it and
  * the second pass cost more); 1: on; 2: on without the margin
  * (test: most pixels take the second pass).  Results are identical in every
- * mode. */
+ * mode.  The mode decides which collectives a frame's combine issues, so it is
+ * one mode for the whole decomposition: on a context with a communicator the
+ * call is collective (every rank calls it with the same mode; a mismatch
+ * returns KFX_ERR_ARG on every rank and leaves the mode unchanged), the mode
+ * held at kfx_comm_init is checked the same way, and kfx_pipeline_group
+ * refuses members whose modes differ. */
 int kfx_set_slab_bound(kfx_ctx *ctx, int mode);
 /* stored slices [zb, zb+zn), owned slices [own0, own1) */
 int kfx_slab_info(kfx_ctx *ctx, int *zb, int *zn, int *own0, int *own1);

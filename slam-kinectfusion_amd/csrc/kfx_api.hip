@@ -1398,6 +1398,18 @@ int kfx_debug_force_icp_stall(kfx_ctx *c) {
   return write_field(c, offsetof(DevState, debug_stall), 1);
 }
 
+int kfx_debug_force_index64(kfx_ctx *c, int on) {
+  int r = check_ctx(c);
+  if (r) return r;
+  if ((c->vol.force64 != 0) != (on != 0)) {  // captured frames hold the other kernels
+    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipStreamSynchronize(c->pstream));
+    destroy_graphs(c);
+  }
+  c->vol.force64 = on != 0;
+  return KFX_OK;
+}
+
 int kfx_set_icp_allreduce(kfx_ctx *c, int enabled) {
   if (!c) return set_err(KFX_ERR_ARG, "null context");
   if (!c->slab) return set_err(KFX_ERR_STATE, "ICP partial all-reduce needs a slab context");
@@ -1904,6 +1916,35 @@ static int extract_events(kfx_ctx *c) {
   return KFX_OK;
 }
 
+// The slab bound decides which collectives a frame's combine issues (the
+// [key | pend] MIN and the resume pass run only when bounded), so every rank of
+// a communicator must hold the same mode: checked by a MIN and a MAX
+// all-reduce of it (blocking; every rank is inside the same call).
+static int comm_check_slab_bound(kfx_ctx *c, int mode) {
+  int *d = nullptr;
+  HIPCHK(hipMalloc(&d, 2 * sizeof(int)));
+  const int h0[2] = {mode, mode};
+  int h[2] = {0, 0};
+  int r = KFX_OK;
+  if (hipMemcpy(d, h0, sizeof(h0), hipMemcpyHostToDevice) != hipSuccess) {
+    r = set_err(KFX_ERR_HIP, "slab bound check: upload");
+  } else {
+    ncclResult_t e = ncclGroupStart();
+    if (e == ncclSuccess) e = ncclAllReduce(d, d, 1, ncclInt32, ncclMin, c->comm, c->stream);
+    if (e == ncclSuccess) e = ncclAllReduce(d + 1, d + 1, 1, ncclInt32, ncclMax, c->comm, c->stream);
+    const ncclResult_t e2 = ncclGroupEnd();
+    if (e == ncclSuccess) e = e2;
+    if (e != ncclSuccess)
+      r = set_err(KFX_ERR_COMM, std::string("slab bound check: ") + ncclGetErrorString(e));
+    else if (hipStreamSynchronize(c->stream) != hipSuccess || hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost) != hipSuccess)
+      r = set_err(KFX_ERR_HIP, "slab bound check: download");
+    else if (h[0] != h[1])
+      r = set_err(KFX_ERR_ARG, "ranks differ in kfx_set_slab_bound mode (every rank must pass the same mode)");
+  }
+  (void)hipFree(d);
+  return r;
+}
+
 int kfx_set_slab_bound(kfx_ctx *c, int mode) {
   int r = check_ctx(c);
   if (r) return r;
@@ -1913,6 +1954,8 @@ int kfx_set_slab_bound(kfx_ctx *c, int mode) {
     HIPCHK(hipStreamSynchronize(c->pstream));
     destroy_graphs(c);
   }
+  // over a communicator the call is collective: every rank passes the same mode
+  if (c->comm && (r = comm_check_slab_bound(c, mode))) return r;
   c->slab_bound = mode;
   return KFX_OK;
 }
@@ -2352,7 +2395,7 @@ int kfx_comm_init(kfx_ctx *c, const uint8_t id[KFX_COMM_ID_BYTES]) {
   std::memcpy(&u, id, sizeof(u));
   NCCLCHK(ncclCommInitRank(&c->comm, c->world, u, c->rank));
   destroy_graphs(c);
-  return KFX_OK;
+  return comm_check_slab_bound(c, c->slab_bound);
 }
 
 int kfx_pipeline_group(kfx_ctx **cs, int n, const uint8_t *bgr, const float *depth_mm) {
@@ -2364,6 +2407,9 @@ int kfx_pipeline_group(kfx_ctx **cs, int n, const uint8_t *bgr, const float *dep
       return set_err(KFX_ERR_ARG, "group member k must be slab k of n without a communicator");
     if (c->intr.width != cs[0]->intr.width || c->intr.height != cs[0]->intr.height)
       return set_err(KFX_ERR_ARG, "group members differ in image size");
+    // the bound decides which combine passes run: one mode for the whole group
+    if (c->slab_bound != cs[0]->slab_bound)
+      return set_err(KFX_ERR_ARG, "group members differ in kfx_set_slab_bound mode");
   }
   const size_t np = (size_t)cs[0]->intr.width * cs[0]->intr.height;
   for (int k = 0; k < n; ++k) {  // members on other devices are read by peer access

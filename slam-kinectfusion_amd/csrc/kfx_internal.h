@@ -125,6 +125,7 @@ struct VolView {
   unsigned *iperm;
   int inchunk;
   int iadapt;  // length-capped chunks + longest-first order (deep volumes), else geometric chunks
+  int force64;  // kfx_debug_force_index64: integrate / raycast take the 64-bit-index kernels at any size
   __host__ __device__ size_t bocc_bytes() const { return (size_t)tiles_x * tiles_y * bw * 8; }
   __host__ __device__ size_t socc_bytes() const { return (size_t)stx * sty * sw * 4; }
   __host__ __device__ size_t local_voxels() const { return slice * (size_t)zn; }

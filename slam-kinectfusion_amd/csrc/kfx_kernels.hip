@@ -1920,6 +1920,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((kSlab || !
 #ifdef KFX_RAY_TRACE
   const unsigned long long t_start = wall_clock64();
   unsigned long long t_march = 0, t_norm = 0, t_ndone = 0;
+  // wave iterations of the march loop by live-lane count: 1 | 2-4 | 5-16 | 17-64
+  unsigned long long t_hist = 0;
 #endif
   // cam2vol = volume_pose^-1 * pose, Rinv = R^T (tsdf_volume.cpp:59-61; D: transpose)
   __shared__ DevPose s_c2v;
@@ -2082,6 +2084,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((kSlab || !
 #endif
     while (__any(live || cand)) {
     while (__any(live)) {
+#ifdef KFX_RAY_TRACE
+      {
+        const int nl = __popcll(__ballot(live));
+        t_hist += 1ull << (nl <= 1 ? 0 : (nl <= 4 ? 16 : (nl <= 16 ? 32 : 48)));
+      }
+#endif
       if (kSlab && live && kbase > kb) {  // pass-1 bound: samples < kbase examined, no owned event
         live = false;
         pend = kbase;
@@ -2358,6 +2366,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((kSlab || !
       r[4] = t_march;
       r[5] = t_norm;
       r[6] = t_ndone;
+      r[7] = t_hist;
     }
   }
 #endif
@@ -3410,7 +3419,7 @@ void launch_integrate(hipStream_t s, VolView v, LevelGeom g0, const float2 *dl0,
   if (!v.iadapt) v.iperm = nullptr, v.iwork = nullptr;  // geometric chunks in block order
   if (counters) v.iwork = nullptr;  // the count-only pass leaves the order alone
   dim3 grd(tiles * nchunk);  // one wave (block) per (tile, chunk) item
-  const bool idx32 = v.local_voxels() < (1ull << 31);  // 32-bit tsdf/weight byte offsets
+  const bool idx32 = !v.force64 && v.local_voxels() < (1ull << 31);  // 32-bit tsdf/weight byte offsets
 #ifdef KFX_INT_TRACE
   static unsigned long long *trace_buf = nullptr;
   if (!trace_buf) {
@@ -3479,7 +3488,7 @@ void launch_raycast(hipStream_t s, VolView v, int levels, const LevelGeom *g, Fr
   for (int l = 0; l < levels; ++l) ra.g[l] = g[l];
   dim3 grd(((g[0].w + 15) / 16) * ((g[0].h + 15) / 16));
   // 32-bit tsdf byte offsets (24-bit operands of the tile * zn products)
-  const bool idx32 = v.local_voxels() < (1ull << 31) && (size_t)v.tiles_x * v.tiles_y < (1ull << 24) &&
+  const bool idx32 = !v.force64 && v.local_voxels() < (1ull << 31) && (size_t)v.tiles_x * v.tiles_y < (1ull << 24) &&
                      v.zn < (1 << 24);
   if (want_stats) {
     if (keys && idx32)

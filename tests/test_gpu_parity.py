@@ -603,3 +603,51 @@ def test_render_matches_oracle(seq_qvga):
             assert np.array_equal(got, want), (k, kind, int((got != want).sum()))
         assert (kf.render("phong") > 0).any()
     kf.close()
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("which", ["qvga128", "vga512"])
+def test_index64_kernels_match_oracle(which, seq_qvga, seq_vga):
+    """The 64-bit-index kernels (k_integrate<.., false>, k_raycast<false, ..>:
+    the path a volume of >= 2^31 stored voxels takes, A9 — the reference's
+    int32 index overflows there, device_utils.cuh:31, tsdf_volume.cpp:24)
+    forced at sizes the oracle runs (kfx_debug_force_index64): 128^3 QVGA and
+    BASELINE C2 (640x480, 512^3 @ 4 mm) through the whole pipeline against
+    O.Pipeline — poses, every level of the raycast model maps and the whole
+    volume bit for bit.  Pose tolerance 1e-6 (0 expected, as everywhere)."""
+    if which == "qvga128":
+        bgr, dep, _ = seq_qvga
+        intr, dims, n = synth.Intrinsics.qvga(), 128, 6
+    else:
+        bgr, dep, _ = seq_vga
+        intr, dims, n = synth.Intrinsics.vga(), 512, 3
+    I = Intrinsics.from_any(intr)
+    kf, p = make(intr, dims=dims)
+    kf.debug_force_index64(True)
+    pipe = O.Pipeline(I, p)
+    for k in range(n):
+        d = dep[k].astype(np.float32)
+        assert kf.pipeline(bgr[k], d) == pipe.process(bgr[k], d) == KFX_OK, k
+    gp, op = kf.pose_record, pipe.poses()
+    assert gp.shape == op.shape == (n, 4, 4)
+    err = float(np.abs(gp - op).max())
+    assert err <= 1e-6, err
+    assert np.abs(gp[-1] - np.eye(4)).max() > 1e-3  # tracked frames: the raycast maps fed ICP
+    if err != 0:
+        pytest.xfail(f"pose differs from the oracle by {err:.3g} (<= 1e-6): maps and volume not compared")
+    for l in range(3):
+        _, gv, gn = kf.frame_maps(KFX_FRAME_PREV, l)
+        assert feq(gv, pipe.map(1, 1, l)), f"vmap level {l}: {mismatch(gv, pipe.map(1, 1, l))} differ"
+        assert feq(gn, pipe.map(1, 2, l)), f"nmap level {l}: {mismatch(gn, pipe.map(1, 2, l))} differ"
+    t, w, c = kf.volume_soa()
+    ot, ow, oc = pipe.volume()
+    assert np.array_equal(t, ot), f"tsdf: {(t != ot).sum()} voxels differ"
+    assert np.array_equal(w, ow), f"weight: {(w != ow).sum()} voxels differ"
+    assert np.array_equal(c, oc), f"rgb: {(c != oc).sum()} bytes differ"
+    assert (w > 0).sum() > 10000
+    # the switch is per context and reversible: the 32-bit kernels continue the same stream identically
+    kf.debug_force_index64(False)
+    d = dep[n].astype(np.float32)
+    assert kf.pipeline(bgr[n], d) == pipe.process(bgr[n], d) == KFX_OK
+    assert np.abs(kf.pose_record - pipe.poses()).max() <= 1e-6
+    kf.close()

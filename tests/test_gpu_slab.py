@@ -11,7 +11,7 @@ rank, see tests/test_slab_dist.py for the multi-process decomposition check).
 import numpy as np
 import pytest
 
-from kfx import KFX_FRAME_PREV, KFX_OK, KFX_TRACKING_LOST, KinectFusion, comm_unique_id, pipeline_group, synth
+from kfx import KFX_FRAME_PREV, KFX_OK, KFX_TRACKING_LOST, KfxError, KinectFusion, comm_unique_id, pipeline_group, synth
 from kfx.abi import Intrinsics, default_params
 import oracle as O
 
@@ -380,6 +380,24 @@ def test_slab_bounded_raycast_modes_match_single_volume(mode, seq_qvga):
 
 
 @pytest.mark.gpu
+def test_group_refuses_mixed_slab_bound(seq_qvga):
+    """The bound decides which combine passes run, so it is one mode for the
+    whole decomposition: a group whose members differ is refused (KFX_ERR_ARG)
+    before any work, and runs once the modes agree."""
+    bgr, dep, _ = seq_qvga
+    intr = synth.Intrinsics.qvga()
+    p = default_params(dims=64, range_m=L_VOL)
+    members = [KinectFusion(Intrinsics.from_any(intr), p, slab=(r, 2)) for r in range(2)]
+    members[1].set_slab_bound(1)
+    with pytest.raises(KfxError, match="slab_bound"):
+        pipeline_group(members, bgr[0], dep[0].astype(np.float32))
+    members[0].set_slab_bound(1)
+    assert pipeline_group(members, bgr[0], dep[0].astype(np.float32)) == KFX_OK
+    for m in members:
+        m.close()
+
+
+@pytest.mark.gpu
 def test_slice_work_at_pose(seq_qvga):
     """kfx_slice_work_at: with no pose it is kfx_slice_work; at a later
     frame's pose its updated count matches that frame's integrate at the same
@@ -410,9 +428,16 @@ def test_slice_work_at_pose(seq_qvga):
 @pytest.mark.gpu
 def test_slab_bound_switch_with_captured_graphs(seq_qvga):
     """A one-rank RCCL slab context replaying captured per-frame graphs and
-    overlapped staged frames (graph mode 2) switches the bounded raycast on
-    and off mid-sequence (kfx_set_slab_bound drops the captured graphs): every
-    frame still equals the single volume's."""
+    overlapped staged frames (graph mode 2) switches the bound setting on and
+    off mid-sequence (kfx_set_slab_bound drops the captured graphs and, over a
+    communicator, checks the mode across ranks collectively): every frame
+    still equals the single volume's.  With one rank the bound itself never
+    engages (a frame is bounded only when world > 1), so this pins the
+    switch, the collective mode check and the graph invalidation; the bounded
+    passes are pinned by the in-process groups of
+    test_slab_bounded_raycast_modes_match_single_volume (world 4).  A
+    world >= 2 RCCL communicator cannot be built on this one-GPU pool (RCCL
+    refuses two ranks on one device)."""
     bgr, dep, _ = seq_qvga
     intr = synth.Intrinsics.qvga()
     p = default_params(dims=64, range_m=L_VOL)

@@ -50,6 +50,13 @@ tnd = np.where(a[:, 5] > 0, a[:, 6] - a[:, 5], 0) * 10
 tend = (a[:, 1] - a[:, 6]) * 10
 for name, x in (("setup", tm), ("march to first normal pass", tn), ("normal pass(es) + rest of loop", tnd), ("stores+resize", tend)):
     print(f"  phase {name:32s} us: med {np.median(x) / 1e3:6.2f} p90 {np.percentile(x, 90) / 1e3:6.2f} max {x.max() / 1e3:6.2f}")
+h = np.stack([(a[:, 7] >> (16 * k)) & 0xffff for k in range(4)], 1)
+tot = h.sum(1)
+print("march-loop iterations per wave by live lanes (1 | 2-4 | 5-16 | 17-64): "
+      f"all waves {h.sum(0).tolist()}")
+slow20 = np.argsort(dur)[-max(1, len(a) // 50):]
+print(f"  slowest 2% of waves: {h[slow20].sum(0).tolist()}  iterations med {np.median(tot[slow20]):.0f} max {tot.max()}")
+print(f"  median waves: iterations med {np.median(tot):.0f}")
 slow = np.argsort(dur)[-8:]
-print("slowest waves: dur us / lookups / batches", [(round(dur[i] / 1e3, 1), int(lk[i]), int(bt[i])) for i in slow])
+print("slowest waves: dur us / lookups / batches / live hist", [(round(dur[i] / 1e3, 1), int(lk[i]), int(bt[i]), h[i].tolist()) for i in slow])
 kf.close()
