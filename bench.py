@@ -71,9 +71,16 @@ def parse():
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r04_integrate_pmc.json"),
                     help="integrate PMC traffic record; attached only when it was measured on this command's "
                          "workload and step counts with the same libkfx.so (sha256)")
-    ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--graph-full", action="store_true",
-                    help="overlapped frames also replay ICP/integrate/raycast as a graph (kfx_set_graph_mode 2)")
+    ap.add_argument("--traffic-c3", default=os.path.join(ROOT, "profiles", "r05_c3_pmc.json"),
+                    help="PMC record of the C3 workload (attached to c3_record under the same rule)")
+    ap.add_argument("--traffic-c5", default=os.path.join(ROOT, "profiles", "r05_c5_pmc.json"),
+                    help="PMC record of the C5 single-volume workload (attached to c5_record under the same rule)")
+    ap.add_argument("--graph", choices=["auto", "0", "1", "2"], default="auto",
+                    help="kfx_set_graph_mode of the timed frames: 0 eager, 1 the pyrDown+preprocess graph, 2 also "
+                         "ICP+integrate+raycast (+RCCL combine) as a graph; auto: 2 for C5 (BASELINE names a "
+                         "hipGraph-captured per-frame pipeline there), 1 otherwise")
+    ap.add_argument("--no-graph", action="store_true", help="= --graph 0")
+    ap.add_argument("--graph-full", action="store_true", help="= --graph 2")
     ap.add_argument("--sample-every", type=int, default=8,
                     help="time kernels on every k-th timed frame with HIP events (0 = off)")
     ap.add_argument("--no-overlap", action="store_true",
@@ -263,17 +270,30 @@ CONFIGS = {  # BASELINE.json configs[1..4]: (width, height, volume dims, volume 
 }
 
 
-def graph_parts(a, mode, effective=None):
+def graph_mode(a, cfg):
+    """kfx_set_graph_mode for a stream of config cfg (--graph; auto: 2 for C5,
+    whose BASELINE config names a hipGraph-captured per-frame pipeline)."""
+    if a.no_graph:
+        return 0
+    if a.graph_full:
+        return 2
+    if a.graph != "auto":
+        return int(a.graph)
+    return 2 if cfg == "c5" else 1
+
+
+def graph_parts(a, mode, effective=None, requested=1):
     """The part of each timed frame replayed as a captured graph (effective:
     kfx_get_graph_mode after the run, lowered where RCCL refused capture)."""
-    if a.no_graph or effective == 0:
+    if requested == 0 or effective == 0:
         return "none (eager)"
     if a.no_overlap:
         return "whole frame (single stream)"
     main = "ICP+integrate+raycast" + ("+RCCL combine" if mode == "slab" else "")
-    if a.graph_full and effective in (None, 2):
-        return f"pyrDown+preprocess graph and {main} graph"
-    return f"pyrDown+preprocess graph; {main} eager" + (" (RCCL refused capture)" if a.graph_full else "")
+    if requested == 2 and effective in (None, 2):
+        return f"pyrDown+preprocess graph and {main} graph (mode 2)"
+    return f"pyrDown+preprocess graph; {main} eager (mode 1)" + (
+        " (mode 2 requested: capture refused, fell back)" if requested == 2 else "")
 
 
 def resolve(a, world):
@@ -315,9 +335,10 @@ def workload_text(name, W, H, n, L, mode, world, icp_ar, cuts="balanced"):
     return t
 
 
-def run_stream(a, intr, params, frames, D, local, slab=None, icp_ar=False, timing=True):
+def run_stream(a, intr, params, frames, D, local, slab=None, icp_ar=False, timing=True, gmode=1):
     """Create a context, warm up, time a.steps staged frames (W/K contract).
-    Returns the open context and the timed-region record; the caller closes it."""
+    Returns the open context and the timed-region record; the caller closes it.
+    gmode: kfx_set_graph_mode of the timed frames (graph_mode)."""
     import kfx
     from kfx.abi import Intrinsics
     bgr, dep, order, gt = frames  # gt: the trajectory's poses (slab cut calibration), or None
@@ -334,7 +355,7 @@ def run_stream(a, intr, params, frames, D, local, slab=None, icp_ar=False, timin
     if slab is not None:
         kf.comm_init(D.bcast_bytes(kfx.comm_unique_id() if slab[0] == 0 else None))
         kf.set_icp_allreduce(icp_ar)
-    kf.set_graph_mode(0 if a.no_graph else (2 if a.graph_full else 1))
+    kf.set_graph_mode(gmode)
     kf.set_frame_overlap(not a.no_overlap)
     kf.stage_frames(bgr, dep)
     for i in range(a.warmup):
@@ -353,7 +374,8 @@ def run_stream(a, intr, params, frames, D, local, slab=None, icp_ar=False, timin
         raise SystemExit(f"bench: {a.steps - tracked} of {a.steps} timed frames were not tracked")
     if ktime is not None and not ktime["samples"]:
         ktime = None
-    return kf, {"elapsed": elapsed, "ktime": ktime, "tracked": tracked, "graph_mode": kf.graph_mode()}
+    return kf, {"elapsed": elapsed, "ktime": ktime, "tracked": tracked, "graph_mode": kf.graph_mode(),
+                "graph_requested": gmode}
 
 
 def balanced_cuts(intr, params, calib, local, world):
@@ -421,22 +443,63 @@ def round_ms(d):
     return {k: round(v, 4) if isinstance(v, float) else v for k, v in d.items()} if d else None
 
 
-def single_record(a, name, intr, n, L, frames, D, local):
-    """A side measurement of one more single-GPU config (C3 at N=1): frames/s
-    over the same W/K contract, kernel ms, integrate roofline."""
+def pmc_record(path, workload, steps, warmup, lib_hash):
+    """A committed rocprofv3 PMC record (tools/prof.sh + tools/traffic.py
+    --commit) for this workload [dims, W, H] and step counts, measured on this
+    very library (sha256): (traffic bytes per integrate launch, raycast bytes,
+    SQ issue records, source text), or Nones with the reason."""
+    try:
+        rec = json.load(open(path))
+    except (OSError, ValueError):
+        return None, None, None, None
+    same_run = (rec.get("workload") == list(workload) and rec.get("steps") == steps and rec.get("warmup") == warmup)
+    rel = os.path.relpath(path, ROOT)
+    if same_run and rec.get("lib_sha256") == lib_hash:
+        sq = {"integrate": rec.get("integrate_sq"), "raycast": rec.get("raycast_sq")}
+        src = (f"{rel}: {rec.get('command')} ({rec.get('regime')}); "
+               f"libkfx.so sha256 {lib_hash[:16]} (commit {rec.get('commit')})")
+        return rec.get("hbm_bytes_per_launch"), rec.get("raycast_hbm_bytes_per_launch"), sq, src
+    if same_run:
+        return None, None, None, (f"none: {rel} was measured on libkfx.so sha256 {str(rec.get('lib_sha256'))[:16]}, "
+                                  f"this run loaded {str(lib_hash)[:16]}")
+    return None, None, None, None
+
+
+def issue_figures(sq, kernel):
+    q = (sq or {}).get(kernel)
+    if not q:
+        return None
+    return {k: q.get(k) for k in ("valu_issue_frac_2cyc", "valu_active_frac", "valu_insts_per_wave",
+                                  "wave_cycles_split", "kernel_cycles")}
+
+
+def single_record(a, name, intr, n, L, frames, D, local, traffic_path=None):
+    """A side measurement of one more single-GPU config (C3 / C5 at N=1):
+    frames/s over the same W/K contract, kernel ms, integrate roofline (with
+    the PMC traffic of a committed record of this workload and library)."""
+    import kfx
     from kfx.abi import default_params
     params = default_params(dims=n, range_m=L)
-    kf, r = run_stream(a, intr, params, frames, D, local)
+    gm = graph_mode(a, name)
+    kf, r = run_stream(a, intr, params, frames, D, local, gmode=gm)
     wk = kf.integrate_stats()
     kf.close()
     kt = r["ktime"]
     W, H = intr.width, intr.height
+    lib_hash = file_sha256(kfx.LIB_PATH)
+    traffic, _, sq, src = pmc_record(traffic_path, [n, W, H], a.steps, a.warmup, lib_hash) if traffic_path else (
+        None, None, None, None)
+    roof = integrate_roofline(wk, kt["integrate"] if kt else float("nan"), W, H,
+                              "timed region, HIP-event-bracketed frames", traffic, src)
+    roof["lib_sha256"] = lib_hash
+    if issue_figures(sq, "integrate"):
+        roof["issue"] = issue_figures(sq, "integrate")
     return {"config": workload_text(name, W, H, n, L, "single", 1, False),
+            "graph": graph_parts(a, "single", r["graph_mode"], r["graph_requested"]),
             "value": round(a.steps / r["elapsed"], 3), "unit": "frames/s",
             "ms_per_step": round(1000.0 * r["elapsed"] / a.steps, 4), "steps": a.steps, "warmup": a.warmup,
             "tracked_frames": r["tracked"], "timed_region_kernel_ms": round_ms(kt), "integrate_voxels": wk,
-            "roofline": integrate_roofline(wk, kt["integrate"] if kt else float("nan"), W, H,
-                                           "timed region, HIP-event-bracketed frames")}
+            "roofline": roof}
 
 
 def main():
@@ -471,7 +534,7 @@ def main():
     # Z-slab stream still leaves a measured line
     replicas = None
     if mode == "slab" and world > 1 and a.replicas:
-        kf, r = run_stream(a, intr, params, frames, D, local, timing=False)
+        kf, r = run_stream(a, intr, params, frames, D, local, timing=False, gmode=graph_mode(a, name))
         kf.close()
         replicas = {"value": round(a.steps * world / r["elapsed"], 3), "unit": "frames/s", "scaling": "weak",
                     "ms_per_step": round(1000.0 * r["elapsed"] / a.steps, 4),
@@ -538,7 +601,7 @@ def main():
         b.steps = a.c3_frames
         W3, H3, n3, L3 = CONFIGS["c3"]
         f3 = (bgr, dep, synth.ping_pong(len(bgr), b.warmup + b.steps), None)
-        out["c3_record"] = single_record(b, "c3", intr, n3, L3, f3, D, local)
+        out["c3_record"] = single_record(b, "c3", intr, n3, L3, f3, D, local, a.traffic_c3)
     # N=1: the C5 single volume (1280x720, 2048^3 @ 2 mm), the N=1 point of the
     # zslab curve the driver's N>1 runs record
     if world == 1 and mode == "single" and a.c5_frames and name == "c2":
@@ -550,7 +613,7 @@ def main():
         u5 = 16
         bgr5, dep5, _ = synth.sequence(u5, i5, L=L5, noise=True, traj_seed=7, dropout=0.005)
         f5 = (bgr5, dep5.astype(np.float32), synth.ping_pong(u5, b.warmup + b.steps), None)
-        out["c5_record"] = single_record(b, "c5", i5, n5, L5, f5, D, local)
+        out["c5_record"] = single_record(b, "c5", i5, n5, L5, f5, D, local, a.traffic_c5)
         del bgr5, dep5, f5
     emit(out)
     D.close()
@@ -590,7 +653,8 @@ def zslab_record(a, intr, frames, D, rank, world, local, icp_ar, geom):
         unique = 16 if W * H > 640 * 480 else 48
         bgr, dep, gt = synth.sequence(unique, zintr, L=L, noise=True, traj_seed=7, dropout=0.005)
         zframes = (bgr, dep.astype(np.float32), synth.ping_pong(unique, a.warmup + a.steps), gt)
-    kf, r = run_stream(a, zintr, params, zframes, D, local, slab=(rank, world), icp_ar=icp_ar)
+    kf, r = run_stream(a, zintr, params, zframes, D, local, slab=(rank, world), icp_ar=icp_ar,
+                       gmode=graph_mode(a, a.zslab))
     kt = r["ktime"] or {}
     work = kf.integrate_stats()
     zb, zn, o0, o1 = kf.slab_info()
@@ -602,7 +666,7 @@ def zslab_record(a, intr, frames, D, rank, world, local, icp_ar, geom):
                  "combine_ms": round(x[3], 4), "integrate_updated": int(x[4]), "owned_slices": int(x[5]),
                  "stored_slices": int(x[6])} for k, x in enumerate(rows)]
     return {"workload": workload_text(a.zslab, W, H, n, L, "slab", world, icp_ar, a.cuts),
-            "graph": graph_parts(a, "slab", r["graph_mode"]),
+            "graph": graph_parts(a, "slab", r["graph_mode"], r["graph_requested"]),
             "value": round(a.steps / r["elapsed"], 3), "unit": "frames/s", "scaling": "strong",
             "ms_per_step": round(1000.0 * r["elapsed"] / a.steps, 4), "steps": a.steps, "warmup": a.warmup,
             "tracked_frames": int(r["tracked"]), "per_rank": per_rank,
@@ -627,7 +691,7 @@ def measure_main(a, name, intr, params, frames, D, rank, world, local, mode, icp
     W, H = intr.width, intr.height
     n, L = params.volu_dims[0], params.volu_range[0]
     slab = (rank, world) if mode == "slab" else None
-    kf, r = run_stream(a, intr, params, frames, D, local, slab=slab, icp_ar=icp_ar)
+    kf, r = run_stream(a, intr, params, frames, D, local, slab=slab, icp_ar=icp_ar, gmode=graph_mode(a, name))
     elapsed, ktime, tracked, gmode = r["elapsed"], r["ktime"], r["tracked"], r["graph_mode"]
     ms_source = (f"timed region, {ktime['samples']} HIP-event-bracketed frames" if ktime else "profiled frames")
 
@@ -712,23 +776,9 @@ def measure_main(a, name, intr, params, frames, D, rank, world, local, mode, icp
     # record (tools/prof.sh), attached only when that record was measured on
     # this workload with the same step counts (the same saturation regime)
     # and on the very library this process loaded (sha256 of libkfx.so)
-    traffic, traffic_src, ray_traffic, sq = None, None, None, None
     lib_hash = file_sha256(kfx.LIB_PATH)
-    try:
-        rec = json.load(open(a.traffic))
-        same_run = (mode == "single" and rec.get("workload") == [n, W, H] and rec.get("steps") == a.steps
-                    and rec.get("warmup") == a.warmup)
-        if same_run and rec.get("lib_sha256") == lib_hash:
-            traffic = rec.get("hbm_bytes_per_launch")
-            ray_traffic = rec.get("raycast_hbm_bytes_per_launch")
-            sq = {"integrate": rec.get("integrate_sq"), "raycast": rec.get("raycast_sq")}
-            traffic_src = (f"{os.path.relpath(a.traffic, ROOT)}: {rec.get('command')} ({rec.get('regime')}); "
-                           f"libkfx.so sha256 {lib_hash[:16]} (commit {rec.get('commit')})")
-        elif same_run:
-            traffic_src = (f"none: {os.path.relpath(a.traffic, ROOT)} was measured on libkfx.so sha256 "
-                           f"{str(rec.get('lib_sha256'))[:16]}, this run loaded {str(lib_hash)[:16]}")
-    except (OSError, ValueError):
-        pass
+    traffic, ray_traffic, sq, traffic_src = (None, None, None, None) if mode != "single" else pmc_record(
+        a.traffic, [n, W, H], a.steps, a.warmup, lib_hash)
     if mode == "slab":
         # the critical path is the slowest rank's integrate
         k = max(range(len(per_rank)), key=lambda q: per_rank[q]["integrate_ms"])
@@ -738,10 +788,8 @@ def measure_main(a, name, intr, params, frames, D, rank, world, local, mode, icp
     else:
         roof = integrate_roofline(work, int_launch_ms, W, H, ms_source, traffic, traffic_src)
         roof["lib_sha256"] = lib_hash
-        if sq and sq.get("integrate"):
-            q = sq["integrate"]
-            roof["issue"] = {k: q.get(k) for k in ("valu_issue_frac_2cyc", "valu_active_frac", "valu_insts_per_wave",
-                                                   "wave_cycles_split", "kernel_cycles")}
+        if issue_figures(sq, "integrate"):
+            roof["issue"] = issue_figures(sq, "integrate")
 
     cpu = c1 = None
     if rank == 0 and world == 1 and a.cpu_frames > 0:
@@ -760,7 +808,7 @@ def measure_main(a, name, intr, params, frames, D, rank, world, local, mode, icp
         "frames_unique": len(bgr),
         # what the timed frames replay as graphs (kfx_set_graph_mode); the few
         # stage-timing sample frames launch eagerly with their events
-        "graph": graph_parts(a, mode, gmode), "overlap": not a.no_overlap,
+        "graph": graph_parts(a, mode, gmode, r["graph_requested"]), "overlap": not a.no_overlap,
         "parallelism": (f"zslab x{world}" + (" + icp allreduce" if icp_ar else "") if mode == "slab" else
                         (f"replicas x{world} (independent streams)" if world > 1 else "single")),
         "collective": ("RCCL: raycast combine per frame" + (" + ICP partials per iteration" if icp_ar else "")

@@ -27,6 +27,9 @@
 #ifndef KFX_RAY_KR
 #define KFX_RAY_KR 14  // raycast: samples per batch (loads in flight per lane)
 #endif
+#ifndef KFX_RAY_PROBES
+#define KFX_RAY_PROBES 0  // raycast skip lookups: brick-map probes ahead along the ray per round trip
+#endif
 #ifndef KFX_INT_OCC
 #define KFX_INT_OCC 8  // integrate: waves per SIMD the register budget is sized for
 #endif
@@ -1905,6 +1908,7 @@ __device__ __forceinline__ float box_limit(int B, int bx, int by, int nbx, int n
 
 #ifdef KFX_RAY_TRACE
 constexpr bool kTrace = true;
+__device__ unsigned long long *g_ray_iter;  // per-wave iteration records (34 u64 per wave)
 #else
 constexpr bool kTrace = false;
 #endif
@@ -1922,6 +1926,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((kSlab || !
   unsigned long long t_march = 0, t_norm = 0, t_ndone = 0;
   // wave iterations of the march loop by live-lane count: 1 | 2-4 | 5-16 | 17-64
   unsigned long long t_hist = 0;
+  // per march-loop iteration (first 16): {lookup-phase cycles << 32 | batch-phase
+  // cycles}, {live lanes | lookups << 8 | max replayed samples << 16}
+  unsigned long long *t_it = g_ray_iter ? g_ray_iter + 34 * ((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) : nullptr;
+  int t_nit = 0;
 #endif
   // cam2vol = volume_pose^-1 * pose, Rinv = R^T (tsdf_volume.cpp:59-61; D: transpose)
   __shared__ DevPose s_c2v;
@@ -2078,6 +2086,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((kSlab || !
     const f3 idv = {1.f / fabsf(dv.x), 1.f / fabsf(dv.y), 1.f / fabsf(dv.z)};
     const float rstep = 1.f / rc.step;
     const bool can_skip = !isnan(dv.x + dv.y + dv.z);
+    // Probes ahead (KFX_RAY_PROBES): a dilated-clear brick at a point q of the
+    // ray clears every sample within Chebyshev distance 7.5 voxels of q (its
+    // nearest voxel then lies in q's brick or a neighbour, all holding no
+    // negative tsdf).  Probe k sits pm * k samples ahead, pm = floor(7.3 /
+    // max |dv|): with the accumulated rounding (< 0.1 voxel within skip_cap
+    // samples) every sample within pm of a probe stays within 7.4 voxels of it,
+    // so a run of clear probes 0..j (probe 0: the current brick) clears samples
+    // 1 .. (j + 1) pm.  All probe words load in the lookup's round trip: a ray
+    // crossing the dilated zone of a surface (where the 3x3-brick box of the
+    // current brick exits after 8-16 voxels of lateral travel) covers up to
+    // (K + 1) pm samples per lookup instead.
+    constexpr int kP = KFX_RAY_PROBES;
+    const int pm = kP > 0 ? (int)(7.3f / fmaxf(fabsf(dv.x), fmaxf(fabsf(dv.y), fabsf(dv.z)))) : 0;
+    const f3 pstep = scl(dv, (float)pm);
     if (kStats || kTrace) st_rays += live ? 1u : 0u;
 #ifdef KFX_RAY_TRACE
     t_march = wall_clock64();
@@ -2085,10 +2107,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((kSlab || !
     while (__any(live || cand)) {
     while (__any(live)) {
 #ifdef KFX_RAY_TRACE
-      {
-        const int nl = __popcll(__ballot(live));
-        t_hist += 1ull << (nl <= 1 ? 0 : (nl <= 4 ? 16 : (nl <= 16 ? 32 : 48)));
-      }
+      const unsigned long long t_i0 = __builtin_amdgcn_s_memtime();
+      unsigned t_lk = 0, t_mx = 0;
+      const int t_nl = __popcll(__ballot(live));
+      t_hist += 1ull << (t_nl <= 1 ? 0 : (t_nl <= 4 ? 16 : (t_nl <= 16 ? 32 : 48)));
 #endif
       if (kSlab && live && kbase > kb) {  // pass-1 bound: samples < kbase examined, no owned event
         live = false;
@@ -2103,12 +2125,43 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((kSlab || !
           const int lbz = min(max((iz >> 3) - v.bz0, 0), v.nbz - 1);
           const int sx = min(max(ix >> 5, 0), v.stx - 1), sy = min(max(iy >> 5, 0), v.sty - 1);
           const int lsz = min(max((iz >> 5) - v.sz0, 0), v.nsz - 1);
-          // both map words in flight together (one round trip per step)
+          // both map words and the probes' words in flight together (one round trip per step)
           const unsigned long long bwd = v.bocc[(size_t)(by * v.tiles_x + bx) * v.bw + (lbz >> 6)];
           const uint32_t swd = v.socc[(size_t)(sy * v.stx + sx) * v.sw + (lsz >> 5)];
+          // probe k: the byte of its brick's map bit (byte loads: one VGPR per
+          // probe; the bits' positions in their bytes packed 3 bits each)
+          uint32_t pw[kP > 0 ? kP : 1];
+          static_assert(kP <= 21, "probe bit positions: 3 bits each in 64");
+          unsigned long long pbits = 0ull;
+          if (kP > 0) {
+            const __amdgpu_buffer_rsrc_t bo = make_rsrc(v.bocc, (unsigned)v.bocc_bytes());
+#pragma unroll
+            for (int k = 0; k < kP; ++k) {
+              const float qx = fmaf((float)(k + 1), pstep.x, cx), qy = fmaf((float)(k + 1), pstep.y, cy),
+                          qz = fmaf((float)(k + 1), pstep.z, cz);
+              const int px = min(max((int)floorf(qx) >> 3, 0), v.tiles_x - 1);
+              const int py = min(max((int)floorf(qy) >> 3, 0), v.tiles_y - 1);
+              const int pz = min(max(((int)floorf(qz) >> 3) - v.bz0, 0), v.nbz - 1);
+              const unsigned off = ((unsigned)__umul24((unsigned)py, (unsigned)v.tiles_x) + (unsigned)px) *
+                                       (unsigned)(8 * v.bw) + ((unsigned)pz >> 3);
+              pw[k] = __builtin_amdgcn_raw_buffer_load_b8(bo, off, 0, 0);
+              pbits |= (unsigned long long)(pz & 7) << (3 * k);
+            }
+          }
           const int bb = lbz & 63, sb = lsz & 31;
           float lim = 0.f;
-          if (!((bwd >> bb) & 1ull)) {  // brick clear: its 3x3 tile box, dilated z run
+          const bool bclear = !((bwd >> bb) & 1ull);
+          if (kP > 0 && bclear) {  // the probes' run of clear bricks
+            int j = 0;
+            bool run = true;
+#pragma unroll
+            for (int k = 0; k < kP; ++k) {
+              run = run && !((pw[k] >> (unsigned)((pbits >> (3 * k)) & 7ull)) & 1u);
+              j += run ? 1 : 0;
+            }
+            lim = (float)((j + 1) * pm);
+          }
+          if (bclear) {  // brick clear: its 3x3 tile box, dilated z run
             float zl = -kInf, zh = kInf;
             if (dv.z > 0.f) {
               const unsigned long long up = bwd >> bb;
@@ -2119,7 +2172,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((kSlab || !
               const int bot = lbz - (dn ? __builtin_clzll(dn) : bb + 1) + 1;
               if (bot > 0) zl = (float)(8 * (bot + v.bz0) - 8);
             }
-            lim = box_limit(8, bx, by, v.tiles_x, v.tiles_y, zl, zh, cx, cy, cz, dv, idv);
+            lim = fmaxf(lim, box_limit(8, bx, by, v.tiles_x, v.tiles_y, zl, zh, cx, cy, cz, dv, idv));
           }
           if (!((swd >> sb) & 1u)) {  // super-brick clear: the same over 32^3 cells
             float zl = -kInf, zh = kInf;
@@ -2151,6 +2204,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((kSlab || !
             st_lookups += 1;
             st_skipped += (unsigned)n;
           }
+#ifdef KFX_RAY_TRACE
+          t_lk += 1;
+          t_mx += (unsigned)n;
+#endif
           // replay: packed adds {x, y} and {z, ray_len} (the per-element IEEE
           // adds of the reference); the first nf samples provably stay below
           // tfar (2 steps of margin over the accumulated rounding)
@@ -2199,6 +2256,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((kSlab || !
           pend = kbase;
         }
       }
+#ifdef KFX_RAY_TRACE
+      const unsigned long long t_i1 = __builtin_amdgcn_s_memtime();
+#endif
       if (!__any(live)) break;
       int16_t raw[kR];
       unsigned pm = 0u, nm = 0u, am = 0u, ownm = 0u;
@@ -2314,6 +2374,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((kSlab || !
       }
       ray_len = rl;
       kbase += kR;
+#ifdef KFX_RAY_TRACE
+      {
+        const unsigned long long t_i2 = __builtin_amdgcn_s_memtime();
+        unsigned lk = t_lk, mx = t_mx;
+        for (int off = 32; off > 0; off >>= 1) {
+          lk = max(lk, (unsigned)__shfl_xor((int)lk, off));
+          mx = max(mx, (unsigned)__shfl_xor((int)mx, off));
+        }
+        if (t_it && lane == 0 && t_nit < 16) {
+          t_it[2 + 2 * t_nit] = ((t_i1 - t_i0) << 32) | (t_i2 - t_i1);
+          t_it[3 + 2 * t_nit] = (unsigned long long)t_nl | ((unsigned long long)min(lk, 255u) << 8) |
+                                ((unsigned long long)mx << 16);
+        }
+        ++t_nit;
+      }
+#endif
     }
     if (kStats) st_cand += cand ? 1u : 0u;
 #ifdef KFX_RAY_TRACE
@@ -2367,6 +2443,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((kSlab || !
       r[5] = t_norm;
       r[6] = t_ndone;
       r[7] = t_hist;
+      if (t_it) t_it[0] = (unsigned long long)t_nit;
     }
   }
 #endif
@@ -3448,8 +3525,17 @@ void launch_integrate(hipStream_t s, VolView v, LevelGeom g0, const float2 *dl0,
 
 #ifdef KFX_RAY_TRACE
 static unsigned long long *g_ray_trace = nullptr;
+static unsigned long long *g_ray_iter_host = nullptr;
 static int g_ray_trace_waves = 0;
 }  // namespace kfx
+// debug build only: the last raycast launch's per-wave iteration records (34 u64 per wave)
+extern "C" int kfx_debug_raycast_iters(unsigned long long *out, int cap) {
+  const int n = std::min(cap, kfx::g_ray_trace_waves);
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpy(out, kfx::g_ray_iter_host, sizeof(unsigned long long) * 34 * n, hipMemcpyDeviceToHost) != hipSuccess)
+    return -1;
+  return n;
+}
 // debug build only: the last raycast launch's per-wave records
 extern "C" int kfx_debug_raycast_trace(unsigned long long *out, int cap) {
   const int n = std::min(cap, kfx::g_ray_trace_waves);
@@ -3466,7 +3552,13 @@ void launch_raycast(hipStream_t s, VolView v, int levels, const LevelGeom *g, Fr
   const bool want_stats = stats != nullptr;
 #ifdef KFX_RAY_TRACE
   if (!stats) {
-    if (!g_ray_trace) (void)hipMalloc(&g_ray_trace, sizeof(unsigned long long) * 8 * (1 << 16));
+    if (!g_ray_trace) {
+      (void)hipMalloc(&g_ray_trace, sizeof(unsigned long long) * 8 * (1 << 16));
+      unsigned long long *it = nullptr;
+      (void)hipMalloc(&it, sizeof(unsigned long long) * 34 * (1 << 16));
+      (void)hipMemcpyToSymbol(HIP_SYMBOL(g_ray_iter), &it, sizeof(it));
+      g_ray_iter_host = it;
+    }
     g_ray_trace_waves = (int)(((g[0].w + 15) / 16) * ((g[0].h + 15) / 16) * 4);
     stats = g_ray_trace;
   }

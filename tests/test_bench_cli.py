@@ -161,7 +161,7 @@ def test_run_stream_plumbing_without_gpu(monkeypatch):
         bcast_bytes = staticmethod(lambda x: b"")
 
     params = types.SimpleNamespace(volu_dims=[64, 64, 64])
-    a = types.SimpleNamespace(cuts="balanced", warmup=2, steps=6, no_graph=False, graph_full=False, no_overlap=False,
+    a = types.SimpleNamespace(cuts="balanced", warmup=2, steps=6, no_graph=False, graph_full=False, no_overlap=False, graph="auto",
                               sample_every=0)
     n = 8
     frames = ([None] * n, [None] * n, list(range(n)) + list(range(n)), [np.eye(4)] * n)
@@ -177,3 +177,43 @@ def test_run_stream_plumbing_without_gpu(monkeypatch):
         created = [c for c in _FakeKF.calls if c[0] == "create" and c[1] == slab]
         assert created[-1][2] == ([0, 32, 64] if want else None)
         assert r["tracked"] == a.steps and r["graph_mode"] == 1
+
+
+def test_c5_defaults_to_the_captured_frame_graph(monkeypatch):
+    """BASELINE C5 names a hipGraph-captured per-frame pipeline: every C5
+    stream (the N>1 zslab record, --config c5, the N=1 c5_record) requests
+    graph mode 2 (ICP + integrate + raycast (+ RCCL combine) captured) by
+    default; other configs the preprocess graph; --graph / --no-graph /
+    --graph-full override.  The record names the mode that ran."""
+    b = load_bench()
+    monkeypatch.setattr(sys, "argv", ["bench.py"])
+    a = b.parse()
+    assert a.graph == "auto"
+    assert b.graph_mode(a, "c5") == 2
+    assert [b.graph_mode(a, c) for c in ("c2", "c3", "c4", "custom")] == [1, 1, 1, 1]
+    for argv, want in ((["--graph", "0"], 0), (["--no-graph"], 0), (["--graph-full"], 2), (["--graph", "1"], 1)):
+        monkeypatch.setattr(sys, "argv", ["bench.py"] + argv)
+        assert b.graph_mode(b.parse(), "c5") == want, argv
+    a.no_overlap = False
+    assert b.graph_parts(a, "slab", 2, 2).endswith("graph (mode 2)") and "RCCL combine" in b.graph_parts(a, "slab", 2, 2)
+    assert "fell back" in b.graph_parts(a, "slab", 1, 2)
+    assert b.graph_parts(a, "single", 0, 0) == "none (eager)"
+
+
+def test_pmc_record_attached_only_to_its_workload_and_library(tmp_path):
+    """The C3 / C5 records carry PMC traffic only from a record of the same
+    workload, step counts and libkfx.so (sha256)."""
+    import json
+    b = load_bench()
+    rec = {"workload": [1024, 640, 480], "steps": 20, "warmup": 5, "lib_sha256": "ab" * 32,
+           "hbm_bytes_per_launch": 123, "raycast_hbm_bytes_per_launch": 45, "command": "x", "regime": "y",
+           "integrate_sq": {"valu_issue_frac_2cyc": 0.4}}
+    p = tmp_path / "c3.json"
+    p.write_text(json.dumps(rec))
+    t, rt, sq, src = b.pmc_record(str(p), [1024, 640, 480], 20, 5, "ab" * 32)
+    assert (t, rt) == (123, 45) and sq["integrate"]["valu_issue_frac_2cyc"] == 0.4 and "sha256" in src
+    assert b.issue_figures(sq, "integrate")["valu_issue_frac_2cyc"] == 0.4
+    t, _, _, src = b.pmc_record(str(p), [1024, 640, 480], 20, 5, "cd" * 32)
+    assert t is None and src.startswith("none:")
+    assert b.pmc_record(str(p), [2048, 1280, 720], 10, 5, "ab" * 32) == (None, None, None, None)
+    assert b.pmc_record(str(tmp_path / "missing.json"), [1024, 640, 480], 20, 5, "ab" * 32)[0] is None

@@ -59,4 +59,33 @@ print(f"  slowest 2% of waves: {h[slow20].sum(0).tolist()}  iterations med {np.m
 print(f"  median waves: iterations med {np.median(tot):.0f}")
 slow = np.argsort(dur)[-8:]
 print("slowest waves: dur us / lookups / batches / live hist", [(round(dur[i] / 1e3, 1), int(lk[i]), int(bt[i]), h[i].tolist()) for i in slow])
+try:
+    ib = (C.c_uint64 * (34 * 65536))()
+    ni = lib.kfx_debug_raycast_iters(ib, 65536)
+    it = np.frombuffer(ib, dtype=np.uint64)[: 34 * ni].reshape(ni, 34).astype(np.int64)
+    valid = np.frombuffer(buf, dtype=np.uint64)[: 8 * n].reshape(n, 8)[:, 1] > 0
+    it = it[:n][valid]
+    print("per-iteration records of the 8 slowest waves (lookup-phase us / batch-phase us / live / lookups / replayed max-lane samples):")
+    for i in slow:
+        k = int(it[i, 0])
+        rows = []
+        for j in range(min(k, 16)):
+            a, b = int(it[i, 2 + 2 * j]), int(it[i, 3 + 2 * j])
+            rows.append((round((a >> 32) / 2400, 2), round((a & 0xffffffff) / 2400, 2), b & 0xff, (b >> 8) & 0xff, b >> 16))
+        tot = sum(((int(it[i, 2 + 2 * j]) >> 32) + (int(it[i, 2 + 2 * j]) & 0xffffffff)) for j in range(min(k, 16)))
+        print(f"    (clock check: {tot} cycles over the march phase's {tn[i] / 1e3:.1f} us = {tot / max(tn[i], 1) * 1e3:.0f} MHz)")
+        print(f"  wave {i}: dur {dur[i] / 1e3:.1f} us, setup {tm[i] / 1e3:.1f} us, {k} iterations:", rows)
+    # all waves: mean cycles per lookup and per batch phase
+    lk_c, bt_c, nlk = [], [], []
+    for i in range(len(it)):
+        for j in range(min(int(it[i, 0]), 16)):
+            a, b = int(it[i, 2 + 2 * j]), int(it[i, 3 + 2 * j])
+            nl = (b >> 8) & 0xff
+            if nl:
+                lk_c.append((a >> 32) / nl)
+            bt_c.append(a & 0xffffffff)
+    print(f"all waves: lookup round (per lookup) us med {np.median(lk_c) / 2400:.2f} p90 {np.percentile(lk_c, 90) / 2400:.2f};"
+          f" batch phase us med {np.median(bt_c) / 2400:.2f} p90 {np.percentile(bt_c, 90) / 2400:.2f}")
+except AttributeError:
+    print("(library without kfx_debug_raycast_iters)")
 kf.close()

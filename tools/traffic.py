@@ -82,16 +82,24 @@ def main():
 
             def arg(name, default):
                 return int(args[args.index(name) + 1]) if name in args else default
-            steps, warmup, dims = arg("--steps", 300), arg("--warmup", 20), arg("--dims", 512)
+            steps, warmup = arg("--steps", 300), arg("--warmup", 20)
+            # the workload [dims, W, H] of the named config (bench.py CONFIGS), --dims overriding
+            cfg = args[args.index("--config") + 1] if "--config" in args else "c2"
+            W, H, dims = {"c2": (640, 480, 512), "c3": (640, 480, 1024), "c4": (640, 480, 1024),
+                          "c5": (1280, 720, 2048)}.get(cfg, (640, 480, 512))
+            dims = arg("--dims", dims)
             r = max(integ, key=lambda r: r["dispatches"])
-            ray = [rr for k, rr in out["kernels"].items() if k.startswith("k_raycast<true, false, false>")]
+            # the single-volume raycast (32- or 64-bit index), not a slab or stats variant
+            ray = sorted([rr for k, rr in out["kernels"].items() if k.startswith("k_raycast<") and
+                          k.endswith(", false, false>") and "hbm_bytes_per_launch" in rr],
+                         key=lambda rr: -rr["dispatches"])
             lib = os.environ.get("KFX_LIB_PATH") or os.path.join(REPO, "slam-kinectfusion_amd", "lib", "libkfx.so")
             rec = {"kernel": "k_integrate", "hbm_bytes_per_launch": int(r["hbm_bytes_per_launch"]),
                    "read_bytes": int(r["read_bytes"]), "write_bytes": int(r["write_bytes"]),
                    "dispatches": r["dispatches"], "factor_units_per_byte": fac,
                    "raycast_hbm_bytes_per_launch": int(ray[0]["hbm_bytes_per_launch"]) if ray and
                    "hbm_bytes_per_launch" in ray[0] else None,
-                   "workload": [dims, 640, 480], "steps": steps, "warmup": warmup,
+                   "workload": [dims, W, H], "steps": steps, "warmup": warmup,
                    "command": "python3 bench.py " + " ".join(args),
                    "regime": ("mean over every dispatch of the run: %d warm-up + %d timed + profiled "
                               "frames%s" % (warmup, steps, " (unsaturated transient: < 64 frames)"
@@ -101,8 +109,9 @@ def main():
                    # record only to a run that loaded the same file
                    "lib": os.path.relpath(lib, REPO), "lib_sha256": sha256(lib),
                    "commit": os.environ.get("KFX_COMMIT")}
-            for pre, name in (("k_integrate<false, true", "integrate_sq"), ("k_raycast<true, false, false>", "raycast_sq")):
-                ks = [k for k in sq if k.startswith(pre)]
+            for pre, name in (("k_integrate<false,", "integrate_sq"), ("k_raycast<", "raycast_sq")):
+                ks = sorted([k for k in sq if k.startswith(pre) and (name != "raycast_sq" or k.endswith(", false, false>"))],
+                            key=lambda k: -sq[k].get("dispatches", 0))
                 if ks:
                     rec[name] = sq_issue(sq[ks[0]])
             name = os.environ.get("PMC_RECORD", "r04_integrate_pmc.json")
