@@ -1025,10 +1025,13 @@ static int create_impl(const kfx_intrinsics *intr, const kfx_params *params, int
   if ((r = dalloc(c, (void **)&c->raw0_u16, np0 * 2))) return fail(r);
   if ((r = dalloc(c, (void **)&c->bgr, np0 * 3))) return fail(r);
   if ((r = dalloc(c, (void **)&c->inv_lambda, np0 * 4))) return fail(r);
-  // {depth, 1/lambda} per pixel + 16 max-depth shards
+  // {depth, 1/lambda} per pixel + 16 max-depth shards + the 16x16-pixel max-depth grid
+  const size_t grid16 = (size_t)((intr->width + 15) / 16) * ((intr->height + 15) / 16);
   for (float2 *&d : c->dl0b)
-    if ((r = dalloc(c, (void **)&d, np0 * 8 + 64))) return fail(r);
+    if ((r = dalloc(c, (void **)&d, np0 * 8 + 64 + grid16 * 4))) return fail(r);
   c->vol = make_vol(p, rank, world, cuts);
+  // raycast wave durations of the last frame (4 waves per 16x16 block; zeroed: no hint)
+  if ((r = dalloc(c, (void **)&c->vol.rdur, grid16 * 4 * sizeof(unsigned)))) return fail(r);
   const size_t n = nvox(c);
   {
     // tsdf and weight in ONE allocation, weight (u8) at a fixed offset (2 MiB-

@@ -37,6 +37,10 @@ struct DevState {
   int debug_stall;      // test hook: block 0 withholds its first ICP arrival (kfx_debug_force_icp_stall)
   DevPose *log;         // the device pose log (the host keeps it current)
   DevPose back;         // log[n_poses - 1] at frame begin: the frame pose's base, one load away
+  // the frame's raycast pose, written by k_integrate (block 0) before the raycast
+  // runs: kind (frame_kind) and cam2vol = volume_pose^-1 * pose (tsdf_volume.cpp:59)
+  int ray_kind;
+  DevPose ray_c2v;
 };
 
 struct LevelGeom {
@@ -126,6 +130,7 @@ struct VolView {
   int inchunk;
   int iadapt;  // length-capped chunks + longest-first order (deep volumes), else geometric chunks
   int force64;  // kfx_debug_force_index64: integrate / raycast take the 64-bit-index kernels at any size
+  unsigned *rdur;  // raycast: each wave's duration in the last frame (1024-cycle units; issue priority hint)
   __host__ __device__ size_t bocc_bytes() const { return (size_t)tiles_x * tiles_y * bw * 8; }
   __host__ __device__ size_t socc_bytes() const { return (size_t)stx * sty * sw * 4; }
   __host__ __device__ size_t local_voxels() const { return slice * (size_t)zn; }

@@ -27,6 +27,14 @@
 #ifndef KFX_RAY_KR
 #define KFX_RAY_KR 14  // raycast: samples per batch (loads in flight per lane)
 #endif
+#ifndef KFX_RAY_HINT
+// raycast: waves whose tile was slow in the last frame (frames are temporally
+// coherent) take a higher issue priority (s_setprio) while all waves compete
+#define KFX_RAY_HINT 0
+#endif
+#ifndef KFX_RAY_HINT_T0
+#define KFX_RAY_HINT_T0 80  // priority thresholds, 1024-cycle units of last frame's wave duration
+#endif
 #ifndef KFX_RAY_PROBES
 #define KFX_RAY_PROBES 0  // raycast skip lookups: brick-map probes ahead along the ray per round trip
 #endif
@@ -72,6 +80,7 @@ constexpr int kShortMax = 32767;               // device_utils.cuh:7
 constexpr int kMaxWeight = 64;                 // device_utils.cuh:5 (A10)
 constexpr float kFixHalf = 65536.0f;           // ICP fixed point 2^32 (D) = 2^16 per factor of a product
 constexpr int kDmaxShards = 16;
+constexpr float kInfF = __builtin_huge_valf();
 
 struct f3 {
   float x, y, z;
@@ -218,6 +227,12 @@ __device__ __forceinline__ void frame_begin(DevState *st) {
 // the frame's max-depth shards live after the level-0 dl table (one per cur buffer)
 __device__ __forceinline__ unsigned *dmax_shards(const float2 *dl0, const LevelGeom &g0) {
   return (unsigned *)(const_cast<float2 *>(dl0) + (size_t)g0.w * g0.h);
+}
+// ... followed by the max-depth grid: the largest valid level-0 depth (m, as
+// float bits; 0: none) of each 16x16-pixel block (k_preprocess_maps), the
+// integrate occlusion clip's input (int_tile_clip; the allocation: kfx_api.hip dl0b)
+__device__ __forceinline__ unsigned *dmax_grid(const float2 *dl0, const LevelGeom &g0) {
+  return dmax_shards(dl0, g0) + kDmaxShards;
 }
 
 // z is the global slice; the view stores slices [zb, zb+zn) (tile-column
@@ -508,6 +523,7 @@ __global__ __launch_bounds__(256) void k_preprocess_maps(BilatArgs a) {
     if (threadIdx.x == 0) {
       const unsigned b = max(max(wm[0], wm[1]), max(wm[2], wm[3]));
       if (b) atomicMax(&dmax_shards(a.dl0, a.t.g[0])[blockIdx.x % kDmaxShards], b);
+      dmax_grid(a.dl0, a.t.g[0])[local] = b;  // this 16x16 block's cell (level-0 blocks are row-major)
     }
   }
 }
@@ -1425,6 +1441,86 @@ __device__ __forceinline__ void int_column(const VolView &v, const LevelGeom &g,
   }
 }
 
+// Occlusion clip of a column tile's intervals (KFX_INT_OCCL).  A voxel can
+// only be updated where its pixel's depth d satisfies d - il |vc| >= -trunc
+// (tsdf_volume.cu:67-71), and il |vc| >= vc.z / 1.0011 for every in-image
+// voxel, so no voxel with vc.z > (D + trunc) * 1.0011 is updated when D bounds
+// the depth of every pixel it can project to.  The lanes' segments (linear vc
+// model, as int_column) project into a pixel box; with 2 pixels of margin it
+// covers every rounded projection, and when it spans at most kOcclCells cells
+// of the frame's 16x16-pixel max-depth grid, D = their max replaces the
+// frame-wide maximum in the far clip (the same form as int_column's).  Voxels
+// behind every surface they project onto (a far Z-slab, the space behind a
+// sphere) are then not visited at all; the result is unchanged (only voxels
+// that cannot pass are dropped).  Lanes' [zl, zh] and the union [wl, wh] are
+// tightened in place (wave-uniform control flow).
+#ifndef KFX_INT_OCCL
+#define KFX_INT_OCCL 1
+#endif
+#ifndef KFX_INT_OCCL_CELLS
+#define KFX_INT_OCCL_CELLS 16
+#endif
+constexpr int kOcclCells = KFX_INT_OCCL_CELLS;
+__device__ __forceinline__ void int_tile_clip(const VolView &v, const LevelGeom &g, const float2 *dl, f3 vc0, f3 zs,
+                                              int lane, int &zl, int &zh, int &wl, int &wh) {
+  if (!KFX_INT_OCCL || wh < wl) return;
+  const bool own = zl <= zh;
+  float umin = kInfF, umax = -kInfF, vmin = kInfF, vmax = -kInfF;
+  bool bad = false;
+  if (own) {
+    const float z1 = (float)zl, z2 = (float)zh;
+    const float pz1 = vc0.z + z1 * zs.z, pz2 = vc0.z + z2 * zs.z;
+    bad = !(pz1 > 1e-3f) || !(pz2 > 1e-3f);
+    const float i1 = __builtin_amdgcn_rcpf(pz1), i2 = __builtin_amdgcn_rcpf(pz2);
+    const float u1 = g.fx * ((vc0.x + z1 * zs.x) * i1) + g.cx, u2 = g.fx * ((vc0.x + z2 * zs.x) * i2) + g.cx;
+    const float w1 = g.fy * ((vc0.y + z1 * zs.y) * i1) + g.cy, w2 = g.fy * ((vc0.y + z2 * zs.y) * i2) + g.cy;
+    umin = fminf(u1, u2);
+    umax = fmaxf(u1, u2);
+    vmin = fminf(w1, w2);
+    vmax = fmaxf(w1, w2);
+    bad = bad || isnan(umin + umax + vmin + vmax);
+  }
+  if (__any(bad)) return;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    umin = fminf(umin, __shfl_xor(umin, off));
+    umax = fmaxf(umax, __shfl_xor(umax, off));
+    vmin = fminf(vmin, __shfl_xor(vmin, off));
+    vmax = fmaxf(vmax, __shfl_xor(vmax, off));
+  }
+  const int nbx = (g.w + 15) >> 4, nby = (g.h + 15) >> 4;
+  // the box's cells, clamped to the image (margin: 2 px over the rounding)
+  const float fu0 = fmaxf(umin - 2.5f, 0.f), fu1 = fminf(umax + 2.5f, (float)(g.w - 1));
+  const float fv0 = fmaxf(vmin - 2.5f, 0.f), fv1 = fminf(vmax + 2.5f, (float)(g.h - 1));
+  if (!(fu0 <= fu1) || !(fv0 <= fv1)) return;  // (the frustum clip already handles boxes off the image)
+  const int cx0 = (int)fu0 >> 4, cx1 = (int)fu1 >> 4, cy0 = (int)fv0 >> 4, cy1 = (int)fv1 >> 4;
+  const int nx = cx1 - cx0 + 1, ncell = nx * (cy1 - cy0 + 1);
+  if (ncell > kOcclCells) return;  // a large footprint: the frame-wide bound stands
+  unsigned dm = 0u;
+  if (lane < ncell) dm = dmax_grid(dl, g)[(cy0 + lane / nx) * nbx + cx0 + lane % nx];
+  (void)nby;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) dm = max(dm, (unsigned)__shfl_xor((int)dm, off));
+  const float zfar = (__uint_as_float(dm) + v.trunc) * 1.02f + 0.01f;
+  if (own) {
+    float lo = (float)zl, hi = (float)zh;
+    clip_lin(zfar - vc0.z, -zs.z, lo, hi);
+    if (hi >= lo) {
+      zh = min(zh, (int)ceilf(hi) + 2);
+    } else {
+      zl = INT_MAX;
+      zh = INT_MIN;
+    }
+  }
+  wl = zl;
+  wh = zh;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    wl = min(wl, __shfl_xor(wl, off));
+    wh = max(wh, __shfl_xor(wh, off));
+  }
+}
+
 // Chunk `chunk` of the wave-uniform union interval [wl, wh] (wl <= wh):
 // [za, zb], or false when this item has no chunk (length-capped mode).
 __device__ __forceinline__ bool int_chunk(const VolView &v, int chunkr, int chunk, int nchunk, int wl, int wh,
@@ -1487,7 +1583,14 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
         gp = frame_pose(st, log, kind);
         s_pose = pose_mul(pose_inv(gp), vpose);  // tsdf_volume.cpp:50
       }
-      if (!kCount && blockIdx.x == 0) frame_bookkeeping(st, log, kind, gp);
+      if (!kCount && blockIdx.x == 0) {
+        frame_bookkeeping(st, log, kind, gp);
+        // the raycast after this integrate reads its pose from here (no
+        // per-block pose math or LDS round trip on its critical path);
+        // frame_kind / frame_pose read fields the bookkeeping leaves alone
+        st->ray_kind = kind;
+        if (kind == 1) st->ray_c2v = pose_mul(pose_inv(vpose), gp);  // tsdf_volume.cpp:59
+      }
     }
   }
   __syncthreads();
@@ -1535,6 +1638,7 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
     wl = min(wl, __shfl_xor(wl, off));
     wh = max(wh, __shfl_xor(wh, off));
   }
+  int_tile_clip(v, g, dl, vc, zs, lane, zl, zh, wl, wh);
   // the next frame's dispatch order (k_int_order) from this interval length
   if (!kCount && chunk == 0 && lane == 0 && v.iwork) v.iwork[tile] = wh >= wl ? (unsigned)(wh - wl + 1) : 0u;
   if (wh < wl || !int_chunk(v, KFX_INT_CHUNKR, chunk, nchunk, wl, wh, za, zb)) return;  // wave-uniform
@@ -1836,8 +1940,76 @@ __device__ __forceinline__ float interp32(const VolView &v, __amdgpu_buffer_rsrc
   return s;
 }
 
+// The 6 trilinear interpolations of compute_normal (kIdx32 volumes) with the
+// loads of kG interpolations in flight together (KFX_RAY_NG: 1 = one round trip
+// per interpolation, 6 = all 48 corner loads in one): the same corners,
+// weights and sum order as interp32.
+#ifndef KFX_RAY_NG
+#define KFX_RAY_NG 1
+#endif
+template <int kG>
+__device__ __forceinline__ f3 compute_normal_g(const VolView &v, const RayConsts &rc, f3 p) {
+  const __amdgpu_buffer_rsrc_t t = make_rsrc(v.tsdf, (unsigned)(2 * v.local_voxels()));
+  const unsigned col = (unsigned)v.zn << 6;
+  float f[6];
+#pragma unroll
+  for (int g0 = 0; g0 < 6; g0 += kG) {
+    int16_t raw[kG][8];
+    bool ok[kG];
+#pragma unroll
+    for (int q = 0; q < kG; ++q) {
+      const int k = g0 + q, ax = k >> 1;
+      const float sgn = (k & 1) ? -1.f : 1.f;
+      const f3 pq = {ax == 0 ? p.x + sgn * rc.gd.x : p.x, ax == 1 ? p.y + sgn * rc.gd.y : p.y,
+                     ax == 2 ? p.z + sgn * rc.gd.z : p.z};
+      const f3 cf = mulc(pq, rc.vs_inv);
+      const int gx = f2i_rd(cf.x), gy = f2i_rd(cf.y), gz = f2i_rd(cf.z);
+      ok[q] = !(gx < 0 || gx >= v.X - 1 || gy < 0 || gy >= v.Y - 1 || gz < 0 || gz >= v.Z - 1) &&
+              (unsigned)(gz - v.zb) < (unsigned)(v.zn - 1);
+      const unsigned tile = __umul24((unsigned)gy >> 3, (unsigned)v.tiles_x) + ((unsigned)gx >> 3);
+      const unsigned i0 = ok[q] ? (((tile * (unsigned)v.zn + (unsigned)(gz - v.zb)) << 6) |
+                                   (((unsigned)gy & 7u) << 3 | ((unsigned)gx & 7u)))
+                                : 0u;
+      const unsigned dx = (gx & 7) == 7 ? col - 7u : 1u;
+      const unsigned dy = (gy & 7) == 7 ? __umul24((unsigned)v.tiles_x, col) - 56u : 8u;
+      const unsigned o[8] = {i0, i0 + 64u, i0 + dy, i0 + dy + 64u, i0 + dx, i0 + dx + 64u, i0 + dx + dy,
+                             i0 + dx + dy + 64u};
+#pragma unroll
+      for (int c = 0; c < 8; ++c)
+        raw[q][c] = ok[q] ? (int16_t)__builtin_amdgcn_raw_buffer_load_b16(t, o[c] << 1, 0, 0) : (int16_t)0;
+    }
+#pragma unroll
+    for (int q = 0; q < kG; ++q) {
+      const int k = g0 + q, ax = k >> 1;
+      const float sgn = (k & 1) ? -1.f : 1.f;
+      const f3 pq = {ax == 0 ? p.x + sgn * rc.gd.x : p.x, ax == 1 ? p.y + sgn * rc.gd.y : p.y,
+                     ax == 2 ? p.z + sgn * rc.gd.z : p.z};
+      const f3 cf = mulc(pq, rc.vs_inv);
+      const int gx = f2i_rd(cf.x), gy = f2i_rd(cf.y), gz = f2i_rd(cf.z);
+      const float a = cf.x - (float)gx, b = cf.y - (float)gy, c = cf.z - (float)gz;
+      auto T = [&](int i) { return (float)raw[q][i] * kDivShortMax; };
+      float s = 0.f;
+      s += T(0) * (1 - a) * (1 - b) * (1 - c);
+      s += T(1) * (1 - a) * (1 - b) * c;
+      s += T(2) * (1 - a) * b * (1 - c);
+      s += T(3) * (1 - a) * b * c;
+      s += T(4) * a * (1 - b) * (1 - c);
+      s += T(5) * a * (1 - b) * c;
+      s += T(6) * a * b * (1 - c);
+      s += T(7) * a * b * c;
+      f[k] = ok[q] ? s : NAN;
+    }
+  }
+  f3 n;
+  n.x = (f[0] - f[1]) / rc.gd.x;
+  n.y = (f[2] - f[3]) / rc.gd.y;
+  n.z = (f[4] - f[5]) / rc.gd.z;
+  return normalized(n);
+}
+
 template <bool kIdx32 = false>
 __device__ f3 compute_normal(const VolView &v, const RayConsts &rc, f3 p) {
+  if constexpr (kIdx32 && KFX_RAY_NG > 1) return compute_normal_g<KFX_RAY_NG>(v, rc, p);
   const __amdgpu_buffer_rsrc_t t = make_rsrc(v.tsdf, kIdx32 ? (unsigned)(2 * v.local_voxels()) : 0u);
   auto ip = [&](f3 q) { return kIdx32 ? interp32(v, t, mulc(q, rc.vs_inv)) : interp(v, mulc(q, rc.vs_inv)); };
   f3 n;
@@ -1931,28 +2103,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((kSlab || !
   unsigned long long *t_it = g_ray_iter ? g_ray_iter + 34 * ((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) : nullptr;
   int t_nit = 0;
 #endif
-  // cam2vol = volume_pose^-1 * pose, Rinv = R^T (tsdf_volume.cpp:59-61; D: transpose)
-  __shared__ DevPose s_c2v;
-  __shared__ float s_rinv[9];
-  __shared__ int s_kind;
-  if (threadIdx.x == 0) {
-    if (xpose) {  // stage seam: explicit cam2vol and Rinv
-      s_kind = 1;
-      for (int i = 0; i < 9; ++i) s_c2v.R[i] = xpose[i];
-      for (int i = 0; i < 3; ++i) s_c2v.t[i] = xpose[9 + i];
-      for (int i = 0; i < 9; ++i) s_rinv[i] = xpose[12 + i];
-    } else {
-      const int kind = frame_kind(st);
-      s_kind = kind;
-      if (kind == 1) {
-        const DevPose c2v = pose_mul(pose_inv(vpose), frame_pose(st, log, kind));
-        s_c2v = c2v;
-        for (int i = 0; i < 3; ++i)
-          for (int j = 0; j < 3; ++j) s_rinv[3 * i + j] = c2v.R[3 * j + i];
-      }
-    }
+  // cam2vol = volume_pose^-1 * pose, Rinv = R^T (tsdf_volume.cpp:59-61; D:
+  // transpose), computed once per frame by k_integrate (DevState::ray_c2v) and
+  // read here by every wave with scalar loads: no per-block pose math, LDS
+  // round trip or barrier before the march.  Stage seam: explicit cam2vol and
+  // Rinv in xpose.
+  const float *pose_src = xpose ? xpose : st->ray_c2v.R;  // R[9], t[3] (+ Rinv[9] in xpose)
+  const int skind = xpose ? 1 : st->ray_kind;
+  const size_t wave_id = (size_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const unsigned long long t_wave0 = KFX_RAY_HINT ? __builtin_amdgcn_s_memtime() : 0ull;
+  if (KFX_RAY_HINT && !kSlab && !kStats && v.rdur) {
+    const unsigned d = __builtin_amdgcn_readfirstlane(v.rdur[wave_id]);
+    if (d >= KFX_RAY_HINT_T0 * 7 / 4) __builtin_amdgcn_s_setprio(3);
+    else if (d >= KFX_RAY_HINT_T0 * 11 / 8) __builtin_amdgcn_s_setprio(2);
+    else if (d >= KFX_RAY_HINT_T0) __builtin_amdgcn_s_setprio(1);
   }
-  __syncthreads();
   const LevelGeom g = ra.g[0];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int nbx = (g.w + 15) / 16;
@@ -1962,7 +2127,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((kSlab || !
   const int x = tx0 + lx, y = ty0 + ly;
   const bool inimg = x < g.w && y < g.h;
   const size_t o = (size_t)y * g.w + x;
-  const int kind = s_kind;
+  const int kind = skind;
   f3 vout = {0.f, 0.f, 0.f}, nout = {0.f, 0.f, 0.f};
   uint32_t key = kind == 0 ? 0u : UINT_MAX;  // kSlab: sample index of the decisive event
   uint32_t pend = UINT_MAX;  // kSlab pass 1: first sample not examined (march stopped at the bound)
@@ -1982,7 +2147,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((kSlab || !
     nout = ld3(cur.n[0], o);
   }
   if (kind == 1) {  // block-uniform
-    const DevPose P = s_c2v;
+    DevPose P;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) (i < 9 ? P.R[i] : P.t[i - 9]) = pose_src[i];
     const f3 org = {P.t[0], P.t[1], P.t[2]};
     float da[3];
     ray_dir(P.R, g, x, y, da);
@@ -2399,14 +2566,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((kSlab || !
       cand = false;
       const f3 n = compute_normal<kIdx32 && KFX_RAY_N32>(v, rc, cvert);
       if (!isnan(n.x * n.y * n.z)) {
-        // Rinv re-read from LDS here (volatile LDS reads: not held in
-        // registers through the march; a generic volatile pointer would
-        // become serialised flat loads)
+        // Rinv read here (scalar loads of the uniform pose; the transpose of
+        // cam2vol's R, or the stage seam's explicit Rinv)
         float ri[9];
-        const volatile __attribute__((address_space(3))) float *vr =
-            (const volatile __attribute__((address_space(3))) float *)s_rinv;
 #pragma unroll
-        for (int q = 0; q < 9; ++q) ri[q] = vr[q];
+        for (int q = 0; q < 9; ++q) ri[q] = xpose ? xpose[12 + q] : pose_src[3 * (q % 3) + q / 3];
         nout = rmul(ri, n);
         vout = rmul(ri, sub(cvert, org));
         key = ckey;
@@ -2457,6 +2621,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((kSlab || !
     }
     return;
   }
+  if (KFX_RAY_HINT && !kSlab && !kStats && v.rdur && (threadIdx.x & 63) == 0)
+    v.rdur[wave_id] = (unsigned)((__builtin_amdgcn_s_memtime() - t_wave0) >> 10);
   if (act) {
     if (kSlab) {  // key, pend + payload {Ts, nout} (kfx_internal.h slab combine)
       const size_t np = (size_t)g.w * g.h;
@@ -3758,6 +3924,7 @@ __global__ __launch_bounds__(256) void k_slice_work(VolView v, LevelGeom g, cons
       wl = min(wl, __shfl_xor(wl, off));
       wh = max(wh, __shfl_xor(wh, off));
     }
+    int_tile_clip(v, g, dl, c0, zs, lane, zl, zh, wl, wh);  // what k_integrate visits
     if (wl <= wh) {
       if (lane == 0) {
         atomicAdd(&lh[wl], 64);
