@@ -30,10 +30,10 @@
 #ifndef KFX_RAY_HINT
 // raycast: waves whose tile was slow in the last frame (frames are temporally
 // coherent) take a higher issue priority (s_setprio) while all waves compete
-#define KFX_RAY_HINT 0
+#define KFX_RAY_HINT 1
 #endif
 #ifndef KFX_RAY_HINT_T0
-#define KFX_RAY_HINT_T0 80  // priority thresholds, 1024-cycle units of last frame's wave duration
+#define KFX_RAY_HINT_T0 70  // priority thresholds, 1024-cycle units of last frame's wave duration
 #endif
 #ifndef KFX_RAY_PROBES
 #define KFX_RAY_PROBES 0  // raycast skip lookups: brick-map probes ahead along the ray per round trip
@@ -877,9 +877,20 @@ __global__ __launch_bounds__(kIcpThreads, KFX_ICP_MINB) void k_icp_track(IcpPlan
     constexpr bool stride = kStride;
     f3 n0[kIcpPix], v0[kIcpPix];
     bool ok[kIcpPix];
-    if (mine && !stride)
-      icp_load_cur(g, pl.xe[l], pl.npix[l], KFX_ICP_XCD ? xcd_remap(blockIdx.x, pl.groups[l]) : (int)blockIdx.x,
-                   pl.ppl[l], pl.cv[l], pl.cn[l], n0, v0, ok);
+    // a level with span[l] > 0 in the plain kernel (IcpPlan::span, CU-uniform
+    // level 0): this block's contiguous range of at most kIcpPix pixels per
+    // lane, held in registers like a group
+    int lppl = pl.ppl[l];
+    if (mine && !stride) {
+      const int r = KFX_ICP_XCD ? xcd_remap(blockIdx.x, pl.groups[l]) : (int)blockIdx.x;
+      if (pl.span[l] > 0) {
+        const int b0 = r * pl.span[l], b1 = min(pl.npix[l], b0 + pl.span[l]);
+        lppl = min(kIcpPix, (b1 - b0 + kIcpThreads - 1) / kIcpThreads);
+        icp_load_cur(g, pl.xe[l], b1, 0, lppl, pl.cv[l], pl.cn[l], n0, v0, ok, b0);
+      } else {
+        icp_load_cur(g, pl.xe[l], pl.npix[l], r, lppl, pl.cv[l], pl.cn[l], n0, v0, ok);
+      }
+    }
     for (int it = 0; it < pl.iters[l] && !fail; ++it, ++slot) {
       unsigned long long *sh = sy->sums + (size_t)slot * kIcpShards * 27;
       target += min(pl.groups[l], (int)gridDim.x);  // arrivals: the blocks with a group
@@ -921,7 +932,7 @@ __global__ __launch_bounds__(kIcpThreads, KFX_ICP_MINB) void k_icp_track(IcpPlan
           }
         } else {
           double acc[27];
-          icp_lane(g, P, n0, v0, ok, pl.ppl[l], pl.pv[l], pl.pn[l], pl.dist2_max, pl.sine2_max, acc);
+          icp_lane(g, P, n0, v0, ok, lppl, pl.pv[l], pl.pn[l], pl.dist2_max, pl.sine2_max, acc);
           if (tr && blockIdx.x == 0) sy->trace[slot][8] = wall_clock64() + (acc[3] == -1.5 ? 1 : 0);
           bsum = icp_block_reduce(red, acc);
         }
@@ -1458,7 +1469,7 @@ __device__ __forceinline__ void int_column(const VolView &v, const LevelGeom &g,
 #define KFX_INT_OCCL 1
 #endif
 #ifndef KFX_INT_OCCL_CELLS
-#define KFX_INT_OCCL_CELLS 16
+#define KFX_INT_OCCL_CELLS 64
 #endif
 constexpr int kOcclCells = KFX_INT_OCCL_CELLS;
 __device__ __forceinline__ void int_tile_clip(const VolView &v, const LevelGeom &g, const float2 *dl, f3 vc0, f3 zs,
@@ -3493,7 +3504,9 @@ bool icp_persistent_ok(IcpPlan &pl, int device) {
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
     return false;
   pl.stride = 0;
-  if ((long long)per_cu * cus >= pl.nblocks) return true;
+  if ((long long)per_cu * cus >= pl.nblocks) {
+    return true;
+  }
   // too many groups to be co-resident: the strided kernel on the blocks that are
   int per_cu_s = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_s, k_icp_track<true>, kIcpThreads, 0) != hipSuccess)
