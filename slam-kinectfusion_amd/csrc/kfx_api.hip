@@ -1995,6 +1995,7 @@ int kfx_get_extract_ms(kfx_ctx *c, float out_ms[3]) {
 // for a count-only call (cap = 0), with kfx_set_extract_passes(2), or when
 // the buffers cannot be allocated: the caller then runs the two-pass path.
 // per = floats per item (3 per point, 9 per triangle).
+constexpr int64_t kExtractPoolItems = (int64_t)1 << 23;  // single-pass pool: <= 8.4 M items (100 MB of points)
 static int extract_single_pass(kfx_ctx *c, const uint8_t *tab, int zlo, int zhi, float *host, int64_t cap,
                                int per, int64_t *total_out) {
   if (cap <= 0 || cap > (int64_t)1 << 36 || c->extract_mode == 2) return 0;
@@ -2006,12 +2007,14 @@ static int extract_single_pass(kfx_ctx *c, const uint8_t *tab, int zlo, int zhi,
                o_at = o_misc + 256, o_list = o_at + al(waves * 8), wsb = o_list + al(waves * 4);
   char *ws = nullptr;
   float *pool = nullptr, *dout = nullptr;
-  const size_t ibytes = (size_t)cap * per * sizeof(float);
-  if (hipMalloc(&ws, wsb) != hipSuccess || hipMalloc(&pool, ibytes) != hipSuccess ||
-      hipMalloc(&dout, ibytes) != hipSuccess) {
+  // the unordered pool holds at most kExtractPoolItems items whatever the
+  // caller's cap (a larger result overflows it and takes the emit pass: the
+  // counts are complete either way); the ordered output is allocated once
+  // the count is known (n = min(total, cap) items, not cap)
+  const int64_t pool_cap = std::min<int64_t>(cap, kExtractPoolItems);
+  if (hipMalloc(&ws, wsb) != hipSuccess || hipMalloc(&pool, (size_t)pool_cap * per * sizeof(float)) != hipSuccess) {
     (void)hipGetLastError();
     if (ws) (void)hipFree(ws);
-    if (pool) (void)hipFree(pool);
     return 0;
   }
   unsigned *counts = (unsigned *)ws;
@@ -2026,7 +2029,7 @@ static int extract_single_pass(kfx_ctx *c, const uint8_t *tab, int zlo, int zhi,
   if (e == hipSuccess && extract_events(c) == KFX_OK) {
     (void)hipEventRecord(c->xev[0], c->stream);
     launch_extract_pool(c->stream, c->vol, vp, zlo, zhi, tab, counts, misc + 1, pool_at, list, pool,
-                        (unsigned long long)cap, (unsigned *)(misc + 2));
+                        (unsigned long long)pool_cap, (unsigned *)(misc + 2));
     (void)hipEventRecord(c->xev[1], c->stream);
     launch_scan(c->stream, counts, offsets, bsum, waves, misc);
     (void)hipEventRecord(c->xev[2], c->stream);
@@ -2036,6 +2039,7 @@ static int extract_single_pass(kfx_ctx *c, const uint8_t *tab, int zlo, int zhi,
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     const int64_t total = (int64_t)h[0], n = std::min<int64_t>(total, cap);
     const bool ovf = (unsigned)h[2] != 0;
+    if (e == hipSuccess && n > 0) e = hipMalloc(&dout, (size_t)n * per * sizeof(float));
     if (e == hipSuccess && n > 0) {
       (void)hipEventRecord(c->xev[3], c->stream);
       if (!ovf)
@@ -2061,7 +2065,7 @@ static int extract_single_pass(kfx_ctx *c, const uint8_t *tab, int zlo, int zhi,
     }
   }
   (void)hipGetLastError();
-  (void)hipFree(dout);
+  if (dout) (void)hipFree(dout);
   (void)hipFree(pool);
   (void)hipFree(ws);
   return done;

@@ -35,9 +35,6 @@
 #ifndef KFX_RAY_HINT_T0
 #define KFX_RAY_HINT_T0 70  // priority thresholds, 1024-cycle units of last frame's wave duration
 #endif
-#ifndef KFX_RAY_PROBES
-#define KFX_RAY_PROBES 0  // raycast skip lookups: brick-map probes ahead along the ray per round trip
-#endif
 #ifndef KFX_INT_OCC
 #define KFX_INT_OCC 8  // integrate: waves per SIMD the register budget is sized for
 #endif
@@ -64,6 +61,9 @@
 #endif
 #ifndef KFX_INT_MAXCHUNK
 #define KFX_INT_MAXCHUNK 8  // integrate: most z-chunks per column tile
+#endif
+#ifndef KFX_INT_SLAB_CHUNK
+#define KFX_INT_SLAB_CHUNK 128  // integrate, Z-slab contexts: chunks of at most about this many slices
 #endif
 #ifndef KFX_FF_MIN
 #define KFX_FF_MIN 768  // fast-forward replays of at least this many adds (shorter ones: the adds; A/B r3m: 384 costs C2 +8 %)
@@ -2264,20 +2264,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((kSlab || !
     const f3 idv = {1.f / fabsf(dv.x), 1.f / fabsf(dv.y), 1.f / fabsf(dv.z)};
     const float rstep = 1.f / rc.step;
     const bool can_skip = !isnan(dv.x + dv.y + dv.z);
-    // Probes ahead (KFX_RAY_PROBES): a dilated-clear brick at a point q of the
-    // ray clears every sample within Chebyshev distance 7.5 voxels of q (its
-    // nearest voxel then lies in q's brick or a neighbour, all holding no
-    // negative tsdf).  Probe k sits pm * k samples ahead, pm = floor(7.3 /
-    // max |dv|): with the accumulated rounding (< 0.1 voxel within skip_cap
-    // samples) every sample within pm of a probe stays within 7.4 voxels of it,
-    // so a run of clear probes 0..j (probe 0: the current brick) clears samples
-    // 1 .. (j + 1) pm.  All probe words load in the lookup's round trip: a ray
-    // crossing the dilated zone of a surface (where the 3x3-brick box of the
-    // current brick exits after 8-16 voxels of lateral travel) covers up to
-    // (K + 1) pm samples per lookup instead.
-    constexpr int kP = KFX_RAY_PROBES;
-    const int pm = kP > 0 ? (int)(7.3f / fmaxf(fabsf(dv.x), fmaxf(fabsf(dv.y), fabsf(dv.z)))) : 0;
-    const f3 pstep = scl(dv, (float)pm);
     if (kStats || kTrace) st_rays += live ? 1u : 0u;
 #ifdef KFX_RAY_TRACE
     t_march = wall_clock64();
@@ -2306,64 +2292,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((kSlab || !
           // both map words and the probes' words in flight together (one round trip per step)
           const unsigned long long bwd = v.bocc[(size_t)(by * v.tiles_x + bx) * v.bw + (lbz >> 6)];
           const uint32_t swd = v.socc[(size_t)(sy * v.stx + sx) * v.sw + (lsz >> 5)];
-          // probe k: the byte of its brick's map bit (byte loads: one VGPR per
-          // probe; the bits' positions in their bytes packed 3 bits each)
-          uint32_t pw[kP > 0 ? kP : 1];
-          static_assert(kP <= 21, "probe bit positions: 3 bits each in 64");
-          unsigned long long pbits = 0ull;
-          if (kP > 0) {
-            const __amdgpu_buffer_rsrc_t bo = make_rsrc(v.bocc, (unsigned)v.bocc_bytes());
-#pragma unroll
-            for (int k = 0; k < kP; ++k) {
-              const float qx = fmaf((float)(k + 1), pstep.x, cx), qy = fmaf((float)(k + 1), pstep.y, cy),
-                          qz = fmaf((float)(k + 1), pstep.z, cz);
-              const int px = min(max((int)floorf(qx) >> 3, 0), v.tiles_x - 1);
-              const int py = min(max((int)floorf(qy) >> 3, 0), v.tiles_y - 1);
-              const int pz = min(max(((int)floorf(qz) >> 3) - v.bz0, 0), v.nbz - 1);
-              const unsigned off = ((unsigned)__umul24((unsigned)py, (unsigned)v.tiles_x) + (unsigned)px) *
-                                       (unsigned)(8 * v.bw) + ((unsigned)pz >> 3);
-              pw[k] = __builtin_amdgcn_raw_buffer_load_b8(bo, off, 0, 0);
-              pbits |= (unsigned long long)(pz & 7) << (3 * k);
-            }
-          }
           const int bb = lbz & 63, sb = lsz & 31;
+          const bool sclear = !((swd >> sb) & 1u), bclear = !((bwd >> bb) & 1ull);
           float lim = 0.f;
-          const bool bclear = !((bwd >> bb) & 1ull);
-          if (kP > 0 && bclear) {  // the probes' run of clear bricks
-            int j = 0;
-            bool run = true;
-#pragma unroll
-            for (int k = 0; k < kP; ++k) {
-              run = run && !((pw[k] >> (unsigned)((pbits >> (3 * k)) & 7ull)) & 1u);
-              j += run ? 1 : 0;
-            }
-            lim = (float)((j + 1) * pm);
-          }
-          if (bclear) {  // brick clear: its 3x3 tile box, dilated z run
+          if (sclear || bclear) {
+            // One box per lookup: the super-brick's when its cell is clear
+            // (its 3x3 box contains the brick's laterally; tools/raysim: the
+            // brick box alone adds < 1 % of lookups there), else the brick's:
+            // the cell's 3x3 tile box with the dilated z run of clear cells
+            // in the direction of travel (the word widened to 64 bits)
+            const unsigned long long w = sclear ? (unsigned long long)swd : bwd;
+            const int nbits = sclear ? 32 : 64, b = sclear ? sb : bb, lc = sclear ? lsz : lbz;
+            const int ncell = sclear ? v.nsz : v.nbz, c0 = sclear ? v.sz0 : v.bz0, B = sclear ? 32 : 8;
             float zl = -kInf, zh = kInf;
             if (dv.z > 0.f) {
-              const unsigned long long up = bwd >> bb;
-              const int top = lbz + (up ? __builtin_ctzll(up) : 64 - bb) - 1;
-              if (top < v.nbz - 1) zh = (float)(8 * (top + v.bz0) + 15);
+              const unsigned long long up = w >> b;
+              const int top = lc + (up ? __builtin_ctzll(up) : nbits - b) - 1;
+              if (top < ncell - 1) zh = (float)(B * (top + c0) + 2 * B - 1);
             } else {
-              const unsigned long long dn = bwd << (63 - bb);
-              const int bot = lbz - (dn ? __builtin_clzll(dn) : bb + 1) + 1;
-              if (bot > 0) zl = (float)(8 * (bot + v.bz0) - 8);
+              const unsigned long long dn = w << (63 - b);
+              const int bot = lc - (dn ? __builtin_clzll(dn) : b + 1) + 1;
+              if (bot > 0) zl = (float)(B * (bot + c0) - B);
             }
-            lim = fmaxf(lim, box_limit(8, bx, by, v.tiles_x, v.tiles_y, zl, zh, cx, cy, cz, dv, idv));
-          }
-          if (!((swd >> sb) & 1u)) {  // super-brick clear: the same over 32^3 cells
-            float zl = -kInf, zh = kInf;
-            if (dv.z > 0.f) {
-              const uint32_t up = swd >> sb;
-              const int top = lsz + (up ? __builtin_ctz(up) : 32 - sb) - 1;
-              if (top < v.nsz - 1) zh = (float)(32 * (top + v.sz0) + 63);
-            } else {
-              const uint32_t dn = swd << (31 - sb);
-              const int bot = lsz - (dn ? __builtin_clz(dn) : sb + 1) + 1;
-              if (bot > 0) zl = (float)(32 * (bot + v.sz0) - 32);
-            }
-            lim = fmaxf(lim, box_limit(32, sx, sy, v.stx, v.sty, zl, zh, cx, cy, cz, dv, idv));
+            lim = box_limit(B, sclear ? sx : bx, sclear ? sy : by, sclear ? v.stx : v.tiles_x,
+                            sclear ? v.sty : v.tiles_y, zl, zh, cx, cy, cz, dv, idv);
           }
           if (!(lim >= 1.f)) {
             if (kStats) st_blocked += 1;
@@ -3609,7 +3561,18 @@ int integrate_chunks(const VolView &v) {
   const int tiles = v.tiles_x * v.tiles_y;
   if (integrate_mode(v) == 1) return std::max(1, std::min(KFX_INT_NC, v.zn / 32));  // chunks of >= 32 slices
   // z-chunks so that >= KFX_INT_WAVES waves exist (12 per SIMD on 1024 SIMDs)
-  return std::max(1, std::min(KFX_INT_MAXCHUNK, (KFX_INT_WAVES + tiles - 1) / tiles));
+  int nc = (KFX_INT_WAVES + tiles - 1) / tiles;
+  // Z-slabs (a context storing part of the volume's slices): also at most
+  // ~KFX_INT_SLAB_CHUNK slices per chunk.  A slab's waves otherwise cover its
+  // whole stored range (C4 slab 0: 344 slices, one chunk per tile: 6150
+  // working waves, 70 % of the wave slots filled at the start and a tail of
+  // 120-260 us waves, tools/slab_int_trace.py)
+  // — as long as the slab keeps <= 4 KFX_INT_WAVES waves (the chunk-start
+  // replays of many chunks cost more than the tail they cut: C5 slab 0, 772
+  // slices of 65536 tiles, took 1.25 ms in 7 chunks against 0.85 ms in one)
+  if (KFX_INT_SLAB_CHUNK > 0 && v.zn < v.Z)
+    nc = std::max(nc, std::min((v.zn + KFX_INT_SLAB_CHUNK - 1) / KFX_INT_SLAB_CHUNK, 4 * KFX_INT_WAVES / tiles));
+  return std::max(1, std::min(KFX_INT_MAXCHUNK, nc));
 }
 
 // Longest-first dispatch order of k_integrate's (tile, chunk) items for the

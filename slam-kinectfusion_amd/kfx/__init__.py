@@ -280,6 +280,12 @@ def slab_balance(slice_work, world: int) -> list:
     return list(cu)
 
 
+def _trim(out: np.ndarray, n: int) -> np.ndarray:
+    """The first n items of a cap-sized output buffer: a copy when n is well
+    below the cap (a view would keep the whole cap-sized allocation alive)."""
+    return out[:n].copy() if 2 * n < len(out) else out[:n]
+
+
 def pipeline_group(members, color: np.ndarray, depth: np.ndarray) -> int:
     """One pipeline() frame over all Z-slabs held in this process
     (members[k] = slab k of len(members))."""
@@ -509,7 +515,7 @@ class KinectFusion:
         out = np.empty((max(cap, 0), 3, 3), np.float32)
         _check(lib().kfx_extract_mesh(self._h, fptr(out) if cap > 0 else None, max(cap, 0), C.byref(n)),
                "kfx_extract_mesh")
-        return out[:min(n.value, max(cap, 0))]
+        return _trim(out, min(n.value, max(cap, 0)))
 
     # ---- point cloud (kinectfusion::extracePointcloud / savePointcloud) ---
     def extract_points(self, cap: int = 10_000_000) -> np.ndarray:
@@ -518,7 +524,7 @@ class KinectFusion:
         out = np.empty((max(cap, 0), 3), np.float32)
         _check(lib().kfx_extract_points(self._h, fptr(out) if cap > 0 else None, max(cap, 0), C.byref(n)),
                "kfx_extract_points")
-        return out[:min(n.value, max(cap, 0))]
+        return _trim(out, min(n.value, max(cap, 0)))
 
     def extract_count(self, mesh: bool = False) -> int:
         """Points (or triangles) the volume holds, without extracting them (count pass only)."""

@@ -195,12 +195,13 @@ struct Sim {
     const int sx = std::min(std::max(ix >> 5, 0), v.stx - 1), sy = std::min(std::max(iy >> 5, 0), v.sty - 1);
     const int lsz = std::min(std::max(iz >> 5, 0), v.nsz - 1);
     float lim = 0.f;
-    if (!v.bocc[v.bi(bx, by, lbz)]) {
+    const bool sclear = !v.socc[v.si(sx, sy, lsz)];
+    if (!v.bocc[v.bi(bx, by, lbz)] && !(variant == 4 && sclear)) {
       float zl, zh;
       zrun([&](int z) { return v.bocc[v.bi(bx, by, z)] != 0; }, lbz, v.nbz, 8, r.dv.z, zl, zh);
       lim = box_limit(8, bx, by, v.tx, v.ty, zl, zh, cxv, cyv, czv, r.dv, r.idv);
     }
-    if (!v.socc[v.si(sx, sy, lsz)]) {
+    if (sclear) {
       float zl, zh;
       zrun([&](int z) { return v.socc[v.si(sx, sy, z)] != 0; }, lsz, v.nsz, 32, r.dv.z, zl, zh);
       lim = fmaxf(lim, box_limit(32, sx, sy, v.stx, v.sty, zl, zh, cxv, cyv, czv, r.dv, r.idv));

@@ -41,9 +41,7 @@ lib = kfx.lib()
 print(f"{cfg} cuts {list(cuts)}")
 for r in ranks:
     m = members[r]
-    pose = Pose.from_matrix(m.pose_record[-1])
-    import oracle as O  # noqa: E402  (pose algebra only)
-    vol2cam = O.pose_mul(O.pose_inv(pose), p.volu_pose)
+    vol2cam = Pose.from_matrix(np.linalg.inv(m.pose_record[-1].astype(np.float64)) @ p.volu_pose.matrix())
     m.stage_integrate(vol2cam, counts=False)
     buf = (C.c_uint64 * (4 * (1 << 20)))()
     nw = lib.kfx_debug_integrate_trace(buf, 1 << 20)

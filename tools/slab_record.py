@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--frames", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--groups", default="equal,balanced,balanced_unbounded,calibrated",
+                    help="cut sets to time (A/B runs: e.g. calibrated)")
     a = ap.parse_args()
     import kfx
     from kfx import synth
@@ -87,7 +89,8 @@ def main():
             slabs.append({"rank": r, "owned_slices": [o0, o1], "stored_slices": [zb, zb + zn],
                           "icp_ms": k["icp"], "integrate_ms": k["integrate"], "raycast_local_ms": k["raycast_local"],
                           "combine_ms": k["combine"], "integrate_updated": w["updated"], "samples": k["samples"]})
-        assert all(np.array_equal(m.pose_record, sp) for m in members), "slab poses differ from the single volume"
+        if not os.environ.get("KFX_TIMING_ONLY"):  # (timing-only variants compute wrong values)
+            assert all(np.array_equal(m.pose_record, sp) for m in members), "slab poses differ from the single volume"
         for m in members:
             m.close()
         it = np.array([s["integrate_ms"] for s in slabs])
@@ -116,35 +119,56 @@ def main():
     # ground-truth poses (bench.py --cuts balanced: cuts for the run)
     seen = sorted(set(order[a.warmup:a.warmup + a.frames]))
     calib = [seen[int(round(j * (len(seen) - 1) / 3))] for j in range(4)]
-    cw = np.mean([probe.slice_work_at(bgr[i], dep[i], gt[i])[0] for i in calib], axis=0).round().astype(np.int64)
+    parts = [probe.slice_work_at(bgr[i], dep[i], gt[i]) for i in calib]
+    cw = np.mean([q[0] for q in parts], axis=0).round().astype(np.int64)
+    ccov = np.mean([q[1] for q in parts], axis=0)  # visited slots per slice (the occlusion-clipped intervals)
+    cupd = np.mean([q[2] for q in parts], axis=0)  # updated voxels per slice
     probe.close()
+    rec["slice_cover_calibrated"] = [float(x) for x in ccov]
+    rec["slice_updated_calibrated"] = [float(x) for x in cupd]
     rec["calibration_frames"] = [int(i) for i in calib]
     rec["slice_work_first_frame"] = [int(x) for x in work]
     rec["slice_work_calibrated"] = [int(x) for x in cw]
     rec["slice_cover_first_frame"] = [int(x) for x in cover]
     rec["slice_updated_first_frame"] = [int(x) for x in upd]
-    rec["equal_cuts"] = group(None)
-    rec["balanced_cuts"] = group(kfx.slab_balance(work, a.world))
+    gs = a.groups.split(",")
+    if "equal" in gs:
+        rec["equal_cuts"] = group(None)
+    if "balanced" in gs:
+        rec["balanced_cuts"] = group(kfx.slab_balance(work, a.world))
     # the same cuts with every slab ray marched to its end (no bound, no resume pass)
-    rec["balanced_cuts_unbounded"] = group(kfx.slab_balance(work, a.world), bound=0)
-    rec["calibrated_cuts_unbounded"] = group(kfx.slab_balance(cw, a.world), bound=0)
-    # integrate ms of a slab against its stored slices' estimated parts:
-    # ms ~ a * cover + b * updated + c (least squares over both cut sets)
-    rows, ys = [], []
-    for k in ("equal_cuts", "balanced_cuts"):
-        for sl in rec[k]["slabs"]:
+    if "balanced_unbounded" in gs:
+        rec["balanced_cuts_unbounded"] = group(kfx.slab_balance(work, a.world), bound=0)
+    if "calibrated" in gs:
+        rec["calibrated_cuts_unbounded"] = group(kfx.slab_balance(cw, a.world), bound=0)
+    # every timed slab's estimated work over its stored slices (the calibration
+    # frames' mean): the inputs of the cost fit (tools/slab_fit.py)
+    for k in ("equal_cuts", "balanced_cuts", "balanced_cuts_unbounded", "calibrated_cuts_unbounded"):
+        for sl in rec.get(k, {}).get("slabs", []):
             z0, z1 = sl["stored_slices"]
-            sl["est_cover"] = int(cover[z0:z1].sum())
-            sl["est_updated"] = int(upd[z0:z1].sum())
-            rows.append([sl["est_cover"], sl["est_updated"], 1.0])
-            ys.append(sl["integrate_ms"])
-    A = np.array(rows, np.float64)
-    coef, *_ = np.linalg.lstsq(A / A.max(axis=0), np.array(ys), rcond=None)
-    coef = coef / A.max(axis=0)
-    pred = A @ coef
-    rec["cost_fit"] = {"ms_per_cover": float(coef[0]), "ms_per_updated": float(coef[1]), "ms_const": float(coef[2]),
-                       "updated_over_cover": float(coef[1] / coef[0]) if coef[0] else None,
-                       "max_rel_err": float(np.max(np.abs(pred - ys) / np.array(ys)))}
+            sl["est_cover"] = float(ccov[z0:z1].sum())
+            sl["est_updated"] = float(cupd[z0:z1].sum())
+            sl["stored_slots"] = float(n * n * (z1 - z0))
+            # k_integrate's waves for this slab (kfx_kernels.hip integrate_chunks)
+            tiles, zn = (n // 8) ** 2, z1 - z0
+            nc = max(nc_min := (12288 + tiles - 1) // tiles, min((zn + 127) // 128, 4 * 12288 // tiles))
+            sl["waves"] = float(tiles * max(1, min(8, max(nc, nc_min))))
+    if not all(k in rec for k in ("equal_cuts", "balanced_cuts")):
+        out = a.out or os.path.join(ROOT, "gpurun_out", f"slabs_{a.config}.json")
+        os.makedirs(os.path.dirname(out), exist_ok=True)
+        json.dump(rec, open(out, "w"), indent=1)
+        for k in ("equal_cuts", "balanced_cuts", "balanced_cuts_unbounded", "calibrated_cuts_unbounded"):
+            if k in rec:
+                sl = rec[k]["slabs"]
+                print(k, "integrate ms", [round(x["integrate_ms"], 3) for x in sl], "sum",
+                      round(sum(x["integrate_ms"] for x in sl), 3), "crit",
+                      round(rec[k]["max_rank_icp_integrate_raycast_combine_ms"], 3))
+        return
+    # integrate ms of a slab against its stored slices' estimated parts
+    # (non-negative least squares, tools/slab_fit.py: this config alone)
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from slab_fit import fit
+    rec["cost_fit"] = fit([rec])
     out = a.out or os.path.join(ROOT, "gpurun_out", f"slabs_{a.config}.json")
     os.makedirs(os.path.dirname(out), exist_ok=True)
     json.dump(rec, open(out, "w"), indent=1)
