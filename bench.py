@@ -374,8 +374,9 @@ def run_stream(a, intr, params, frames, D, local, slab=None, icp_ar=False, timin
         raise SystemExit(f"bench: {a.steps - tracked} of {a.steps} timed frames were not tracked")
     if ktime is not None and not ktime["samples"]:
         ktime = None
+    note = kf.graph_note() if hasattr(kf, "graph_note") else ""
     return kf, {"elapsed": elapsed, "ktime": ktime, "tracked": tracked, "graph_mode": kf.graph_mode(),
-                "graph_requested": gmode}
+                "graph_requested": gmode, "graph_note": note}
 
 
 def balanced_cuts(intr, params, calib, local, world):
@@ -666,7 +667,8 @@ def zslab_record(a, intr, frames, D, rank, world, local, icp_ar, geom):
                  "combine_ms": round(x[3], 4), "integrate_updated": int(x[4]), "owned_slices": int(x[5]),
                  "stored_slices": int(x[6])} for k, x in enumerate(rows)]
     return {"workload": workload_text(a.zslab, W, H, n, L, "slab", world, icp_ar, a.cuts),
-            "graph": graph_parts(a, "slab", r["graph_mode"], r["graph_requested"]),
+            "graph": graph_parts(a, "slab", r["graph_mode"], r["graph_requested"]) +
+                     (f" [{r['graph_note']}]" if r.get("graph_note") else ""),
             "value": round(a.steps / r["elapsed"], 3), "unit": "frames/s", "scaling": "strong",
             "ms_per_step": round(1000.0 * r["elapsed"] / a.steps, 4), "steps": a.steps, "warmup": a.warmup,
             "tracked_frames": int(r["tracked"]), "per_rank": per_rank,

@@ -142,6 +142,9 @@ int kfx_set_graph_mode(kfx_ctx *ctx, int enabled);
  * refusing capture: 2 -> 1 for overlapped frames, 1 -> 0 for single-stream
  * frames of a communicator context). */
 int kfx_get_graph_mode(kfx_ctx *ctx, int *mode);
+/* Why graph mode 2 was lowered to 1 on this context (the RCCL / capture error
+ * text), or "" (valid until the context is destroyed). */
+const char *kfx_get_graph_note(kfx_ctx *ctx);
 /* Overlap each staged frame's preprocess with the previous frame's tracking on
  * a second stream, over double-buffered frame maps (default on; staged frames
  * then launch eagerly instead of through graphs).  Results are identical. */

@@ -152,6 +152,8 @@ struct kfx_ctx {
   bool ov_graph_full = false;  // also capture ICP/integrate/raycast (kfx_set_graph_mode 2)
   bool cap_ext = false;        // capturing: the ev_icp record becomes an event-record node
   bool ov_main_refused = false;  // the main graph's capture failed (RCCL refused capture): eager
+  hipError_t cap_err = hipSuccess;  // the last capture's HIP error (capture_graph)
+  std::string graph_note;           // why the main graph was dropped (kfx_get_graph_note)
   const uint8_t *last_bgr = nullptr;              // colour the last frame integrated
   hipEvent_t ev[kStageEvents]{};  // stage events; [5]: local raycast done, [6]: combine starts (slabs)
   float stage_ms[5]{};
@@ -219,11 +221,11 @@ int dalloc(kfx_ctx *c, void **p, size_t bytes) {
 #ifndef KFX_PREP_AFTER_ICP
 #define KFX_PREP_AFTER_ICP 1  // overlapped frames: next preprocess waits for this frame's ICP
 #endif
-#ifndef KFX_UPDATED_COST
-#define KFX_UPDATED_COST 0  // slab balancing: cost of an updated voxel over a visited slot (slice_cost)
+#ifndef KFX_COST_UPDATED
+#define KFX_COST_UPDATED 32  // slab balancing: weight of an updated voxel (64 = one visited slot; slice_cost)
 #endif
-#ifndef KFX_SLOT_DIV
-#define KFX_SLOT_DIV 40  // slab balancing: a stored voxel slot costs 1/KFX_SLOT_DIV visited slot (0: none)
+#ifndef KFX_COST_SLOT
+#define KFX_COST_SLOT 3  // slab balancing: weight of a stored voxel slot (64 = one visited slot)
 #endif
 #ifndef KFX_VOL_PAD
 #define KFX_VOL_PAD 4096  // weight offset past the 2 MiB-rounded tsdf (bytes)
@@ -537,9 +539,11 @@ int enqueue_frame_overlap(kfx_ctx *c, FrameInput in, hipEvent_t *ev, hipGraphExe
 template <typename F>
 int capture_graph(kfx_ctx *c, hipStream_t s, F &&body, hipGraphExec_t *out) {
   hipGraph_t graph = nullptr;
+  c->cap_err = hipSuccess;
   HIPCHK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
   const int r = body();
   const hipError_t ec = hipStreamEndCapture(s, &graph);
+  c->cap_err = ec;
   if (r) {
     if (graph) (void)hipGraphDestroy(graph);
     return r;
@@ -581,7 +585,14 @@ int ensure_ov_graphs(kfx_ctx *c, FrameInput in, hipGraphExec_t *gx, int p) {
     c->cap_ext = true;
     r = capture_graph(c, c->stream, [&] { return enqueue_main_overlap(c, in, nullptr); }, &gx[1]);
     c->cap_ext = false;
-    if (r && (c->comm || c->icp_sharded)) {
+    // only a collective that refused capture (an RCCL error inside the
+    // capture, or a capture the runtime reports unsupported / invalidated)
+    // drops the main graph for good; every other failure is returned
+    const bool refused = r == KFX_ERR_COMM || c->cap_err == hipErrorStreamCaptureUnsupported ||
+                         c->cap_err == hipErrorStreamCaptureInvalidated ||
+                         c->cap_err == hipErrorStreamCaptureImplicit;
+    if (r && (c->comm || c->icp_sharded) && refused) {
+      c->graph_note = kfx_last_error();
       (void)hipGetLastError();
       gx[1] = nullptr;
       c->ov_main_refused = true;
@@ -889,17 +900,17 @@ int kfx_create_slab_cuts(const kfx_intrinsics *intr, const kfx_params *params, i
   return create_impl(intr, params, device, rank, world, true, out, cuts);
 }
 
-// Integrate cost of one slice from kfx_slice_work_parts, in voxel-slot units:
-// every slot a wave steps through, plus kUpdatedCost more per updated voxel
-// (its tsdf / weight / colour read-modify-write), plus the slice's X*Y stored
-// slots / kSlotDiv (the waves of column tiles outside the frustum still start
-// and test their range).  Fitted to per-slab integrate times of C4 and C5
-// (tools/slab_record.py): an updated voxel costs no more than a
-// visited one, a stored slot 1/40 of one.
-constexpr int64_t kUpdatedCost = KFX_UPDATED_COST;
-constexpr int64_t kSlotDiv = KFX_SLOT_DIV;
+// Integrate cost of one slice from kfx_slice_work_parts, in 1/64 voxel-slot
+// units: every slot a wave steps through (the occlusion-clipped intervals),
+// kCostUpdated / 64 more per updated voxel (its tsdf / weight / colour
+// read-modify-write) and kCostSlot / 64 per stored slot (the waves of column
+// tiles outside the frustum still start and test their range).  Weights from
+// a non-negative least-squares fit of per-slab integrate times of C4 and C5
+// (tools/slab_fit.py): per visited slot, an updated voxel
+// 0.44-0.61, a stored slot 0-0.05.
+constexpr int64_t kCostUpdated = KFX_COST_UPDATED, kCostSlot = KFX_COST_SLOT;
 static int64_t slice_cost(int64_t cover, int64_t updated, int64_t slots) {
-  return cover + kUpdatedCost * updated + (kSlotDiv > 0 ? slots / kSlotDiv : 0);
+  return 64 * cover + kCostUpdated * updated + kCostSlot * slots;
 }
 
 int kfx_slab_balance(const int64_t *slice_work, int Z, int world, int *cuts) {
@@ -1380,6 +1391,10 @@ int kfx_get_graph_mode(kfx_ctx *c, int *mode) {
   if (!c || !mode) return set_err(KFX_ERR_ARG, "null argument");
   *mode = !c->graph_mode ? 0 : (c->ov_graph_full && !c->ov_main_refused ? 2 : 1);
   return KFX_OK;
+}
+
+const char *kfx_get_graph_note(kfx_ctx *c) {
+  return c ? c->graph_note.c_str() : "";
 }
 
 int kfx_set_icp_persistent(kfx_ctx *c, int enabled) {

@@ -33,7 +33,7 @@ EXPORTS = [
     "kfx_write_poses_txt", "kfx_get_frame_maps", "kfx_set_frame_maps", "kfx_download_tsdf",
     "kfx_upload_tsdf", "kfx_download_volume_soa", "kfx_stage_preprocess", "kfx_stage_icp_accumulate",
     "kfx_stage_icp", "kfx_stage_integrate", "kfx_stage_raycast", "kfx_set_profiling", "kfx_get_stage_ms",
-    "kfx_integrate_counts", "kfx_integrate_stats", "kfx_raycast_stats", "kfx_download_columns", "kfx_pipeline_async", "kfx_pipeline_async_u16", "kfx_register_host_buffer", "kfx_unregister_host_buffer", "kfx_slab_mask_payload", "kfx_slab_expand", "kfx_set_icp_allreduce", "kfx_create_slab", "kfx_create_slab_cuts", "kfx_slice_work", "kfx_slice_work_parts", "kfx_slice_work_at", "kfx_get_graph_mode", "kfx_slab_balance", "kfx_slab_info", "kfx_comm_get_unique_id", "kfx_comm_init",
+    "kfx_integrate_counts", "kfx_integrate_stats", "kfx_raycast_stats", "kfx_download_columns", "kfx_pipeline_async", "kfx_pipeline_async_u16", "kfx_register_host_buffer", "kfx_unregister_host_buffer", "kfx_slab_mask_payload", "kfx_slab_expand", "kfx_set_icp_allreduce", "kfx_create_slab", "kfx_create_slab_cuts", "kfx_slice_work", "kfx_slice_work_parts", "kfx_slice_work_at", "kfx_get_graph_mode", "kfx_get_graph_note", "kfx_slab_balance", "kfx_slab_info", "kfx_comm_get_unique_id", "kfx_comm_init",
     "kfx_pipeline_group", "kfx_slab_frame_local", "kfx_slab_frame_finish", "kfx_render", "kfx_volume_checksum", "kfx_extract_points", "kfx_write_ply", "kfx_save_pointcloud",
     "kfx_extract_mesh", "kfx_write_ply_mesh", "kfx_get_extract_ms", "kfx_set_extract_passes", "kfx_get_extract_passes", "kfx_set_slab_bound",
     "kfx_dataset_open", "kfx_dataset_info", "kfx_dataset_read", "kfx_dataset_close", "kfx_png_info",
@@ -117,6 +117,7 @@ def lib():
         "kfx_slice_work_parts": ([vp, P(C.c_uint8), P(f), P(C.c_int64), P(C.c_int64)], i),
         "kfx_slice_work_at": ([vp, P(C.c_uint8), P(f), P(Pose), P(C.c_int64), P(C.c_int64), P(C.c_int64)], i),
         "kfx_get_graph_mode": ([vp, P(i)], i),
+        "kfx_get_graph_note": ([vp], C.c_char_p),
         "kfx_slab_balance": ([P(C.c_int64), i, i, P(i)], i),
         "kfx_slab_info": ([vp, P(i), P(i), P(i), P(i)], i),
         "kfx_comm_get_unique_id": ([P(C.c_uint8)], i),
@@ -422,6 +423,10 @@ class KinectFusion:
         m = C.c_int()
         _check(lib().kfx_get_graph_mode(self._h, C.byref(m)), "kfx_get_graph_mode")
         return m.value
+
+    def graph_note(self) -> str:
+        """Why graph mode 2 was lowered (RCCL / capture error text), or ""."""
+        return (lib().kfx_get_graph_note(self._h) or b"").decode(errors="replace")
 
     def set_kernel_timing(self, every: int, max_samples: int = 1024):
         """Bracket every `every`-th pipelined frame with HIP events (0 = off)."""
