@@ -68,7 +68,7 @@ def parse():
                     help="frames fed from host memory through kfx_pipeline_async for host_input (0 = skip)")
     ap.add_argument("--c1-frames", type=int, default=100,
                     help="oracle frames of the C1 record (128^3, same frames; 0 = skip)")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r04_integrate_pmc.json"),
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r05_integrate_pmc.json"),
                     help="integrate PMC traffic record; attached only when it was measured on this command's "
                          "workload and step counts with the same libkfx.so (sha256)")
     ap.add_argument("--traffic-c3", default=os.path.join(ROOT, "profiles", "r05_c3_pmc.json"),

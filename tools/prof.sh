@@ -13,7 +13,7 @@ ARGS="$*"   # the stats pass runs bench.py with these (default: its defaults)
 # same frames and step counts as the stats pass; no side runs (the PMC record
 # averages every dispatch of a kernel, so only the main stream may launch it)
 PMC_ARGS="$ARGS --cpu-frames 0 --c1-frames 0 --c3-frames 0 --c5-frames 0 --host-frames 0"
-OUT="$ROOT/gpurun_out/prof"
+OUT="$ROOT/${PROF_OUT:-gpurun_out/prof}"
 mkdir -p "$OUT"
 run() {  # name, timeout, rocprof args...
   local name=$1 secs=$2
