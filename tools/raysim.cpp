@@ -493,6 +493,49 @@ static WaveCost run_wave_interleaved(const Sim &S, std::vector<Ray> &L, double c
   return w;
 }
 
+// variant 5: a lookup and the batch from the same position in ONE round trip
+// (the batch's loads issued with the map words; used only when the lookup is
+// blocked): per round each lane either skips (clear) or marches a batch
+static WaveCost run_wave_fused(const Sim &S, std::vector<Ray> &L, double cL, double cB, double cN) {
+  WaveCost w;
+  auto any = [&](auto f) {
+    for (size_t i = 0; i < L.size(); ++i)
+      if (f(i)) return true;
+    return false;
+  };
+  std::vector<uint32_t> nsk(L.size(), 0);
+  while (any([&](size_t i) { return L[i].live || L[i].cand; })) {
+    while (any([&](size_t i) { return L[i].live; })) {
+      bool anyb = false, anyl = false;
+      for (size_t i = 0; i < L.size(); ++i) {
+        Ray &r = L[i];
+        if (!r.live) continue;
+        if (r.can_skip && r.sprev >= 0) {
+          anyl = true;
+          nsk[i] = 0;
+          if (S.lookup_step(r, nsk[i])) {  // skipped: the loaded batch is dropped
+            S.after_skip(r, nsk[i]);
+            continue;
+          }
+          S.after_skip(r, nsk[i]);
+          if (!r.live) continue;
+        }
+        anyb = true;
+        S.batch(r);
+      }
+      if (anyb) w.bt_rounds++;
+      else if (anyl) w.lk_rounds++;
+    }
+    if (any([&](size_t i) { return L[i].cand; })) {
+      w.nm_rounds++;
+      for (size_t i = 0; i < L.size(); ++i)
+        if (L[i].cand) S.normal(L[i]);
+    }
+  }
+  w.t = w.lk_rounds * cL + w.bt_rounds * cB + w.nm_rounds * cN;
+  return w;
+}
+
 int main(int argc, char **argv) {
   const std::string dir = argc > 1 ? argv[1] : "/tmp/raysim";
   Sim S;
@@ -560,7 +603,8 @@ int main(int argc, char **argv) {
           }
         }
       }
-      WaveCost w = S.variant == 1 ? run_wave_interleaved(S, L, cL, cB, cN) : run_wave_kernel(S, L, cL, cB, cN);
+      WaveCost w = S.variant == 1 ? run_wave_interleaved(S, L, cL, cB, cN)
+                   : (S.variant == 5 ? run_wave_fused(S, L, cL, cB, cN) : run_wave_kernel(S, L, cL, cB, cN));
       w.tx0 = tx0;
       w.ty0 = ty0;
       for (auto &r : L) {
