@@ -180,6 +180,14 @@ int kfx_debug_force_icp_stall(kfx_ctx *ctx);
  * device_utils.cuh:31, tsdf_volume.cpp:24) at any volume size, so the oracle
  * can pin them at sizes it runs.  Results are identical either way. */
 int kfx_debug_force_index64(kfx_ctx *ctx, int on);
+/* Test and tuning hook for the two-phase raycast: a wave of the raycast
+ * marches for cap x 1024 clock cycles, then queues its unfinished rays, which
+ * groups of lanes finish (the reference loop, tsdf_volume.cu:234-258, split at
+ * an arbitrary sample).  cap = 0 sends every marching ray to the second phase,
+ * cap < 0 disables it.  Results are identical for every cap. */
+int kfx_debug_ray_queue(kfx_ctx *ctx, int cap);
+/* Rays the last two-phase raycast queued for its second phase (>= 0), <0 on error. */
+int kfx_debug_ray_queued(kfx_ctx *ctx);
 /* Slab contexts (SURVEY.md §8e alternative): instead of every rank running
  * the whole ICP (default), rank r accumulates the 27 products over its band
  * of each level's rows and the exact int64 partials are all-reduced (SUM)

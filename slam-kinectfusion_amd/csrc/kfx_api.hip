@@ -221,6 +221,9 @@ int dalloc(kfx_ctx *c, void **p, size_t bytes) {
 #ifndef KFX_PREP_AFTER_ICP
 #define KFX_PREP_AFTER_ICP 1  // overlapped frames: next preprocess waits for this frame's ICP
 #endif
+#ifndef KFX_RAY_QCAP
+#define KFX_RAY_QCAP -1  // two-phase raycast: a wave's phase 1 in 1024-cycle units (< 0: one phase)
+#endif
 #ifndef KFX_COST_UPDATED
 #define KFX_COST_UPDATED 32  // slab balancing: weight of an updated voxel (64 = one visited slot; slice_cost)
 #endif
@@ -1043,6 +1046,9 @@ static int create_impl(const kfx_intrinsics *intr, const kfx_params *params, int
   c->vol = make_vol(p, rank, world, cuts);
   // raycast wave durations of the last frame (4 waves per 16x16 block; zeroed: no hint)
   if ((r = dalloc(c, (void **)&c->vol.rdur, grid16 * 4 * sizeof(unsigned)))) return fail(r);
+  // two-phase raycast queue (zeroed: empty; kfx_internal.h rq_rec_off)
+  if ((r = dalloc(c, (void **)&c->vol.rq, rq_words(grid16, np0) * sizeof(unsigned)))) return fail(r);
+  c->vol.rqcap = KFX_RAY_QCAP;
   const size_t n = nvox(c);
   {
     // tsdf and weight in ONE allocation, weight (u8) at a fixed offset (2 MiB-
@@ -1426,6 +1432,29 @@ int kfx_debug_force_index64(kfx_ctx *c, int on) {
   }
   c->vol.force64 = on != 0;
   return KFX_OK;
+}
+
+int kfx_debug_ray_queue(kfx_ctx *c, int cap) {
+  int r = check_ctx(c);
+  if (r) return r;
+  const int v = cap < 0 ? -1 : cap;
+  if (c->vol.rqcap != v) {  // the cap is a kernel argument of captured frames
+    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipStreamSynchronize(c->pstream));
+    destroy_graphs(c);
+    HIPCHK(hipMemset(c->vol.rq + 1, 0, sizeof(unsigned)));  // kfx_debug_ray_queued: none yet
+  }
+  c->vol.rqcap = v;
+  return KFX_OK;
+}
+
+int kfx_debug_ray_queued(kfx_ctx *c) {
+  int r = check_ctx(c);
+  if (r) return r;
+  HIPCHK(hipStreamSynchronize(c->stream));
+  unsigned n = 0;
+  HIPCHK(hipMemcpy(&n, c->vol.rq + 1, sizeof(n), hipMemcpyDeviceToHost));
+  return (int)n;
 }
 
 int kfx_set_icp_allreduce(kfx_ctx *c, int enabled) {

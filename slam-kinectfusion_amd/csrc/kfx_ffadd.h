@@ -113,4 +113,38 @@ KFX_HD inline float ff_add(float x, float s, int n) {
   return x;
 }
 
+// ff_add out of line (ff_add_fast's rare fallback: one copy of the loop per
+// kernel instead of one per call site)
+KFX_HD __attribute__((noinline)) inline float ff_add_call(float x, float s, int n) { return ff_add(x, s, n); }
+
+// ff_add when all n steps stay in x's binade without a tie (the common case
+// of a ray's next few hundred samples): ff_add's first iteration with no loop
+// (X + R and X + n R both in range: the progression in between is too), a
+// fixed branch-light sequence; anything else takes ff_add.  Same results.
+KFX_HD inline float ff_add_fast(float x, float s, int n) {
+  const float as = s < 0.f ? -s : s, ax = x < 0.f ? -x : x;
+  if (n > 0 && ax >= 4.f * as && ax >= 0x1p-90f && ax < 0x1p90f && as >= 0x1p-90f) {
+    const uint32_t bx = ff_f_bits(ax);
+    const int E = (int)((bx >> 23) & 0xffu) - 127;
+    const int X = (int)((bx & 0x7fffffu) | 0x800000u);
+    const float su = (x < 0.f ? -s : s) * ff_pow2f(23 - E);  // exact, |su| <= 2^22
+    const float rf = __builtin_rintf(su);
+    const float f = su - rf;
+    if (f != 0.5f && f != -0.5f) {
+      const int R = (int)rf;
+      const int lb = 0x800000 + (f < 0.f ? 1 : 0), ub = 0x1000000 - (f < 0.f ? 0 : 1);
+      const long long Xn = (long long)X + (long long)n * R;
+      if (X + R >= lb && X + R <= ub && Xn >= lb && Xn <= ub) {
+        const float xn = (float)(int)Xn * ff_pow2f(E - 23);  // exact
+        return x < 0.f ? -xn : xn;
+      }
+    }
+  }
+#if !defined(KFX_FF_NOINLINE) || KFX_FF_NOINLINE
+  return ff_add_call(x, s, n);
+#else
+  return ff_add(x, s, n);
+#endif
+}
+
 }  // namespace kfx

@@ -131,6 +131,11 @@ struct VolView {
   int iadapt;  // length-capped chunks + longest-first order (deep volumes), else geometric chunks
   int force64;  // kfx_debug_force_index64: integrate / raycast take the 64-bit-index kernels at any size
   unsigned *rdur;  // raycast: each wave's duration in the last frame (1024-cycle units; issue priority hint)
+  // Two-phase raycast: rays still marching when their wave has
+  // run rqcap x 1024 cycles go to the ray queue rq (layout: rq_rec_off) and are
+  // finished by lane groups (k_ray_tail); rqcap < 0: one phase
+  unsigned *rq;
+  int rqcap;
   __host__ __device__ size_t bocc_bytes() const { return (size_t)tiles_x * tiles_y * bw * 8; }
   __host__ __device__ size_t socc_bytes() const { return (size_t)stx * sty * sw * 4; }
   __host__ __device__ size_t local_voxels() const { return slice * (size_t)zn; }
@@ -139,6 +144,15 @@ struct VolView {
   //   index(x, y, z) = (tile(x, y) * zn + (z - zb)) * 64 + (y & 7) * 8 + (x & 7)
   __host__ __device__ size_t tile_voxels() const { return (size_t)zn * 64; }
 };
+
+// Ray queue words: [0] queued rays, [1] the last raycast's, [16, 16 + blocks) per 16x16-pixel block
+// "its resize waits for queued rays", then kRqWords per queued ray: {pixel,
+// nextp.xyz} {ray_len, tprev, tfar, sprev} {dir.xyz, 0} (16-byte aligned).
+constexpr int kRqWords = 12;
+__host__ __device__ inline size_t rq_rec_off(size_t blocks16) { return 16 + ((blocks16 + 15) & ~(size_t)15); }
+__host__ __device__ inline size_t rq_words(size_t blocks16, size_t pixels) {
+  return rq_rec_off(blocks16) + (size_t)kRqWords * pixels;
+}
 
 // ---- slab raycast combine, shared by the kernels and the host entry points
 // (kfx_slab_mask_payload / kfx_slab_expand) so a CPU test drives the same code.
@@ -261,7 +275,7 @@ void launch_raycast_touch(hipStream_t s, VolView v, LevelGeom g0, const DevState
                           DevPose vpose, const float *xpose, uint32_t *bits, unsigned long long *out);
 // resizePointsNormals of levels >= 1 from the level-0 model maps
 void launch_resize(hipStream_t s, int levels, const LevelGeom *g, FrameView cur, FrameView prev,
-                   const DevState *st, const float *xpose);
+                   const DevState *st, const float *xpose, unsigned *rq = nullptr);
 // cross-slab combine: clear maps where the local key lost the MIN
 // out[0] += sum of per-voxel hashes, out[1] += voxels with weight > 0 (owned slices)
 void launch_checksum(hipStream_t s, VolView v, unsigned long long *out);

@@ -1,4 +1,4 @@
-// Brute-force check of kfx::ff_add (csrc/kfx_ffadd.h) against the plain loop
+// Brute-force check of kfx::ff_add and ff_add_fast (csrc/kfx_ffadd.h) against the plain loop
 // of float adds it fast-forwards.  argv: seed cases.  Prints "bad <count>".
 #include "kfx_ffadd.h"
 
@@ -43,9 +43,13 @@ int main(int argc, char** argv) {
     const int n = (int)(g() % 2100);
     float a = x;
     for (int k = 0; k < n; ++k) a = a + s;
-    const float b = kfx::ff_add(x, s, n);
+    const float b = kfx::ff_add(x, s, n), c = kfx::ff_add_fast(x, s, n);
     if (std::memcmp(&a, &b, 4) != 0 && !(std::isnan(a) && std::isnan(b))) {
       if (bad < 10) std::printf("x=%a s=%a n=%d loop %a ff %a\n", x, s, n, a, b);
+      ++bad;
+    }
+    if (std::memcmp(&a, &c, 4) != 0 && !(std::isnan(a) && std::isnan(c))) {
+      if (bad < 10) std::printf("x=%a s=%a n=%d loop %a ff_fast %a\n", x, s, n, a, c);
       ++bad;
     }
   }

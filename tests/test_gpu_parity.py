@@ -291,11 +291,18 @@ def test_720p_pipeline_matches_oracle():
     kf.close()
 
 
-def test_raycast_bit_exact(seq_qvga):
+@pytest.mark.parametrize("cap", [None, 0, 2, -1])
+def test_raycast_bit_exact(cap, seq_qvga):
+    """The raycast against the oracle's (tsdf_volume.cu:210-260) at every map
+    level; cap: the two-phase split (kfx_debug_ray_queue: None = the default,
+    0 = every ray finished by the lane groups of k_ray_tail, 2 = split a few
+    thousand cycles in, -1 = one phase)."""
     bgr, dep, gt = seq_qvga
     intr = synth.Intrinsics.qvga()
     I = Intrinsics.from_any(intr)
     kf, p = make(intr, dims=128)
+    if cap is not None:
+        kf.debug_ray_queue(cap)
     vol = O.Volume((128,) * 3, (L_VOL,) * 3)
     for k in (0, 1, 2):
         d = dep[k].astype(np.float32)
@@ -313,10 +320,54 @@ def test_raycast_bit_exact(seq_qvga):
         assert feq(gv, ov), f"vmap: {mismatch(gv, ov)} differ"
         assert feq(gn, on), f"nmap: {mismatch(gn, on)} differ"
         assert (ov[..., 2] > 0).mean() > 0.5
+        if cap == 0:  # every ray that entered the volume went to the second phase
+            assert kf.debug_ray_queued() > 0.5 * ov[..., 0].size
+        elif cap == -1:
+            assert kf.debug_ray_queued() == 0
         for l in (1, 2):
             ov, on = O.resize_points_normals(ov, on)
             _, gv, gn = kf.frame_maps(KFX_FRAME_PREV, l)
             assert feq(gv, ov) and feq(gn, on), f"level {l}"
+    kf.close()
+
+
+@pytest.mark.timeout(300)
+def test_two_phase_raycast_c2_matches_one_phase(seq_vga):
+    """BASELINE C2 (640x480, 512^3 @ 4 mm) after tracked frames: the raycast
+    split into two phases at several points (every ray queued, a few, the
+    default) gives the one-phase maps bit for bit at every level (the one-phase
+    raycast is pinned to the oracle at C2 by test_index64_kernels_match_oracle
+    and the pipeline tests), and the queue holds the rays the cap implies; the
+    same for the 64-bit-index kernels."""
+    bgr, dep, _ = seq_vga
+    intr = synth.Intrinsics.vga()
+    kf, p = make(intr, dims=512)
+    for k in range(4):
+        assert kf.pipeline(bgr[k], dep[k].astype(np.float32)) == KFX_OK
+    cam2vol = O.pose_mul(O.pose_inv(p.volu_pose), Pose.from_matrix(kf.pose_record[-1].astype(np.float32)))
+    Rinv = cam2vol.matrix()[:3, :3].T.copy()
+    maps, queued = {}, {}
+    for cap in (-1, 0, 4, 40, 90):
+        kf.debug_ray_queue(cap)
+        kf.stage_raycast(cam2vol, Rinv)
+        queued[cap] = kf.debug_ray_queued()
+        maps[cap] = [kf.frame_maps(KFX_FRAME_PREV, l)[1:] for l in range(3)]
+    ref = maps[-1]
+    assert (ref[0][0][..., 2] > 0).mean() > 0.5
+    for cap in (0, 4, 40, 90):
+        for l in range(3):
+            assert feq(maps[cap][l][0], ref[l][0]), f"cap {cap} vmap level {l}: {mismatch(maps[cap][l][0], ref[l][0])}"
+            assert feq(maps[cap][l][1], ref[l][1]), f"cap {cap} nmap level {l}: {mismatch(maps[cap][l][1], ref[l][1])}"
+    assert queued[-1] == 0 and queued[0] > 0.5 * 640 * 480 and queued[0] >= queued[4] >= queued[40] > 0, queued
+    # the 64-bit-index kernels (kfx_debug_force_index64) split the same way
+    kf.debug_force_index64(True)
+    for cap in (0, 40):
+        kf.debug_ray_queue(cap)
+        kf.stage_raycast(cam2vol, Rinv)
+        assert kf.debug_ray_queued() > 0
+        for l in range(3):
+            _, gv, gn = kf.frame_maps(KFX_FRAME_PREV, l)
+            assert feq(gv, ref[l][0]) and feq(gn, ref[l][1]), f"index64 cap {cap} level {l}"
     kf.close()
 
 

@@ -536,6 +536,128 @@ static WaveCost run_wave_fused(const Sim &S, std::vector<Ray> &L, double cL, dou
   return w;
 }
 
+// variant 6: two phases.  Phase 1 is the kernel's schedule capped at `cap`
+// wave rounds (lookups + batches); the rays still marching then go to a queue
+// (candidates pending at the cap take the wave's normal pass first).  Phase 2
+// marches each queued ray with a group of G lanes: a scan round (lane j looks
+// up the box at sample k + j*S; the contiguous clear prefix is replayed) and a
+// dense round (G consecutive samples in one round trip), repeated.
+struct Phase2 {
+  int cap = 20, G = 64, S = 8;
+};
+static int phase2_ray(const Sim &S, Ray r, const Phase2 &P, int &scans, int &denses, int &norms) {
+  int rounds = 0;
+  const int saved_kR = S.kR;
+  Sim &M = const_cast<Sim &>(S);
+  while (r.live) {
+    if (r.can_skip && r.sprev >= 0) {
+      ++rounds;
+      ++scans;
+      // lane j: box at the position of sample (carried) + j*S
+      int E = 0;
+      Ray q = r;
+      for (int j = 0; j < P.G && q.live; ++j) {
+        const int sj = j * P.S;
+        if (sj > E) break;
+        // advance q to sample sj (sequential adds: the exact positions)
+        while ((int)(q.kbase - r.kbase) < sj && q.live) {
+          if (!(q.ray_len < q.tfar)) q.live = false;
+          q.nextp = add(q.nextp, q.vstep);
+          q.ray_len = q.ray_len + S.v.vs;
+          q.kbase++;
+        }
+        if (!q.live) break;
+        const float lim = S.lookup_kernel(q);
+        if (lim >= 1.f) E = std::max(E, sj + (int)fminf(lim, S.skip_cap));
+      }
+      if (E > 0) {
+        uint32_t nsk = 0;
+        // replay E samples from r
+        for (int i = 0; i < E && r.live; ++i) {
+          if (!(r.ray_len < r.tfar)) {
+            r.live = false;
+            break;
+          }
+          r.nextp = add(r.nextp, r.vstep);
+          r.ray_len = r.ray_len + S.v.vs;
+          ++nsk;
+        }
+        S.after_skip(r, nsk);
+        if (!r.live) break;
+      }
+    }
+    ++rounds;
+    ++denses;
+    for (int h = 0; h < (P.G + 31) / 32 && r.live; ++h) {
+      M.kR = std::min(32, P.G - 32 * h);
+      S.batch(r);
+    }
+    M.kR = saved_kR;
+    if (r.cand) {
+      ++rounds;
+      ++norms;
+      S.normal(r);
+    }
+  }
+  return rounds;
+}
+static WaveCost run_wave_two_phase(const Sim &S, std::vector<Ray> &L, double cL, double cB, double cN,
+                                   const Phase2 &P, std::vector<int> &queued_rounds) {
+  WaveCost w;
+  auto any = [&](auto f) {
+    for (auto &r : L)
+      if (f(r)) return true;
+    return false;
+  };
+  int rounds = 0;
+  bool capped = false;
+  while (!capped && any([](const Ray &r) { return r.live || r.cand; })) {
+    while (any([](const Ray &r) { return r.live; })) {
+      if (rounds >= P.cap) {
+        capped = true;
+        break;
+      }
+      std::vector<char> in(L.size());
+      std::vector<uint32_t> nsk(L.size(), 0);
+      for (size_t i = 0; i < L.size(); ++i) in[i] = L[i].can_skip && L[i].live && L[i].sprev >= 0;
+      for (;;) {
+        bool a = false;
+        for (size_t i = 0; i < L.size(); ++i) a |= in[i] != 0;
+        if (!a) break;
+        w.lk_rounds++;
+        ++rounds;
+        for (size_t i = 0; i < L.size(); ++i)
+          if (in[i] && !S.lookup_step(L[i], nsk[i])) in[i] = 0;
+        if (rounds >= P.cap) {  // lanes still in the lookup loop stop where they are
+          for (size_t i = 0; i < L.size(); ++i) in[i] = 0;
+        }
+      }
+      for (size_t i = 0; i < L.size(); ++i) S.after_skip(L[i], nsk[i]);
+      if (!any([](const Ray &r) { return r.live; })) break;
+      if (rounds >= P.cap) {
+        capped = true;
+        break;
+      }
+      w.bt_rounds++;
+      ++rounds;
+      for (auto &r : L)
+        if (r.live) S.batch(r);
+    }
+    if (any([](const Ray &r) { return r.cand; })) {
+      w.nm_rounds++;
+      for (auto &r : L)
+        if (r.cand) S.normal(r);
+    }
+  }
+  for (auto &r : L)
+    if (r.live) {
+      int sc = 0, dn = 0, nm = 0;
+      queued_rounds.push_back(phase2_ray(S, r, P, sc, dn, nm));
+    }
+  w.t = w.lk_rounds * cL + w.bt_rounds * cB + w.nm_rounds * cN;
+  return w;
+}
+
 int main(int argc, char **argv) {
   const std::string dir = argc > 1 ? argv[1] : "/tmp/raysim";
   Sim S;
@@ -588,6 +710,11 @@ int main(int argc, char **argv) {
   const double cL = 1.6, cB = 1.9, cN = 5.0;
   std::vector<WaveCost> waves;
   long long tot_lk = 0, tot_bt = 0;
+  Phase2 P2;
+  if (getenv("RAYSIM_CAP")) P2.cap = atoi(getenv("RAYSIM_CAP"));
+  if (getenv("RAYSIM_G")) P2.G = atoi(getenv("RAYSIM_G"));
+  if (getenv("RAYSIM_S")) P2.S = atoi(getenv("RAYSIM_S"));
+  std::vector<int> queued;  // variant 6: phase-2 rounds of each queued ray
   for (int ty0 = 0; ty0 < S.H; ty0 += 8)
     for (int tx0 = 0; tx0 < S.W; tx0 += 8) {
       std::vector<Ray> L(64);
@@ -603,8 +730,10 @@ int main(int argc, char **argv) {
           }
         }
       }
-      WaveCost w = S.variant == 1 ? run_wave_interleaved(S, L, cL, cB, cN)
-                   : (S.variant == 5 ? run_wave_fused(S, L, cL, cB, cN) : run_wave_kernel(S, L, cL, cB, cN));
+      WaveCost w = S.variant == 1   ? run_wave_interleaved(S, L, cL, cB, cN)
+                   : S.variant == 5 ? run_wave_fused(S, L, cL, cB, cN)
+                   : S.variant == 6 ? run_wave_two_phase(S, L, cL, cB, cN, P2, queued)
+                                    : run_wave_kernel(S, L, cL, cB, cN);
       w.tx0 = tx0;
       w.ty0 = ty0;
       for (auto &r : L) {
@@ -632,6 +761,16 @@ int main(int argc, char **argv) {
          pct(btd, 1.0));
   printf("  modeled wave us (excl. setup) med %.1f p90 %.1f p99 %.1f max %.1f\n", pct(t, .5), pct(t, .9), pct(t, .99),
          pct(t, 1.0));
+  if (S.variant == 6) {
+    std::vector<double> q(queued.begin(), queued.end());
+    if (q.empty()) q.push_back(0);
+    double sum = 0;
+    for (double x : q) sum += x;
+    printf("  phase 2 (cap %d, G %d, S %d): queued rays %zu; rounds/ray mean %.2f med %.0f p90 %.0f p99 %.0f max %.0f; "
+           "wave-rounds %.0f\n",
+           P2.cap, P2.G, P2.S, queued.size(), sum / q.size(), pct(q, .5), pct(q, .9), pct(q, .99), pct(q, 1.0),
+           sum * P2.G / 64.0);
+  }
   if (getenv("RAYSIM_SLOW")) {
     std::vector<size_t> idx(waves.size());
     for (size_t i = 0; i < idx.size(); ++i) idx[i] = i;
