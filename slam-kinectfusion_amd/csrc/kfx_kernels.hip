@@ -2093,13 +2093,43 @@ __device__ __forceinline__ float box_limit(int B, int bx, int by, int nbx, int n
 __device__ __forceinline__ f3 ff_add3(f3 p, f3 s, int n) {
   return {ff_add_fast(p.x, s.x, n), ff_add_fast(p.y, s.y, n), ff_add_fast(p.z, s.z, n)};
 }
-// One skip lookup at voxel position (cx, cy, cz): the samples a ray may replay
-// from there (lim < 1: blocked).  Both map words of the current column are in
-// flight together (one round trip per lookup); one box per lookup: the
-// super-brick's when its cell is clear (its 3x3 box contains the brick's
-// laterally; tools/raysim: the brick box alone adds < 1 % of lookups there),
-// else the brick's: the cell's 3x3 tile box with the dilated z run of clear
-// cells in the direction of travel (the word widened to 64 bits).
+#ifndef KFX_RAY_CHAIN
+#define KFX_RAY_CHAIN 2  // skip lookups: boxes per round trip (1 or 2)
+#endif
+// The brick box's lateral (x / y) exit from voxel position (cx, cy) in cell (bx, by).
+__device__ __forceinline__ float brick_lateral_exit(const VolView &v, int bx, int by, float cx, float cy, f3 dv, f3 idv) {
+  const float xl = bx > 0 ? (float)(8 * bx - 8) : -kInf, xh = bx < v.tiles_x - 1 ? (float)(8 * bx + 15) : kInf;
+  const float yl = by > 0 ? (float)(8 * by - 8) : -kInf, yh = by < v.tiles_y - 1 ? (float)(8 * by + 15) : kInf;
+  return fminf(axis_limit(cx, dv.x, idv.x, xl, xh), axis_limit(cy, dv.y, idv.y, yl, yh));
+}
+// The clear box of a brick column word at voxel position (cx, cy, cz) of cell
+// (bx, by, lbz): the cell's 3x3 tile box with the dilated z run of clear cells
+// in the direction of travel (lim < 1: blocked).
+__device__ __forceinline__ float run_box(const VolView &v, unsigned long long w, int nbits, int b, int lc, int ncell,
+                                         int c0, int B, int bx, int by, int nbx, int nby, float cx, float cy, float cz,
+                                         f3 dv, f3 idv) {
+  float zl = -kInf, zh = kInf;
+  if (dv.z > 0.f) {
+    const unsigned long long up = w >> b;
+    const int top = lc + (up ? __builtin_ctzll(up) : nbits - b) - 1;
+    if (top < ncell - 1) zh = (float)(B * (top + c0) + 2 * B - 1);
+  } else {
+    const unsigned long long dn = w << (63 - b);
+    const int bot = lc - (dn ? __builtin_clzll(dn) : b + 1) + 1;
+    if (bot > 0) zl = (float)(B * (bot + c0) - B);
+  }
+  return box_limit(B, bx, by, nbx, nby, zl, zh, cx, cy, cz, dv, idv);
+}
+// Samples a ray may replay from voxel position (cx, cy, cz) (< 1: blocked).
+// The super-brick's box when its cell is clear (its 3x3 box contains the
+// brick's laterally; tools/raysim: the brick box alone adds < 1 % of lookups
+// there), else the brick's.  KFX_RAY_CHAIN 2: the words of the column at the
+// brick box's lateral exit point (known before any word is back) are loaded
+// in the same round trip, and that column's brick box extends the run when
+// the point lies inside it (a ray along a tilted surface leaves the boxes
+// sideways one after another: tools/raysim variant 8, C2's slowest wave 54
+// -> 36 lookup rounds).  Every sample of the run lies in one of the boxes at
+// model positions c + t dv: the same 0.2-voxel margins as one box.
 __device__ __forceinline__ float skip_limit(const VolView &v, float cx, float cy, float cz, f3 dv, f3 idv) {
   const int ix = (int)floorf(cx), iy = (int)floorf(cy), iz = (int)floorf(cz);
   const int bx = min(max(ix >> 3, 0), v.tiles_x - 1), by = min(max(iy >> 3, 0), v.tiles_y - 1);
@@ -2108,25 +2138,30 @@ __device__ __forceinline__ float skip_limit(const VolView &v, float cx, float cy
   const int lsz = min(max((iz >> 5) - v.sz0, 0), v.nsz - 1);
   const unsigned long long bwd = v.bocc[(size_t)(by * v.tiles_x + bx) * v.bw + (lbz >> 6)];
   const uint32_t swd = v.socc[(size_t)(sy * v.stx + sx) * v.sw + (lsz >> 5)];
+#if KFX_RAY_CHAIN >= 2
+  const float t1r = brick_lateral_exit(v, bx, by, cx, cy, dv, idv);
+  const float t1 = t1r < 1.0e6f ? t1r : 0.f;  // (no lateral exit: the same column, unused)
+  const float c1x = cx + t1 * dv.x, c1y = cy + t1 * dv.y, c1z = cz + t1 * dv.z;
+  const int ix1 = (int)floorf(c1x), iy1 = (int)floorf(c1y), iz1 = (int)floorf(c1z);
+  const int bx1 = min(max(ix1 >> 3, 0), v.tiles_x - 1), by1 = min(max(iy1 >> 3, 0), v.tiles_y - 1);
+  const int lbz1 = min(max((iz1 >> 3) - v.bz0, 0), v.nbz - 1);
+  const unsigned long long bwd1 = v.bocc[(size_t)(by1 * v.tiles_x + bx1) * v.bw + (lbz1 >> 6)];
+#endif
   const int bb = lbz & 63, sb = lsz & 31;
   const bool sclear = !((swd >> sb) & 1u), bclear = !((bwd >> bb) & 1ull);
   float lim = 0.f;
   if (sclear || bclear) {
-    const unsigned long long w = sclear ? (unsigned long long)swd : bwd;
-    const int nbits = sclear ? 32 : 64, b = sclear ? sb : bb, lc = sclear ? lsz : lbz;
-    const int ncell = sclear ? v.nsz : v.nbz, c0 = sclear ? v.sz0 : v.bz0, B = sclear ? 32 : 8;
-    float zl = -kInf, zh = kInf;
-    if (dv.z > 0.f) {
-      const unsigned long long up = w >> b;
-      const int top = lc + (up ? __builtin_ctzll(up) : nbits - b) - 1;
-      if (top < ncell - 1) zh = (float)(B * (top + c0) + 2 * B - 1);
-    } else {
-      const unsigned long long dn = w << (63 - b);
-      const int bot = lc - (dn ? __builtin_clzll(dn) : b + 1) + 1;
-      if (bot > 0) zl = (float)(B * (bot + c0) - B);
+    lim = run_box(v, sclear ? (unsigned long long)swd : bwd, sclear ? 32 : 64, sclear ? sb : bb, sclear ? lsz : lbz,
+                  sclear ? v.nsz : v.nbz, sclear ? v.sz0 : v.bz0, sclear ? 32 : 8, sclear ? sx : bx, sclear ? sy : by,
+                  sclear ? v.stx : v.tiles_x, sclear ? v.sty : v.tiles_y, cx, cy, cz, dv, idv);
+#if KFX_RAY_CHAIN >= 2
+    const int bb1 = lbz1 & 63;
+    if (t1 > 0.f && t1 <= lim && !((bwd1 >> bb1) & 1ull)) {
+      const float lim1 = run_box(v, bwd1, 64, bb1, lbz1, v.nbz, v.bz0, 8, bx1, by1, v.tiles_x, v.tiles_y, c1x, c1y, c1z,
+                                 dv, idv);
+      if (lim1 >= 1.f) lim = fmaxf(lim, t1 + lim1);
     }
-    lim = box_limit(B, sclear ? sx : bx, sclear ? sy : by, sclear ? v.stx : v.tiles_x, sclear ? v.sty : v.tiles_y,
-                    zl, zh, cx, cy, cz, dv, idv);
+#endif
   }
   return lim;
 }

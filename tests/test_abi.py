@@ -69,7 +69,8 @@ def test_product_build_refuses_experiment_macros():
     src = open(os.path.join(pkg, "csrc", "kfx_kernels.hip")).read()
     for m in ("KFX_INT_ZCLASS", "KFX_INT_CERT", "KFX_INT_DEDUP", "KFX_INT_LEAN", "KFX_INT_PLAN", "KFX_INT_PRIO",
               "KFX_RAY_PRIO", "KFX_ICP_XCOARSE", "KFX_INT_EXP", "KFX_PLAN_EXP", "KFX_RAY_NOREPLAY",
-              "KFX_RAY_NONORMAL", "wrong values"):
+              "KFX_RAY_NONORMAL", "KFX_RAY_PIPE", "KFX_RAY_FFREPLAY", "KFX_RAY_FF_MIN", "KFX_RAY_FAKE_REPLAY",
+              "KFX_RAY_LDS", "wrong values"):
         assert m not in src, m
 
 

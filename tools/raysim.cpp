@@ -259,9 +259,90 @@ struct Sim {
     return lim;
   }
 
+  // variant 7: up to chainK lookups in one round trip, chained while each box is
+  // left through a lateral (x / y) face (the next columns along the ray's xy
+  // path are predictable without the loaded words): the boxes at the model
+  // positions c + total * dv, total capped by skip_cap
+  int chainK = 4;
+  float lookup_chain(const Ray &r) const {
+    const float inv = 1.f / v.vs;
+    float total = 0.f;
+    for (int k = 0; k < chainK; ++k) {
+      const float cxv = r.nextp.x * inv + total * r.dv.x, cyv = r.nextp.y * inv + total * r.dv.y,
+                  czv = r.nextp.z * inv + total * r.dv.z;
+      const int ix = (int)floorf(cxv), iy = (int)floorf(cyv), iz = (int)floorf(czv);
+      const int bx = std::min(std::max(ix >> 3, 0), v.tx - 1), by = std::min(std::max(iy >> 3, 0), v.ty - 1);
+      const int lbz = std::min(std::max(iz >> 3, 0), v.nbz - 1);
+      const int sx = std::min(std::max(ix >> 5, 0), v.stx - 1), sy = std::min(std::max(iy >> 5, 0), v.sty - 1);
+      const int lsz = std::min(std::max(iz >> 5, 0), v.nsz - 1);
+      float lim = 0.f, zlim = 0.f;
+      auto axes = [&](int B, int cbx, int cby, int nbx, int nby, float zl, float zh, float &lz) {
+        const float xl = cbx > 0 ? (float)(B * cbx - B) : -kInf, xh = cbx < nbx - 1 ? (float)(B * cbx + 2 * B - 1) : kInf;
+        const float yl = cby > 0 ? (float)(B * cby - B) : -kInf, yh = cby < nby - 1 ? (float)(B * cby + 2 * B - 1) : kInf;
+        lz = axis_limit(czv, r.dv.z, r.idv.z, zl, zh);
+        return fminf(fminf(axis_limit(cxv, r.dv.x, r.idv.x, xl, xh), axis_limit(cyv, r.dv.y, r.idv.y, yl, yh)), lz);
+      };
+      const bool sclear = !v.socc[v.si(sx, sy, lsz)];
+      if (sclear) {
+        float zl, zh;
+        zrun([&](int z) { return v.socc[v.si(sx, sy, z)] != 0; }, lsz, v.nsz, 32, r.dv.z, zl, zh);
+        lim = axes(32, sx, sy, v.stx, v.sty, zl, zh, zlim);
+      } else if (!v.bocc[v.bi(bx, by, lbz)]) {
+        float zl, zh;
+        zrun([&](int z) { return v.bocc[v.bi(bx, by, z)] != 0; }, lbz, v.nbz, 8, r.dv.z, zl, zh);
+        lim = axes(8, bx, by, v.tx, v.ty, zl, zh, zlim);
+      }
+      if (!(lim >= 1.f)) break;
+      total += lim;
+      if (total >= skip_cap || lim >= zlim) break;  // capped, or left through z: the next words are not predictable
+    }
+    return total;
+  }
+
+  // variant 8 (implementable: every word address known before any word is
+  // back): point j+1 is the lateral (x / y) exit of the BRICK box of point j's
+  // cell (no loaded data needed); the words of all chainK points are loaded in
+  // one round trip; the box at point 0 as the kernel (super when clear, else
+  // brick), brick boxes at the others; a point extends the run while it lies
+  // inside the run cleared so far
+  float lookup_chain2(const Ray &r) const {
+    const float inv = 1.f / v.vs;
+    float T = 0.f, t = 0.f;
+    for (int k = 0; k < chainK; ++k) {
+      const float cxv = r.nextp.x * inv + t * r.dv.x, cyv = r.nextp.y * inv + t * r.dv.y, czv = r.nextp.z * inv + t * r.dv.z;
+      const int ix = (int)floorf(cxv), iy = (int)floorf(cyv), iz = (int)floorf(czv);
+      const int bx = std::min(std::max(ix >> 3, 0), v.tx - 1), by = std::min(std::max(iy >> 3, 0), v.ty - 1);
+      const int lbz = std::min(std::max(iz >> 3, 0), v.nbz - 1);
+      const int sx = std::min(std::max(ix >> 5, 0), v.stx - 1), sy = std::min(std::max(iy >> 5, 0), v.sty - 1);
+      const int lsz = std::min(std::max(iz >> 5, 0), v.nsz - 1);
+      const float xl = bx > 0 ? (float)(8 * bx - 8) : -kInf, xh = bx < v.tx - 1 ? (float)(8 * bx + 15) : kInf;
+      const float yl = by > 0 ? (float)(8 * by - 8) : -kInf, yh = by < v.ty - 1 ? (float)(8 * by + 15) : kInf;
+      const float tlat = fminf(axis_limit(cxv, r.dv.x, r.idv.x, xl, xh), axis_limit(cyv, r.dv.y, r.idv.y, yl, yh));
+      if (t <= T || k == 0) {
+        float lim = 0.f;
+        const bool sclear = k == 0 && !v.socc[v.si(sx, sy, lsz)];
+        if (sclear) {
+          float zl, zh;
+          zrun([&](int z) { return v.socc[v.si(sx, sy, z)] != 0; }, lsz, v.nsz, 32, r.dv.z, zl, zh);
+          lim = box_limit(32, sx, sy, v.stx, v.sty, zl, zh, cxv, cyv, czv, r.dv, r.idv);
+        } else if (!v.bocc[v.bi(bx, by, lbz)]) {
+          float zl, zh;
+          zrun([&](int z) { return v.bocc[v.bi(bx, by, z)] != 0; }, lbz, v.nbz, 8, r.dv.z, zl, zh);
+          lim = box_limit(8, bx, by, v.tx, v.ty, zl, zh, cxv, cyv, czv, r.dv, r.idv);
+        }
+        if (k == 0 && !(lim >= 1.f)) return 0.f;
+        if (lim >= 1.f) T = fmaxf(T, t + lim);
+      }
+      if (!(tlat < kInf)) break;
+      t += tlat;
+      if (t > T || t >= skip_cap) break;
+    }
+    return fminf(T, skip_cap);
+  }
+
   // one lookup + replay; returns false when the lane leaves the lookup loop
   bool lookup_step(Ray &r, uint32_t &nsk) const {
-    float lim = variant == 2 ? fmaxf(lookup_kernel(r), lookup_dist(r)) : lookup_kernel(r);
+    float lim = variant == 2 ? fmaxf(lookup_kernel(r), lookup_dist(r)) : (variant == 7 ? lookup_chain(r) : (variant == 8 ? lookup_chain2(r) : lookup_kernel(r)));
     if (variant == 3) lim = fmaxf(lim, lookup_probe(r));
     if (r.trace) {
       const float inv = 1.f / v.vs;
@@ -666,6 +747,7 @@ int main(int argc, char **argv) {
   if (argc > 4) S.probesK = atoi(argv[4]);
   if (argc > 5) S.probeS = atoi(argv[5]);
   if (getenv("RAYSIM_SUP")) S.suppress = atoi(getenv("RAYSIM_SUP"));
+  if (getenv("RAYSIM_K")) S.chainK = atoi(getenv("RAYSIM_K"));
   int dims[3];
   FILE *f = fopen((dir + "/dims.bin").c_str(), "rb");
   if (!f || fread(dims, 4, 3, f) != 3) return 1;
@@ -736,6 +818,19 @@ int main(int argc, char **argv) {
                                     : run_wave_kernel(S, L, cL, cB, cN);
       w.tx0 = tx0;
       w.ty0 = ty0;
+      if (getenv("RAYSIM_TILE")) {  // per-lane counts of one wave (x0,y0), then the busiest lane traced
+        int qx, qy;
+        if (sscanf(getenv("RAYSIM_TILE"), "%d,%d", &qx, &qy) == 2 && qx == tx0 && qy == ty0) {
+          int best = 0;
+          for (int l = 0; l < 64; ++l) {
+            printf("  lane %2d px (%d,%d): lookups %d batches %d normals %d hit %d dir (%.3f %.3f %.3f)\n", l,
+                   tx0 + (l & 7), ty0 + (l >> 3), L[l].lookups, L[l].batches, L[l].normals, (int)L[l].hit, L[l].dir.x,
+                   L[l].dir.y, L[l].dir.z);
+            if (L[l].lookups + L[l].batches > L[best].lookups + L[best].batches) best = l;
+          }
+          printf("  busiest lane %d: RAYSIM_PIX=%d,%d\n", best, tx0 + (best & 7), ty0 + (best >> 3));
+        }
+      }
       for (auto &r : L) {
         tot_lk += r.lookups;
         tot_bt += r.batches;
