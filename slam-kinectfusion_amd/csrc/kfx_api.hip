@@ -113,6 +113,7 @@ struct kfx_ctx {
   hipStream_t pstream = nullptr;
   hipEvent_t ev_prep = nullptr, ev_free[2]{};
   hipEvent_t ev_icp = nullptr;  // after the last overlapped frame's ICP (the next preprocess starts there)
+  hipEvent_t ev_group = nullptr;  // kfx_pipeline_group combine: fork (member 0) / join (the others)
   bool group_chain = false;     // kfx_pipeline_group member: record ev_icp after every ICP
   bool graphs_stale = false;    // a refused persistent ICP launch: captured graphs still hold it
 
@@ -1018,6 +1019,9 @@ static int create_impl(const kfx_intrinsics *intr, const kfx_params *params, int
   for (hipEvent_t *e : {&c->ev_prep, &c->ev_free[0], &c->ev_free[1], &c->ev_icp})
     if (hipEventCreateWithFlags(e, hipEventDisableTiming | hipEventReleaseToDevice) != hipSuccess)
       return fail(set_err(KFX_ERR_HIP, "hipEventCreate failed"));
+  // group members may sit on other devices: a system-scope release
+  if (hipEventCreateWithFlags(&c->ev_group, hipEventDisableTiming) != hipSuccess)
+    return fail(set_err(KFX_ERR_HIP, "hipEventCreate failed"));
 
   for (int l = 0; l < c->L; ++l) {
     const size_t np = (size_t)c->g[l].w * c->g[l].h;
@@ -1108,7 +1112,7 @@ int kfx_destroy(kfx_ctx *c) {
   for (void *a : c->allocs) (void)hipFree(a);
   for (auto &e : c->ev)
     if (e) (void)hipEventDestroy(e);
-  for (hipEvent_t e : {c->ev_prep, c->ev_free[0], c->ev_free[1], c->ev_icp})
+  for (hipEvent_t e : {c->ev_prep, c->ev_free[0], c->ev_free[1], c->ev_icp, c->ev_group})
     if (e) (void)hipEventDestroy(e);
   for (hipEvent_t e : c->tsets) (void)hipEventDestroy(e);
   for (hipEvent_t e : c->xev)
@@ -2541,10 +2545,12 @@ int kfx_pipeline_group(kfx_ctx **cs, int n, const uint8_t *bgr, const float *dep
     HIPCHK(hipStreamSynchronize(cs[k]->stream));
   }
   // combine, with the reductions of the collective path run by one kernel over
-  // every member's buffer.  The shared part (reductions, resume passes,
-  // masks) runs on member 0's stream; each member's timed combine is that
-  // part ([7]..[8]) plus its own expand + pyramid ([6]..[4]) — what one rank
-  // of the RCCL path spends, without the members queuing behind each other.
+  // every member's buffer on member 0's stream; each member's resume pass and
+  // mask run on its own stream (its own device's volume), forked from and
+  // joined back to member 0's stream by events.  Each member's timed combine
+  // is the shared part ([7]..[8]) plus its own expand + pyramid ([6]..[4]) —
+  // what one rank of the RCCL path spends, without the members queuing behind
+  // each other.
   uint32_t *kin[kMaxGroup], *kout[kMaxGroup], *pay[kMaxGroup];
   for (int k = 0; k < n; ++k) {
     kin[k] = cs[k]->key_local;
@@ -2556,12 +2562,27 @@ int kfx_pipeline_group(kfx_ctx **cs, int n, const uint8_t *bgr, const float *dep
   hipStream_t s0 = c0->stream;
   for (int k = 0; k < n; ++k)
     if (tev[k]) HIPCHK(hipEventRecord(tev[k][7], s0));
+  // per-member work forked from s0 and joined back (each launch on its own device)
+  auto per_member = [&](auto &&work) -> int {
+    int e;
+    HIPCHK(hipEventRecord(c0->ev_group, s0));
+    for (int k = 0; k < n; ++k) {
+      if ((e = check_ctx(cs[k]))) return e;
+      if (k > 0) HIPCHK(hipStreamWaitEvent(cs[k]->stream, c0->ev_group, 0));
+      work(cs[k]);
+      if (k > 0) HIPCHK(hipEventRecord(cs[k]->ev_group, cs[k]->stream));
+    }
+    if ((e = check_ctx(c0))) return e;
+    for (int k = 1; k < n; ++k) HIPCHK(hipStreamWaitEvent(s0, cs[k]->ev_group, 0));
+    return KFX_OK;
+  };
   if (c0->pass1_bounded) {  // [key | pend] MIN, then the resume passes
     launch_group_reduce(s0, kin, n, kout, n, 2 * np, false);
-    for (int k = 0; k < n; ++k) enqueue_slab_resume(cs[k], s0);
+    if ((r = per_member([](kfx_ctx *c) { enqueue_slab_resume(c, c->stream); }))) return r;
   }
   launch_group_reduce(s0, kin, n, kout, n, np, false);
-  for (int k = 0; k < n; ++k) launch_slab_mask(s0, cs[k]->key_local, cs[k]->key_min, (int)np);
+  if ((r = per_member([np](kfx_ctx *c) { launch_slab_mask(c->stream, c->key_local, c->key_min, (int)np); })))
+    return r;
   launch_group_reduce(s0, pay, n, pay, n, 4 * np, true);
   for (int k = 0; k < n; ++k)
     if (tev[k]) HIPCHK(hipEventRecord(tev[k][8], s0));
