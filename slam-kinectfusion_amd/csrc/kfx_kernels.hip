@@ -68,6 +68,9 @@
 #ifndef KFX_FF_MIN
 #define KFX_FF_MIN 768  // fast-forward replays of at least this many adds (shorter ones: the adds; A/B r3m: 384 costs C2 +8 %)
 #endif
+#ifndef KFX_INT_SLAB_CAPW
+#define KFX_INT_SLAB_CAPW 4  // integrate, Z-slab contexts: at most this many times KFX_INT_WAVES waves
+#endif
 #ifndef KFX_INT_WAVES
 #define KFX_INT_WAVES 12288  // integrate: target wave count (z-chunks per column tile; C2: 3 chunks of 4096 tiles)
 #endif
@@ -3797,7 +3800,7 @@ int integrate_chunks(const VolView &v) {
   // replays of many chunks cost more than the tail they cut: C5 slab 0, 772
   // slices of 65536 tiles, took 1.25 ms in 7 chunks against 0.85 ms in one)
   if (KFX_INT_SLAB_CHUNK > 0 && v.zn < v.Z)
-    nc = std::max(nc, std::min((v.zn + KFX_INT_SLAB_CHUNK - 1) / KFX_INT_SLAB_CHUNK, 4 * KFX_INT_WAVES / tiles));
+    nc = std::max(nc, std::min((v.zn + KFX_INT_SLAB_CHUNK - 1) / KFX_INT_SLAB_CHUNK, KFX_INT_SLAB_CAPW * KFX_INT_WAVES / tiles));
   return std::max(1, std::min(KFX_INT_MAXCHUNK, nc));
 }
 
