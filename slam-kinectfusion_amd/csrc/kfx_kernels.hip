@@ -2096,6 +2096,9 @@ __device__ __forceinline__ float box_limit(int B, int bx, int by, int nbx, int n
 __device__ __forceinline__ f3 ff_add3(f3 p, f3 s, int n) {
   return {ff_add_fast(p.x, s.x, n), ff_add_fast(p.y, s.y, n), ff_add_fast(p.z, s.z, n)};
 }
+#ifndef KFX_RAY_EXIT
+#define KFX_RAY_EXIT 1  // a ray whose remaining samples all lie in a clear box ends there
+#endif
 #ifndef KFX_RAY_CHAIN
 #define KFX_RAY_CHAIN 2  // skip lookups: boxes per round trip (1 or 2)
 #endif
@@ -2399,6 +2402,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((kSlab || !
             if (kStats) st_blocked += 1;
             break;
           }
+#if KFX_RAY_EXIT
+          if (!kSlab && (tfar - ray_len) * rstep + 2.f <= fminf(lim, rc.skip_cap)) {
+            // every sample the loop has left (at most (tfar - ray_len) / step
+            // + 1, 2 of margin over the accumulated rounding) lies in the
+            // clear box: no event follows (tsdf_volume.cu:234), the ray ends
+            // here without a hit and without replaying its last run
+            if (kStats || kTrace) st_lookups += 1;
+            live = false;
+            break;
+          }
+#endif
           int n = (int)fminf(lim, rc.skip_cap);
           if (kSlab) {
             // a slab's ray ends 2 slices past its owned range (no owned
