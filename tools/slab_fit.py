@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Slab integrate cost model: a slab's integrate ms against
 its stored slices' estimated work, ms ~ c + a * cover + b * updated + s * slots
-+ w * waves (cover: visited voxel slots of the occlusion-clipped column
++ w * waves, minimising the relative errors (cover: visited voxel slots of the occlusion-clipped column
 intervals, updated: voxels passing the update test, slots: stored voxel slots,
 waves: k_integrate's (tile, chunk) waves; the calibration
 frames' means, tools/slab_record.py), fitted by non-negative least squares over
@@ -43,7 +43,11 @@ def fit(recs):
     y = np.array([r[4] for r in rs], np.float64)
     scale = A.max(axis=0)
     scale[scale == 0] = 1.0
-    coef, _ = nnls(A / scale, y)
+    # relative least squares (rows divided by the measured ms): the model is
+    # judged by its relative error per slab, and small slabs would otherwise
+    # carry little weight
+    w = 1.0 / y
+    coef, _ = nnls((A / scale) * w[:, None], y * w)
     coef = coef / scale
     pred = A @ coef
     rel = (pred - y) / y
