@@ -1084,6 +1084,7 @@ static int create_impl(const kfx_intrinsics *intr, const kfx_params *params, int
   for (int b = 0; b < 2; ++b)
     c->planb[b] = make_icp_plan(c->L, c->g, c->p.icp_iter_count, c->curb[b], c->prev,
                                 c->p.icp_dist_threshold, c->angle_thr);
+  for (int b = 0; b < 2; ++b) c->planb[b].vpose = to_dev(c->p.volu_pose);
   // (both sets: the fit may cap nblocks and select the strided kernel)
   c->icp_persistent = icp_persistent_ok(c->planb[0], c->device) && icp_persistent_ok(c->planb[1], c->device);
   set_par(c, 0);

@@ -41,6 +41,12 @@ struct DevState {
   // runs: kind (frame_kind) and cam2vol = volume_pose^-1 * pose (tsdf_volume.cpp:59)
   int ray_kind;
   DevPose ray_c2v;
+  // frames begun so far (frame_begin), and integrate's vol2cam of a tracked
+  // frame (tsdf_volume.cpp:50) written by the persistent ICP's block 0 with
+  // int_tag = that frame's serial: integrate's blocks read it instead of
+  // composing the pose each (any other path leaves the tag stale)
+  unsigned frame_serial, int_tag;
+  DevPose int_v2c;
 };
 
 struct LevelGeom {
@@ -68,6 +74,7 @@ struct IcpPlan {
   // size; groups[l] is then the number of non-empty ranges)
   int stride;
   int span[kMaxLevels];
+  DevPose vpose;  // the volume pose (DevState::int_v2c)
 };
 constexpr int kIcpStrideMax = 16;
 

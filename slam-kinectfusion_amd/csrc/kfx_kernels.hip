@@ -221,6 +221,7 @@ __device__ DevPose pose_inv(const DevPose &a) {
 }
 
 __device__ __forceinline__ void frame_begin(DevState *st) {
+  st->frame_serial += 1u;
   st->mode = (st->frame_count == 1) ? MODE_BOOT : MODE_TRACK;
   st->icp_fail = 0;
   st->n_base = st->n_poses;
@@ -1032,7 +1033,14 @@ __global__ __launch_bounds__(kIcpThreads, KFX_ICP_MINB) void k_icp_track(IcpPlan
     }
   }
   if (threadIdx.x == 0) {
-    if (blockIdx.x == 0) st->icp_pose = P;
+    if (blockIdx.x == 0) {
+      st->icp_pose = P;
+      if (!fail) {  // integrate's vol2cam of this tracked frame, once (k_integrate)
+        const DevPose gp = pose_mul(st->back, P);  // frame_pose(st, log, 1)
+        st->int_v2c = pose_mul(pose_inv(gp), pl.vpose);
+        st->int_tag = st->frame_serial;
+      }
+    }
     // exit ticket: the last block out clears the slots and the counters
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     const unsigned t = __hip_atomic_fetch_add(&sy->exit, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1569,6 +1577,20 @@ __device__ __forceinline__ bool int_chunk(const VolView &v, int chunkr, int chun
 // the reference's bit for bit.
 // kCount: count-only variant (no voxel traffic) giving N_upd / N_col, the
 // algorithmic-byte inputs of the roofline.
+// RN(1/d), d = 1..256 (RN(1/1) at 0), evaluated by the compiler (IEEE
+// binary32 division, round to nearest): the same values as the per-block
+// divisions it replaces
+struct RcpTable {
+  float v[257];
+};
+constexpr RcpTable make_rcp_table() {
+  RcpTable t{};
+  t.v[0] = 1.f;
+  for (int i = 1; i < 257; ++i) t.v[i] = 1.f / (float)i;
+  return t;
+}
+__constant__ RcpTable c_rtab = make_rcp_table();
+
 template <bool kCount, bool kIdx32>
 __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(KFX_INT_OCC, KFX_INT_OCC))) void k_integrate(VolView v, LevelGeom g,
                                                    const float2 *__restrict__ dl,
@@ -1583,7 +1605,7 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
   __shared__ float rtab[257];
   __shared__ DevPose s_pose;
   __shared__ int s_kind;
-  for (int i = threadIdx.x; i < 257; i += KFX_INT_BLOCK) rtab[i] = 1.f / (float)max(1, i);
+  for (int i = threadIdx.x; i < 257; i += KFX_INT_BLOCK) rtab[i] = c_rtab.v[i];
   if (threadIdx.x == 0) {  // (inline rather than int_frame_pose: that form spills in the loop)
     if (xpose) {  // stage seam: explicit vol2cam
       s_kind = 1;
@@ -1593,7 +1615,9 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
       const int kind = frame_kind(st);
       s_kind = kind;
       DevPose gp = pose_identity();
-      if (kind != 2) {
+      if (kind == 1 && blockIdx.x != 0 && st->int_tag == st->frame_serial) {
+        s_pose = st->int_v2c;  // composed once by the persistent ICP (DevState::int_v2c)
+      } else if (kind != 2) {
         gp = frame_pose(st, log, kind);
         s_pose = pose_mul(pose_inv(gp), vpose);  // tsdf_volume.cpp:50
       }
