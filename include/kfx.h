@@ -180,14 +180,6 @@ int kfx_debug_force_icp_stall(kfx_ctx *ctx);
  * device_utils.cuh:31, tsdf_volume.cpp:24) at any volume size, so the oracle
  * can pin them at sizes it runs.  Results are identical either way. */
 int kfx_debug_force_index64(kfx_ctx *ctx, int on);
-/* Test and tuning hook for the two-phase raycast: a wave of the raycast
- * marches for cap x 1024 clock cycles, then queues its unfinished rays, which
- * groups of lanes finish (the reference loop, tsdf_volume.cu:234-258, split at
- * an arbitrary sample).  cap = 0 sends every marching ray to the second phase,
- * cap < 0 disables it.  Results are identical for every cap. */
-int kfx_debug_ray_queue(kfx_ctx *ctx, int cap);
-/* Rays the last two-phase raycast queued for its second phase (>= 0), <0 on error. */
-int kfx_debug_ray_queued(kfx_ctx *ctx);
 /* Slab contexts (SURVEY.md §8e alternative): instead of every rank running
  * the whole ICP (default), rank r accumulates the 27 products over its band
  * of each level's rows and the exact int64 partials are all-reduced (SUM)
@@ -432,10 +424,12 @@ int kfx_slab_balance(const int64_t *slice_work, int Z, int world, int *cuts);
  * (test: most pixels take the second pass).  Results are identical in every
  * mode.  The mode decides which collectives a frame's combine issues, so it is
  * one mode for the whole decomposition: on a context with a communicator the
- * call is collective (every rank calls it with the same mode; a mismatch
- * returns KFX_ERR_ARG on every rank and leaves the mode unchanged), the mode
- * held at kfx_comm_init is checked the same way, and kfx_pipeline_group
- * refuses members whose modes differ. */
+ * call is collective (every rank calls it with the same mode; a mismatch, or
+ * a mode outside 0..2 on any rank, returns KFX_ERR_ARG on every rank and
+ * leaves the mode unchanged), the mode held at kfx_comm_init is checked the
+ * same way (a mismatch there returns KFX_ERR_ARG and leaves the context
+ * without a communicator, so no frame can issue mismatched collectives), and
+ * kfx_pipeline_group refuses members whose modes differ. */
 int kfx_set_slab_bound(kfx_ctx *ctx, int mode);
 /* stored slices [zb, zb+zn), owned slices [own0, own1) */
 int kfx_slab_info(kfx_ctx *ctx, int *zb, int *zn, int *own0, int *own1);

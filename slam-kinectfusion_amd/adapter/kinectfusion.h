@@ -206,3 +206,19 @@ class kinectfusion {
 };
 
 }  // namespace kf
+
+// kf::file::exportPly (kinectfusion.h:77-83): the reference declares it ("TODO:
+// file") but never defines or calls it (main.cpp saves through
+// savePointcloud).  Here it writes the same ASCII PLY as savePointcloud
+// (kinectfusion.cpp:148-166) from a 1 x N CV_32FC3 cloud, the format
+// extracePointcloud returns.
+namespace kf {
+namespace file {
+inline void exportPly(const std::string &filename, cv::Mat pointcloud) {
+  cv::Mat p = pointcloud.isContinuous() ? pointcloud : pointcloud.clone();
+  const int64_t n = p.empty() ? 0 : (int64_t)p.rows * p.cols;
+  if (kfx_write_ply(filename.c_str(), n ? p.ptr<float>() : nullptr, n) != KFX_OK)
+    throw std::runtime_error(kfx_last_error());
+}
+}  // namespace file
+}  // namespace kf

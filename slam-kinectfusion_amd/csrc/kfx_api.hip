@@ -194,6 +194,7 @@ struct kfx_ctx {
   std::vector<HostReg> host_regs;  // kfx_register_host_buffer ranges
   hipStream_t cstream = nullptr;
   ncclComm_t comm = nullptr;      // RCCL communicator over the slab ranks (one process per GPU)
+  int *comm_chk = nullptr;        // 2 device words of the collective slab-bound check (kfx_comm_init)
   hipEvent_t xev[5]{};            // extraction pass events (kfx_get_extract_ms)
   int extract_passes = 0;         // the last extraction: 1 (single pass) or 2 (count + emit)
   int extract_mode = 1;           // kfx_set_extract_passes: 1 single pass when a buffer is given, 2 always two
@@ -221,9 +222,6 @@ int dalloc(kfx_ctx *c, void **p, size_t bytes) {
 
 #ifndef KFX_PREP_AFTER_ICP
 #define KFX_PREP_AFTER_ICP 1  // overlapped frames: next preprocess waits for this frame's ICP
-#endif
-#ifndef KFX_RAY_QCAP
-#define KFX_RAY_QCAP -1  // two-phase raycast: a wave's phase 1 in 1024-cycle units (< 0: one phase)
 #endif
 #ifndef KFX_COST_UPDATED
 #define KFX_COST_UPDATED 32  // slab balancing: weight of an updated voxel (64 = one visited slot; slice_cost)
@@ -1050,9 +1048,6 @@ static int create_impl(const kfx_intrinsics *intr, const kfx_params *params, int
   c->vol = make_vol(p, rank, world, cuts);
   // raycast wave durations of the last frame (4 waves per 16x16 block; zeroed: no hint)
   if ((r = dalloc(c, (void **)&c->vol.rdur, grid16 * 4 * sizeof(unsigned)))) return fail(r);
-  // two-phase raycast queue (zeroed: empty; kfx_internal.h rq_rec_off)
-  if ((r = dalloc(c, (void **)&c->vol.rq, rq_words(grid16, np0) * sizeof(unsigned)))) return fail(r);
-  c->vol.rqcap = KFX_RAY_QCAP;
   const size_t n = nvox(c);
   {
     // tsdf and weight in ONE allocation, weight (u8) at a fixed offset (2 MiB-
@@ -1437,29 +1432,6 @@ int kfx_debug_force_index64(kfx_ctx *c, int on) {
   }
   c->vol.force64 = on != 0;
   return KFX_OK;
-}
-
-int kfx_debug_ray_queue(kfx_ctx *c, int cap) {
-  int r = check_ctx(c);
-  if (r) return r;
-  const int v = cap < 0 ? -1 : cap;
-  if (c->vol.rqcap != v) {  // the cap is a kernel argument of captured frames
-    HIPCHK(hipStreamSynchronize(c->stream));
-    HIPCHK(hipStreamSynchronize(c->pstream));
-    destroy_graphs(c);
-    HIPCHK(hipMemset(c->vol.rq + 1, 0, sizeof(unsigned)));  // kfx_debug_ray_queued: none yet
-  }
-  c->vol.rqcap = v;
-  return KFX_OK;
-}
-
-int kfx_debug_ray_queued(kfx_ctx *c) {
-  int r = check_ctx(c);
-  if (r) return r;
-  HIPCHK(hipStreamSynchronize(c->stream));
-  unsigned n = 0;
-  HIPCHK(hipMemcpy(&n, c->vol.rq + 1, sizeof(n), hipMemcpyDeviceToHost));
-  return (int)n;
 }
 
 int kfx_set_icp_allreduce(kfx_ctx *c, int enabled) {
@@ -1873,6 +1845,9 @@ int kfx_raycast_stats(kfx_ctx *c, int64_t out[8]) {
   if (r) return r;
   if (!out) return set_err(KFX_ERR_ARG, "null out");
   HIPCHK(hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * 8, c->stream));
+  // the raycast's pose from the current state (as k_raycast_touch below), not
+  // only the last pipeline integrate's
+  launch_ray_pose(c->stream, c->st, c->pose_log, to_dev(c->p.volu_pose));
   launch_raycast(c->stream, c->vol, c->L, c->g, c->cur, c->prev, c->st, c->pose_log,
                  to_dev(c->p.volu_pose), nullptr, c->slab ? c->key_local : nullptr, c->counters);
   HIPCHK(hipGetLastError());
@@ -1971,43 +1946,53 @@ static int extract_events(kfx_ctx *c) {
 // The slab bound decides which collectives a frame's combine issues (the
 // [key | pend] MIN and the resume pass run only when bounded), so every rank of
 // a communicator must hold the same mode: checked by a MIN and a MAX
-// all-reduce of it (blocking; every rank is inside the same call).
+// all-reduce of it (blocking; every rank is inside the same call).  A rank
+// with an invalid mode enters the collective with the sentinel -1, so every
+// rank returns KFX_ERR_ARG instead of the others blocking in the all-reduce;
+// the scratch words are allocated at kfx_comm_init, so no local allocation
+// failure can skip the collective either.
 static int comm_check_slab_bound(kfx_ctx *c, int mode) {
-  int *d = nullptr;
-  HIPCHK(hipMalloc(&d, 2 * sizeof(int)));
+  int *d = c->comm_chk;
   const int h0[2] = {mode, mode};
   int h[2] = {0, 0};
   int r = KFX_OK;
-  if (hipMemcpy(d, h0, sizeof(h0), hipMemcpyHostToDevice) != hipSuccess) {
+  const bool up = hipMemcpyAsync(d, h0, sizeof(h0), hipMemcpyHostToDevice, c->stream) == hipSuccess;
+  // enter the collective even when the upload failed (its words then hold
+  // the last check's values; the error is reported after the collective)
+  ncclResult_t e = ncclGroupStart();
+  if (e == ncclSuccess) e = ncclAllReduce(d, d, 1, ncclInt32, ncclMin, c->comm, c->stream);
+  if (e == ncclSuccess) e = ncclAllReduce(d + 1, d + 1, 1, ncclInt32, ncclMax, c->comm, c->stream);
+  const ncclResult_t e2 = ncclGroupEnd();
+  if (e == ncclSuccess) e = e2;
+  if (e != ncclSuccess)
+    r = set_err(KFX_ERR_COMM, std::string("slab bound check: ") + ncclGetErrorString(e));
+  else if (hipStreamSynchronize(c->stream) != hipSuccess || hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost) != hipSuccess)
+    r = set_err(KFX_ERR_HIP, "slab bound check: download");
+  else if (!up)
     r = set_err(KFX_ERR_HIP, "slab bound check: upload");
-  } else {
-    ncclResult_t e = ncclGroupStart();
-    if (e == ncclSuccess) e = ncclAllReduce(d, d, 1, ncclInt32, ncclMin, c->comm, c->stream);
-    if (e == ncclSuccess) e = ncclAllReduce(d + 1, d + 1, 1, ncclInt32, ncclMax, c->comm, c->stream);
-    const ncclResult_t e2 = ncclGroupEnd();
-    if (e == ncclSuccess) e = e2;
-    if (e != ncclSuccess)
-      r = set_err(KFX_ERR_COMM, std::string("slab bound check: ") + ncclGetErrorString(e));
-    else if (hipStreamSynchronize(c->stream) != hipSuccess || hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost) != hipSuccess)
-      r = set_err(KFX_ERR_HIP, "slab bound check: download");
-    else if (h[0] != h[1])
-      r = set_err(KFX_ERR_ARG, "ranks differ in kfx_set_slab_bound mode (every rank must pass the same mode)");
-  }
-  (void)hipFree(d);
+  else if (h[0] < 0)
+    r = set_err(KFX_ERR_ARG, "slab bound modes are 0, 1, 2 (a rank passed another value)");
+  else if (h[0] != h[1])
+    r = set_err(KFX_ERR_ARG, "ranks differ in kfx_set_slab_bound mode (every rank must pass the same mode)");
   return r;
 }
 
 int kfx_set_slab_bound(kfx_ctx *c, int mode) {
   int r = check_ctx(c);
   if (r) return r;
-  if (mode < 0 || mode > 2) return set_err(KFX_ERR_ARG, "slab bound modes are 0, 1, 2");
+  const bool valid = mode >= 0 && mode <= 2;
+  if (c->comm) {
+    // over a communicator the call is collective: every rank passes the same
+    // mode, and every rank enters the check (an invalid mode as -1)
+    if ((r = comm_check_slab_bound(c, valid ? mode : -1))) return r;
+  } else if (!valid) {
+    return set_err(KFX_ERR_ARG, "slab bound modes are 0, 1, 2");
+  }
   if (mode != c->slab_bound) {  // captured frames hold the old passes
     HIPCHK(hipStreamSynchronize(c->stream));
     HIPCHK(hipStreamSynchronize(c->pstream));
     destroy_graphs(c);
   }
-  // over a communicator the call is collective: every rank passes the same mode
-  if (c->comm && (r = comm_check_slab_bound(c, mode))) return r;
   c->slab_bound = mode;
   return KFX_OK;
 }
@@ -2449,9 +2434,18 @@ int kfx_comm_init(kfx_ctx *c, const uint8_t id[KFX_COMM_ID_BYTES]) {
   if (c->comm) return set_err(KFX_ERR_STATE, "communicator already initialised");
   ncclUniqueId u;
   std::memcpy(&u, id, sizeof(u));
+  if (!c->comm_chk) {  // before the collective init: no later local failure skips a collective
+    HIPCHK(hipMalloc(&c->comm_chk, 2 * sizeof(int)));
+    c->allocs.push_back(c->comm_chk);
+  }
   NCCLCHK(ncclCommInitRank(&c->comm, c->world, u, c->rank));
   destroy_graphs(c);
-  return comm_check_slab_bound(c, c->slab_bound);
+  r = comm_check_slab_bound(c, c->slab_bound);
+  if (r) {  // ranks disagree: no communicator, so no frame can issue mismatched collectives
+    (void)ncclCommDestroy(c->comm);
+    c->comm = nullptr;
+  }
+  return r;
 }
 
 int kfx_pipeline_group(kfx_ctx **cs, int n, const uint8_t *bgr, const float *depth_mm) {
@@ -2564,18 +2558,32 @@ int kfx_pipeline_group(kfx_ctx **cs, int n, const uint8_t *bgr, const float *dep
   for (int k = 0; k < n; ++k)
     if (tev[k]) HIPCHK(hipEventRecord(tev[k][7], s0));
   // per-member work forked from s0 and joined back (each launch on its own device)
+  // On an error partway, the members forked so far are still joined back to
+  // s0 and member 0's device is current again, so no enqueued work is orphaned.
   auto per_member = [&](auto &&work) -> int {
-    int e;
+    int e = KFX_OK, forked = 1;
     HIPCHK(hipEventRecord(c0->ev_group, s0));
-    for (int k = 0; k < n; ++k) {
-      if ((e = check_ctx(cs[k]))) return e;
-      if (k > 0) HIPCHK(hipStreamWaitEvent(cs[k]->stream, c0->ev_group, 0));
+    for (int k = 0; k < n && !e; ++k) {
+      if ((e = check_ctx(cs[k]))) break;
+      if (k > 0 && hipStreamWaitEvent(cs[k]->stream, c0->ev_group, 0) != hipSuccess) {
+        e = set_err(KFX_ERR_HIP, "group combine: fork");
+        break;
+      }
       work(cs[k]);
-      if (k > 0) HIPCHK(hipEventRecord(cs[k]->ev_group, cs[k]->stream));
+      if (k > 0) {
+        if (hipEventRecord(cs[k]->ev_group, cs[k]->stream) != hipSuccess) {
+          // not joinable by its event: wait for the member's stream instead
+          (void)hipStreamSynchronize(cs[k]->stream);
+          e = set_err(KFX_ERR_HIP, "group combine: join record");
+          break;
+        }
+        forked = k + 1;
+      }
     }
-    if ((e = check_ctx(c0))) return e;
-    for (int k = 1; k < n; ++k) HIPCHK(hipStreamWaitEvent(s0, cs[k]->ev_group, 0));
-    return KFX_OK;
+    const int e0 = check_ctx(c0);
+    for (int k = 1; k < forked; ++k)
+      if (hipStreamWaitEvent(s0, cs[k]->ev_group, 0) != hipSuccess && !e) e = set_err(KFX_ERR_HIP, "group combine: join");
+    return e ? e : e0;
   };
   if (c0->pass1_bounded) {  // [key | pend] MIN, then the resume passes
     launch_group_reduce(s0, kin, n, kout, n, 2 * np, false);

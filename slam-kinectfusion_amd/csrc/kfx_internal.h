@@ -38,7 +38,9 @@ struct DevState {
   DevPose *log;         // the device pose log (the host keeps it current)
   DevPose back;         // log[n_poses - 1] at frame begin: the frame pose's base, one load away
   // the frame's raycast pose, written by k_integrate (block 0) before the raycast
-  // runs: kind (frame_kind) and cam2vol = volume_pose^-1 * pose (tsdf_volume.cpp:59)
+  // runs: kind (frame_kind) and cam2vol = volume_pose^-1 * pose (tsdf_volume.cpp:59).
+  // Valid right after a pipeline integrate; a raycast with no explicit pose
+  // outside a frame refreshes them first (k_ray_pose, kfx_raycast_stats).
   int ray_kind;
   DevPose ray_c2v;
   // frames begun so far (frame_begin), and integrate's vol2cam of a tracked
@@ -138,11 +140,6 @@ struct VolView {
   int iadapt;  // length-capped chunks + longest-first order (deep volumes), else geometric chunks
   int force64;  // kfx_debug_force_index64: integrate / raycast take the 64-bit-index kernels at any size
   unsigned *rdur;  // raycast: each wave's duration in the last frame (1024-cycle units; issue priority hint)
-  // Two-phase raycast: rays still marching when their wave has
-  // run rqcap x 1024 cycles go to the ray queue rq (layout: rq_rec_off) and are
-  // finished by lane groups (k_ray_tail); rqcap < 0: one phase
-  unsigned *rq;
-  int rqcap;
   __host__ __device__ size_t bocc_bytes() const { return (size_t)tiles_x * tiles_y * bw * 8; }
   __host__ __device__ size_t socc_bytes() const { return (size_t)stx * sty * sw * 4; }
   __host__ __device__ size_t local_voxels() const { return slice * (size_t)zn; }
@@ -151,15 +148,6 @@ struct VolView {
   //   index(x, y, z) = (tile(x, y) * zn + (z - zb)) * 64 + (y & 7) * 8 + (x & 7)
   __host__ __device__ size_t tile_voxels() const { return (size_t)zn * 64; }
 };
-
-// Ray queue words: [0] queued rays, [1] the last raycast's, [16, 16 + blocks) per 16x16-pixel block
-// "its resize waits for queued rays", then kRqWords per queued ray: {pixel,
-// nextp.xyz} {ray_len, tprev, tfar, sprev} {dir.xyz, 0} (16-byte aligned).
-constexpr int kRqWords = 12;
-__host__ __device__ inline size_t rq_rec_off(size_t blocks16) { return 16 + ((blocks16 + 15) & ~(size_t)15); }
-__host__ __device__ inline size_t rq_words(size_t blocks16, size_t pixels) {
-  return rq_rec_off(blocks16) + (size_t)kRqWords * pixels;
-}
 
 // ---- slab raycast combine, shared by the kernels and the host entry points
 // (kfx_slab_mask_payload / kfx_slab_expand) so a CPU test drives the same code.
@@ -278,11 +266,12 @@ void launch_raycast(hipStream_t s, VolView v, int levels, const LevelGeom *g, Fr
                     const SlabPass &sp = SlabPass{});
 // the reference raycast's distinct voxels read (out[0]) and reads (out[1]),
 // count-only (bits: one bit per stored voxel, workspace)
+void launch_ray_pose(hipStream_t s, DevState *st, const DevPose *log, DevPose vpose);
 void launch_raycast_touch(hipStream_t s, VolView v, LevelGeom g0, const DevState *st, const DevPose *log,
                           DevPose vpose, const float *xpose, uint32_t *bits, unsigned long long *out);
 // resizePointsNormals of levels >= 1 from the level-0 model maps
 void launch_resize(hipStream_t s, int levels, const LevelGeom *g, FrameView cur, FrameView prev,
-                   const DevState *st, const float *xpose, unsigned *rq = nullptr);
+                   const DevState *st, const float *xpose);
 // cross-slab combine: clear maps where the local key lost the MIN
 // out[0] += sum of per-voxel hashes, out[1] += voxels with weight > 0 (owned slices)
 void launch_checksum(hipStream_t s, VolView v, unsigned long long *out);

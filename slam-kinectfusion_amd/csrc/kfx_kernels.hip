@@ -2202,7 +2202,7 @@ __device__ unsigned long long *g_ray_iter;  // per-wave iteration records (34 u6
 #else
 constexpr bool kTrace = false;
 #endif
-template <bool kIdx32, bool kSlab, bool kStats = false, bool kQueue = false>
+template <bool kIdx32, bool kSlab, bool kStats = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((kSlab || !kIdx32) ? KFX_RAY_SLAB_OCC : KFX_RAY_OCC))) void k_raycast(VolView v, RayArgs ra, RayConsts rc,
                                                     FrameView cur, FrameView prev,
                                                     const DevState *__restrict__ st,
@@ -2229,17 +2229,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((kSlab || !
   const float *pose_src = xpose ? xpose : st->ray_c2v.R;  // R[9], t[3] (+ Rinv[9] in xpose)
   const int skind = xpose ? 1 : st->ray_kind;
   const size_t wave_id = (size_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  // two-phase march (kQ, VolView::rq): past qend (wave clock), the rays still
-  // marching are queued with their loop state for k_ray_tail
-  constexpr bool kQ = kQueue && !kSlab && !kStats;
-  const unsigned long long t_wave0 = (KFX_RAY_HINT || kQ) ? __builtin_amdgcn_s_memtime() : 0ull;
-  // the deadline as a 32-bit clock value (one register; "off" = 2^31 - 1
-  // cycles away, far beyond any launch)
-  const unsigned qend = (unsigned)t_wave0 + ((kQ && v.rq != nullptr && v.rqcap >= 0)
-                                                 ? ((unsigned)min(v.rqcap, 0x1FFFFF) << 10)
-                                                 : 0x7FFFFFFFu);
-  auto past_q = [&]() { return kQ && (int)((unsigned)__builtin_amdgcn_s_memtime() - qend) >= 0; };
-  bool queued = false;
+  const unsigned long long t_wave0 = KFX_RAY_HINT ? __builtin_amdgcn_s_memtime() : 0ull;
   if (KFX_RAY_HINT && !kSlab && !kStats && v.rdur) {
     const unsigned d = __builtin_amdgcn_readfirstlane(v.rdur[wave_id]);
     if (d >= KFX_RAY_HINT_T0 * 7 / 4) __builtin_amdgcn_s_setprio(3);
@@ -2397,29 +2387,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((kSlab || !
         live = false;
         pend = kbase;
       }
-      if (past_q()) {
-        // phase 1 over: queue the marching rays (one atomic per wave) with the
-        // loop state a lane group resumes from (kfx_internal.h rq_rec_off)
-        const unsigned long long m = __ballot(live);
-        const int first = m ? __builtin_ctzll(m) : 0;
-        unsigned base = 0u;
-        if (m && lane == first) base = atomicAdd(v.rq, (unsigned)__popcll(m));
-        base = (unsigned)__shfl((int)base, first);
-        if (live) {
-          const unsigned idx = base + (unsigned)__popcll(m & ((1ull << lane) - 1ull));
-          float4 *rec = reinterpret_cast<float4 *>(v.rq + rq_rec_off(gridDim.x)) + 3 * (size_t)idx;
-          rec[0] = make_float4(__uint_as_float((unsigned)o), nextp.x, nextp.y, nextp.z);
-          rec[1] = make_float4(ray_len, tprev, tfar, __int_as_float(sprev));
-          rec[2] = make_float4(dir.x, dir.y, dir.z, 0.f);
-          queued = true;
-          live = false;
-        }
-        break;
-      }
       if (can_skip && live && sprev >= 0) {
         uint32_t nsk = 0;
         for (;;) {
-          if (past_q()) break;  // phase 1 over: the lanes stop here
           const float cx = nextp.x * rc.vs_inv.x, cy = nextp.y * rc.vs_inv.y, cz = nextp.z * rc.vs_inv.z;
           const float lim = skip_limit(v, cx, cy, cz, dv, idv);
           if (!(lim >= 1.f)) {
@@ -2506,7 +2476,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((kSlab || !
       const unsigned long long t_i1 = __builtin_amdgcn_s_memtime();
 #endif
       if (!__any(live)) break;
-      if (past_q()) continue;  // queued at the loop's top
       int16_t raw[kR];
       unsigned pm = 0u, nm = 0u, am = 0u, ownm = 0u;
       if (kStats || kTrace) st_batches += live ? 1u : 0u;
@@ -2703,7 +2672,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((kSlab || !
   }
   if (KFX_RAY_HINT && !kSlab && !kStats && v.rdur && (threadIdx.x & 63) == 0)
     v.rdur[wave_id] = (unsigned)((__builtin_amdgcn_s_memtime() - t_wave0) >> 10);
-  if (act && !queued) {  // (queued rays: k_ray_tail writes their maps)
+  if (act) {
     if (kSlab) {  // key, pend + payload {Ts, nout} (kfx_internal.h slab combine)
       const size_t np = (size_t)g.w * g.h;
       keys[o] = key;
@@ -2718,148 +2687,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((kSlab || !
     }
   }
   if (kSlab) return;  // resize runs after the cross-slab combine (k_resize)
-  if (kQ && v.rq != nullptr && v.rqcap >= 0) {
-    // a block with queued rays resizes after k_ray_tail (k_resize over the
-    // flagged blocks); the flags are rewritten every frame
-    const int anyq = __syncthreads_or(queued ? 1 : 0);
-    if (threadIdx.x == 0) v.rq[16 + (ty0 / 16) * nbx + tx0 / 16] = anyq ? 1u : 0u;
-    if (anyq) return;
-  }
   resize_tile(ra, kind, tx0, ty0, lx, ly, vout, nout, cur, prev);
-}
-
-// ---- Phase 2 of the two-phase raycast: the rays k_raycast
-// queued when their wave ran past VolView::rqcap, each finished by a group of
-// kG lanes from its queued loop state.  Lane i reaches sample i of the window
-// with the exact result of i repeated float adds (ff_add, kfx_ffadd.h) rather
-// than by the chain, so the group takes kG samples (dense round) or kG skip
-// lookups kS samples apart (scan round) in one round trip.  The reference's
-// events depend only on consecutive samples (tsdf_volume.cu:234-258), so the
-// first event of the window (by ballot) is the ray's; its Ts, vertex and
-// normal use the phase-1 ops.  Outputs: the level-0 maps of the queued pixels.
-#ifndef KFX_RAY_TAIL_G
-#define KFX_RAY_TAIL_G 32  // lanes per queued ray
-#endif
-#ifndef KFX_RAY_TAIL_S
-#define KFX_RAY_TAIL_S 8  // samples between the lanes' lookups in a scan round
-#endif
-#ifndef KFX_RAY_TAIL_BLOCKS
-#define KFX_RAY_TAIL_BLOCKS 1280  // 5 waves per SIMD: every group resident at once
-#endif
-template <bool kIdx32, int kG, int kS>
-__global__ __launch_bounds__(256) void k_ray_tail(VolView v, RayArgs ra, RayConsts rc, FrameView prev,
-                                                  const DevState *__restrict__ st, const float *xpose) {
-  static_assert(kG == 8 || kG == 16 || kG == 32 || kG == 64, "lane groups tile the wave");
-  constexpr int kGroups = 256 / kG;
-  const unsigned n = v.rq[0];
-  const int lane = threadIdx.x & 63, gl = lane & (kG - 1), gb = lane & ~(kG - 1);
-  const unsigned long long full = kG == 64 ? ~0ull : ((1ull << kG) - 1ull);
-  auto gballot = [&](bool b) { return (__ballot(b) >> gb) & full; };
-  const LevelGeom g = ra.g[0];
-  const float *pose_src = xpose ? xpose : st->ray_c2v.R;
-  const f3 org = {pose_src[9], pose_src[10], pose_src[11]};
-  const RayMem<kIdx32> mem(v);
-  const float hx = (float)(v.X - 2), hy = (float)(v.Y - 2), hz = (float)(v.Z - 2);
-  const size_t blocks16 = (size_t)((g.w + 15) / 16) * (size_t)((g.h + 15) / 16);
-  const float4 *recs = reinterpret_cast<const float4 *>(v.rq + rq_rec_off(blocks16));
-  for (unsigned r = blockIdx.x * kGroups + threadIdx.x / kG; r < n; r += gridDim.x * kGroups) {  // group-uniform
-    const float4 q0 = recs[3 * (size_t)r], q1 = recs[3 * (size_t)r + 1], q2 = recs[3 * (size_t)r + 2];
-    const unsigned o = __float_as_uint(q0.x);
-    f3 p = {q0.y, q0.z, q0.w};  // the carried sample's position and ray_len
-    float rl = q1.x;
-    const float tfar = q1.z;
-    int sc = __float_as_int(q1.w);  // its sign (0: NaN)
-    const f3 dir = {q2.x, q2.y, q2.z};
-    const f3 vstep = mulc(dir, rc.vs);
-    const f3 dv = mulc(vstep, rc.vs_inv);
-    const f3 idv = {1.f / fabsf(dv.x), 1.f / fabsf(dv.y), 1.f / fabsf(dv.z)};
-    const bool can_skip = !isnan(dv.x + dv.y + dv.z);
-    f3 vout = {0.f, 0.f, 0.f}, nout = {0.f, 0.f, 0.f};
-    for (;;) {
-      if (can_skip && sc >= 0) {
-        // scan round: lane j looks up the box at sample j*kS; the lanes up to
-        // the first whose box clears fewer than kS samples are contiguous (each
-        // box reaches the next lane's sample), so the furthest of their clear
-        // runs is replayed (the phase-1 rule: with the carried sample >= 0 or
-        // NaN, no event can happen inside a clear box)
-        const int sj = gl * kS;
-        const f3 c = ff_add3(p, vstep, sj);
-        const float lim = skip_limit(v, c.x * rc.vs_inv.x, c.y * rc.vs_inv.y, c.z * rc.vs_inv.z, dv, idv);
-        const int nj = lim >= 1.f ? (int)fminf(lim, rc.skip_cap) : 0;
-        const unsigned long long sh = gballot(nj < kS);
-        const int f = sh ? __builtin_ctzll(sh) : kG - 1;
-        int e = (gl <= f && nj > 0) ? sj + nj : 0;
-#pragma unroll
-        for (int off = kG / 2; off > 0; off >>= 1) e = max(e, __shfl_xor(e, off));
-        if (e > 0) {
-          const float rle = ff_add_fast(rl, rc.step, e - 1);  // the last ray_len tested before an add
-          if (!(rle < tfar)) break;                       // the loop ends inside the clear run: no event
-          p = ff_add3(p, vstep, e);
-          rl = rle + rc.step;
-        }
-      }
-      // dense round: lane j takes sample j of the window (0: the carried one)
-      const f3 pj = ff_add3(p, vstep, gl);
-      const float rlj = ff_add_fast(rl, rc.step, gl);
-      const float fx = rintf(pj.x * rc.vs_inv.x), fy = rintf(pj.y * rc.vs_inv.y), fz = rintf(pj.z * rc.vs_inv.z);
-      const bool val = (fx >= 1.f) & (fx <= hx) & (fy >= 1.f) & (fy <= hy) & (fz >= 1.f) & (fz <= hz);
-      const int16_t raw = mem.ld(val, (int)fx, (int)fy, (int)fz);
-      const float tj = (float)raw * kDivShortMax;
-      const unsigned long long P = gballot(val && raw > 0), N = gballot(val && raw < 0);
-      // sample j + 1 is examined iff ray_len of sample j < tfar (monotone)
-      const unsigned long long nA = ~gballot(rlj < tfar) & full;
-      const int q = nA ? __builtin_ctzll(nA) : kG;  // samples 1..q of the window are examined
-      const unsigned long long exam = (q >= kG - 1 ? full : ((2ull << q) - 1ull)) & ~1ull;
-      const unsigned long long hitm = (P << 1) & N & exam, stopm = (N << 1) & P & exam;
-      if (hitm | stopm) {
-        const int j0 = __builtin_ctzll(hitm | stopm);
-        if ((stopm >> j0) & 1ull) break;  // tsdf_cur < 0 && tsdf_next > 0: no surface
-        const float tc = __shfl(tj, gb + j0 - 1), tn = __shfl(tj, gb + j0);
-        const float rj = __shfl(rlj, gb + j0 - 1);  // ray_len of tsdf_cur's sample
-        const float Ts = rj - (v.vs[0] * tc) / (tc - tn);  // A3 (R)
-        const f3 cvert = add(org, scl(dir, Ts));
-        // the 6 interpolations of compute_normal on lanes 0..5 of the group
-        // (one round trip), combined with its ops
-        float fk = 0.f;
-        if (gl < 6) {
-          const int ax = gl >> 1;
-          const float sgn = (gl & 1) ? -1.f : 1.f;
-          const f3 pq = {ax == 0 ? cvert.x + sgn * rc.gd.x : cvert.x, ax == 1 ? cvert.y + sgn * rc.gd.y : cvert.y,
-                         ax == 2 ? cvert.z + sgn * rc.gd.z : cvert.z};
-          if constexpr (kIdx32 && KFX_RAY_N32)
-            fk = interp32(v, make_rsrc(v.tsdf, (unsigned)(2 * v.local_voxels())), mulc(pq, rc.vs_inv));
-          else
-            fk = interp(v, mulc(pq, rc.vs_inv));
-        }
-        f3 nrm;
-        nrm.x = (__shfl(fk, gb) - __shfl(fk, gb + 1)) / rc.gd.x;
-        nrm.y = (__shfl(fk, gb + 2) - __shfl(fk, gb + 3)) / rc.gd.y;
-        nrm.z = (__shfl(fk, gb + 4) - __shfl(fk, gb + 5)) / rc.gd.z;
-        nrm = normalized(nrm);
-        if (!isnan(nrm.x * nrm.y * nrm.z)) {
-          float ri[9];
-#pragma unroll
-          for (int k = 0; k < 9; ++k) ri[k] = xpose ? xpose[12 + k] : pose_src[3 * (k % 3) + k / 3];
-          nout = rmul(ri, nrm);
-          vout = rmul(ri, sub(cvert, org));
-          break;
-        }
-        // NaN normal: the march goes on after the candidate (tsdf_volume.cu:251)
-        p = {__shfl(pj.x, gb + j0), __shfl(pj.y, gb + j0), __shfl(pj.z, gb + j0)};
-        rl = __shfl(rlj, gb + j0);
-        sc = -1;
-        continue;
-      }
-      if (q < kG) break;  // the loop ended inside the window: no event
-      p = {__shfl(pj.x, gb + kG - 1), __shfl(pj.y, gb + kG - 1), __shfl(pj.z, gb + kG - 1)};
-      rl = __shfl(rlj, gb + kG - 1);
-      sc = ((P >> (kG - 1)) & 1ull) ? 1 : (((N >> (kG - 1)) & 1ull) ? -1 : 0);
-    }
-    if (gl == 0) {
-      st3(prev.v[0], o, vout);
-      st3(prev.n[0], o, nout);
-    }
-  }
 }
 
 // SURVEY.md §8d raycast roofline input (count-only, off the frame path): the
@@ -3019,19 +2847,10 @@ __device__ void resize_tile(const RayArgs &ra, int kind, int tx0, int ty0, int l
 
 // Resize of the combined level-0 model maps (slab mode): same tiles and ops as
 // the resize fused into k_raycast.
-// Two-phase raycast (rq): only the blocks whose resize waited for queued rays,
-// and the queue is emptied for the next frame (its count kept in rq[1]).
 __global__ __launch_bounds__(256) void k_resize(RayArgs ra, FrameView cur, FrameView prev,
                                                 const DevState *__restrict__ st,
-                                                const float *xpose, unsigned *rq) {
+                                                const float *xpose) {
   const int t = blockIdx.x;
-  if (rq) {
-    if (t == 0 && threadIdx.x == 0) {
-      rq[1] = rq[0];  // kfx_debug_ray_queued
-      rq[0] = 0u;
-    }
-    if (!rq[16 + t]) return;  // block-uniform
-  }
   const int kind = xpose ? 1 : frame_kind(st);
   const LevelGeom g = ra.g[0];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -3614,7 +3433,7 @@ static int g_int_trace_waves = 0;
 extern "C" int kfx_debug_integrate_trace(unsigned long long *out, int cap) {
   const int n = std::min(cap, kfx::g_int_trace_waves);
   if (hipDeviceSynchronize() != hipSuccess) return -1;
-  if (hipMemcpy(out, kfx::g_int_trace, sizeof(unsigned long long) * 8 * n, hipMemcpyDeviceToHost) != hipSuccess)
+  if (hipMemcpy(out, kfx::g_int_trace, sizeof(unsigned long long) * 4 * n, hipMemcpyDeviceToHost) != hipSuccess)
     return -1;
   return n;
 }
@@ -4013,13 +3832,6 @@ void launch_raycast(hipStream_t s, VolView v, int levels, const LevelGeom *g, Fr
     else
       hipLaunchKernelGGL((k_raycast<false, true>), grd, dim3(256), 0, s, v, ra, rc, cur, prev, st,
                          log, vpose, xpose, keys);
-  } else if (v.rq && v.rqcap >= 0) {  // two-phase (kfx_debug_ray_queue): the march, the queued rays,
-    if (idx32)                         // then the blocks that waited for them
-      hipLaunchKernelGGL((k_raycast<true, false, false, true>), grd, dim3(256), 0, s, v, ra, rc, cur, prev, st, log,
-                         vpose, xpose, keys);
-    else
-      hipLaunchKernelGGL((k_raycast<false, false, false, true>), grd, dim3(256), 0, s, v, ra, rc, cur, prev, st,
-                         log, vpose, xpose, keys);
   } else if (idx32) {
     hipLaunchKernelGGL((k_raycast<true, false>), grd, dim3(256), 0, s, v, ra, rc, cur, prev, st, log,
                        vpose, xpose, keys);
@@ -4027,19 +3839,22 @@ void launch_raycast(hipStream_t s, VolView v, int levels, const LevelGeom *g, Fr
     hipLaunchKernelGGL((k_raycast<false, false>), grd, dim3(256), 0, s, v, ra, rc, cur, prev, st,
                        log, vpose, xpose, keys);
   }
-  if (!keys && v.rq && v.rqcap >= 0) {
-    const size_t px = (size_t)g[0].w * g[0].h;
-    const int blocks = (int)std::min<size_t>(KFX_RAY_TAIL_BLOCKS, (px * KFX_RAY_TAIL_G + 255) / 256);
-    if (idx32)
-      hipLaunchKernelGGL((k_ray_tail<true, KFX_RAY_TAIL_G, KFX_RAY_TAIL_S>), dim3(blocks), dim3(256), 0, s, v, ra,
-                         rc, prev, st, xpose);
-    else
-      hipLaunchKernelGGL((k_ray_tail<false, KFX_RAY_TAIL_G, KFX_RAY_TAIL_S>), dim3(blocks), dim3(256), 0, s, v, ra,
-                         rc, prev, st, xpose);
-    launch_resize(s, levels, g, cur, prev, st, xpose, v.rq);
-  }
 }
 
+// DevState::ray_kind / ray_c2v from the current tracking state, as the
+// frame's k_integrate writes them (kfx_raycast_stats: a raycast that is not
+// preceded by a pipeline integrate, e.g. after kfx_stage_icp_accumulate, uses
+// the current ICP pose, as k_raycast_touch does; right after a frame the
+// values are the ones integrate wrote: the bookkeeping leaves the fields
+// frame_kind / frame_pose read alone)
+__global__ void k_ray_pose(DevState *st, const DevPose *log, DevPose vpose) {
+  const int kind = frame_kind(st);
+  st->ray_kind = kind;
+  if (kind == 1) st->ray_c2v = pose_mul(pose_inv(vpose), frame_pose(st, log, 1));  // tsdf_volume.cpp:59
+}
+void launch_ray_pose(hipStream_t s, DevState *st, const DevPose *log, DevPose vpose) {
+  hipLaunchKernelGGL(k_ray_pose, dim3(1), dim3(1), 0, s, st, log, vpose);
+}
 void launch_raycast_touch(hipStream_t s, VolView v, LevelGeom g0, const DevState *st, const DevPose *log,
                           DevPose vpose, const float *xpose, uint32_t *bits, unsigned long long *out) {
   RayConsts rc;
@@ -4057,12 +3872,12 @@ void launch_raycast_touch(hipStream_t s, VolView v, LevelGeom g0, const DevState
 }
 
 void launch_resize(hipStream_t s, int levels, const LevelGeom *g, FrameView cur, FrameView prev,
-                   const DevState *st, const float *xpose, unsigned *rq) {
+                   const DevState *st, const float *xpose) {
   RayArgs ra{};
   ra.levels = levels;
   for (int l = 0; l < levels; ++l) ra.g[l] = g[l];
   dim3 grd(((g[0].w + 15) / 16) * ((g[0].h + 15) / 16));
-  hipLaunchKernelGGL(k_resize, grd, dim3(256), 0, s, ra, cur, prev, st, xpose, rq);
+  hipLaunchKernelGGL(k_resize, grd, dim3(256), 0, s, ra, cur, prev, st, xpose);
 }
 
 void launch_render(hipStream_t s, const float *vmap, const float *nmap, int n, const DevState *st,

@@ -1,5 +1,6 @@
 // main.cpp's use of kf::kinectfusion (main.cpp:54-105), against the adapter:
-// construction from default_params, pipeline, render, extraction + PLY,
+// construction from default_params, pipeline, render, extraction + PLY
+// (savePointcloud and kf::file::exportPly),
 // reset, pose_record, release.  Compiled and linked by tests/test_abi.py.
 #include <fstream>
 #include <iostream>
@@ -17,6 +18,7 @@ int main(int argc, char **argv) {
     cv::Mat img = kinfu.getRenderMap(kf::kinectfusion::PHONG);
     if (kinfu.frame_count % 5 == 0) kinfu.extracePointcloud();
     kinfu.savePointcloud(argc > 1 ? argv[1] : "/dev/null");
+    kf::file::exportPly(argc > 2 ? argv[2] : "/dev/null", kinfu.extracePointcloud());
     std::cout << kinfu.getCurCameraPose().matrix(0, 0) << " " << kinfu.pose_record.size() << img.rows << std::endl;
     kinfu.reset();
     kinfu.release();

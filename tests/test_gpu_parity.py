@@ -125,7 +125,7 @@ def test_icp_track_matches_oracle(dist, angle, seq_vga):
         assert st == 0
     # the double cos/sin of the Rodrigues step are the only non-IEEE-basic ops
     if st == 0:
-        assert np.abs(gpose.matrix() - opose.matrix()).max() <= 1e-6
+        assert np.abs(gpose.matrix() - opose.matrix()).max() == 0
     kf.close()
 
 
@@ -152,7 +152,7 @@ def test_icp_track_720p_strided_matches_oracle():
                                PA(*[fptr(a) for a in prev[1]]), PA(*[fptr(a) for a in prev[2]]),
                                C.byref(I), C.byref(p), C.byref(opose))
     assert rc == KFX_OK and st == 0
-    assert np.abs(gpose.matrix() - opose.matrix()).max() <= 1e-6
+    assert np.abs(gpose.matrix() - opose.matrix()).max() == 0
     assert kf.set_icp_persistent(False)  # True: the persistent path was the one in use
     kf.close()
 
@@ -234,22 +234,19 @@ def test_c3_pipeline_two_frames_match_oracle(seq_vga):
     gp, op = kf.pose_record, pipe.poses()
     assert gp.shape == op.shape == (2, 4, 4)
     err = np.abs(gp - op).max()
-    assert err <= 1e-6, err  # 0 measured at 128^3 / 512^3 (Rodrigues cos/sin: <= 1 ulp in double)
-    if err == 0:
-        for l in range(3):
-            _, gv, gn = kf.frame_maps(KFX_FRAME_PREV, l)
-            assert feq(gv, pipe.map(1, 1, l)), f"vmap level {l}: {mismatch(gv, pipe.map(1, 1, l))} differ"
-            assert feq(gn, pipe.map(1, 2, l)), f"nmap level {l}"
-        rng = np.random.default_rng(11)
-        cols = np.unique(np.stack([rng.integers(0, n, 3000), rng.integers(0, n, 3000)], 1).astype(np.int32), axis=0)
-        gt_, gw, gc = kf.download_columns(cols)
-        ot, ow, oc = pipe.volume()
-        idx = (cols[:, 0][:, None] + n * cols[:, 1][:, None] + n * n * np.arange(n, dtype=np.int64)[None, :])
-        assert np.array_equal(gt_, ot[idx]) and np.array_equal(gw, ow[idx])
-        assert np.array_equal(gc.reshape(-1, n, 4), oc.reshape(-1, 4)[idx])
-        assert (gw > 0).sum() > 10000
-    else:  # a last-ulp Rodrigues difference: the maps / volume are not comparable bit for bit
-        pytest.xfail(f"pose differs from the oracle by {err:.3g} (<= 1e-6): maps and volume not compared")
+    assert err == 0, err  # bit-exact: every stage, the Rodrigues cos/sin included
+    for l in range(3):
+        _, gv, gn = kf.frame_maps(KFX_FRAME_PREV, l)
+        assert feq(gv, pipe.map(1, 1, l)), f"vmap level {l}: {mismatch(gv, pipe.map(1, 1, l))} differ"
+        assert feq(gn, pipe.map(1, 2, l)), f"nmap level {l}"
+    rng = np.random.default_rng(11)
+    cols = np.unique(np.stack([rng.integers(0, n, 3000), rng.integers(0, n, 3000)], 1).astype(np.int32), axis=0)
+    gt_, gw, gc = kf.download_columns(cols)
+    ot, ow, oc = pipe.volume()
+    idx = (cols[:, 0][:, None] + n * cols[:, 1][:, None] + n * n * np.arange(n, dtype=np.int64)[None, :])
+    assert np.array_equal(gt_, ot[idx]) and np.array_equal(gw, ow[idx])
+    assert np.array_equal(gc.reshape(-1, n, 4), oc.reshape(-1, 4)[idx])
+    assert (gw > 0).sum() > 10000
     kf.close()
 
 
@@ -260,7 +257,7 @@ def test_720p_pipeline_matches_oracle():
     This pins the A2 ICP floor grid at 720p (rows 704 / 352 / 160 of 720 / 360
     / 180; rigid_icp.cu:135-139), the strided persistent ICP (k_icp_track<true>:
     level 0 has more pixel groups than the co-resident grid), and the 720p
-    raycast + resize.  Poses (tolerance 1e-6, 0 expected), every level of the
+    raycast + resize.  Poses identical, every level of the
     raycast model maps bit for bit, and the whole volume bit for bit."""
     intr = synth.Intrinsics.hd720()
     L = 4.096
@@ -275,10 +272,8 @@ def test_720p_pipeline_matches_oracle():
     gp, op = kf.pose_record, pipe.poses()
     assert gp.shape == op.shape == (len(dep), 4, 4)
     err = float(np.abs(gp - op).max())
-    assert err <= 1e-6, err
+    assert err == 0, err
     assert np.abs(gp[-1] - np.eye(4)).max() > 1e-3  # the camera moved: ICP did work
-    if err != 0:
-        pytest.xfail(f"pose differs from the oracle by {err:.3g} (<= 1e-6): maps and volume not compared")
     for l in range(3):
         _, gv, gn = kf.frame_maps(KFX_FRAME_PREV, l)
         assert feq(gv, pipe.map(1, 1, l)), f"vmap level {l}: {mismatch(gv, pipe.map(1, 1, l))} differ"
@@ -298,7 +293,7 @@ def test_c4_geometry_pipeline_matches_oracle():
     """BASELINE C4's single volume (640x480, 1024^3 @ 2 mm: 2^30 voxels, the
     geometry the 8-slab split reproduces) through the whole pipeline against
     the serial oracle, 2 frames (bootstrap + one tracked: ICP over the 1024^3
-    raycast maps): the tracked pose (tolerance 1e-6, 0 expected), every level
+    raycast maps): the tracked pose (identical), every level
     of the raycast model maps bit for bit, and 4000 volume columns bit for bit
     (the oracle's 8.6 GB volume is read in place).  The oracle takes about 30 s
     a frame at this size."""
@@ -317,9 +312,7 @@ def test_c4_geometry_pipeline_matches_oracle():
     gp, op = kf.pose_record, pipe.poses()
     assert gp.shape == op.shape == (2, 4, 4)
     err = float(np.abs(gp - op).max())
-    assert err <= 1e-6, err
-    if err != 0:
-        pytest.xfail(f"pose differs from the oracle by {err:.3g} (<= 1e-6): maps and volume not compared")
+    assert err == 0, err
     for l in range(3):
         _, gv, gn = kf.frame_maps(KFX_FRAME_PREV, l)
         assert feq(gv, pipe.map(1, 1, l)), f"vmap level {l}: {mismatch(gv, pipe.map(1, 1, l))} differ"
@@ -340,14 +333,11 @@ def test_c4_geometry_pipeline_matches_oracle():
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.skipif(os.environ.get("KFX_SLOW_TESTS") != "1", reason="2-3 minutes of oracle work and 69 GB of host "
-                    "memory: KFX_SLOW_TESTS=1 (record: profiles/r05_c5_geometry_oracle_test.log)")
 def test_c5_geometry_poses_match_oracle():
     """BASELINE C5's single volume (1280x720, 2048^3 @ 2 mm: 2^33 voxels, the
     64-bit-index integrate and raycast) through the whole pipeline against the
     serial oracle (69 GB of host memory), 2 frames: the tracked pose computed
-    by the GPU's own ICP over its own 2048^3 raycast (tolerance 1e-6, 0
-    expected) and every level of the raycast model maps bit for bit.  About
+    by the GPU's own ICP over its own 2048^3 raycast (bit-exact) and every level of the raycast model maps bit for bit.  About
     140 s on the GPU box (the oracle), so opt-in: a silent test that long can
     pass for a hung one."""
     intr = synth.Intrinsics.hd720()
@@ -365,9 +355,7 @@ def test_c5_geometry_poses_match_oracle():
     gp, op = kf.pose_record, pipe.poses()
     assert gp.shape == op.shape == (2, 4, 4)
     err = float(np.abs(gp - op).max())
-    assert err <= 1e-6, err
-    if err != 0:
-        pytest.xfail(f"pose differs from the oracle by {err:.3g} (<= 1e-6): maps not compared")
+    assert err == 0, err
     for l in range(3):
         _, gv, gn = kf.frame_maps(KFX_FRAME_PREV, l)
         assert feq(gv, pipe.map(1, 1, l)), f"vmap level {l}: {mismatch(gv, pipe.map(1, 1, l))} differ"
@@ -376,18 +364,13 @@ def test_c5_geometry_poses_match_oracle():
     del pipe  # the oracle's 69 GB volume
 
 
-@pytest.mark.parametrize("cap", [None, 0, 2, -1])
-def test_raycast_bit_exact(cap, seq_qvga):
+def test_raycast_bit_exact(seq_qvga):
     """The raycast against the oracle's (tsdf_volume.cu:210-260) at every map
-    level; cap: the two-phase split (kfx_debug_ray_queue: None = the default,
-    0 = every ray finished by the lane groups of k_ray_tail, 2 = split a few
-    thousand cycles in, -1 = one phase)."""
+    level."""
     bgr, dep, gt = seq_qvga
     intr = synth.Intrinsics.qvga()
     I = Intrinsics.from_any(intr)
     kf, p = make(intr, dims=128)
-    if cap is not None:
-        kf.debug_ray_queue(cap)
     vol = O.Volume((128,) * 3, (L_VOL,) * 3)
     for k in (0, 1, 2):
         d = dep[k].astype(np.float32)
@@ -405,54 +388,10 @@ def test_raycast_bit_exact(cap, seq_qvga):
         assert feq(gv, ov), f"vmap: {mismatch(gv, ov)} differ"
         assert feq(gn, on), f"nmap: {mismatch(gn, on)} differ"
         assert (ov[..., 2] > 0).mean() > 0.5
-        if cap == 0:  # every ray that entered the volume went to the second phase
-            assert kf.debug_ray_queued() > 0.5 * ov[..., 0].size
-        elif cap == -1:
-            assert kf.debug_ray_queued() == 0
         for l in (1, 2):
             ov, on = O.resize_points_normals(ov, on)
             _, gv, gn = kf.frame_maps(KFX_FRAME_PREV, l)
             assert feq(gv, ov) and feq(gn, on), f"level {l}"
-    kf.close()
-
-
-@pytest.mark.timeout(300)
-def test_two_phase_raycast_c2_matches_one_phase(seq_vga):
-    """BASELINE C2 (640x480, 512^3 @ 4 mm) after tracked frames: the raycast
-    split into two phases at several points (every ray queued, a few, the
-    default) gives the one-phase maps bit for bit at every level (the one-phase
-    raycast is pinned to the oracle at C2 by test_index64_kernels_match_oracle
-    and the pipeline tests), and the queue holds the rays the cap implies; the
-    same for the 64-bit-index kernels."""
-    bgr, dep, _ = seq_vga
-    intr = synth.Intrinsics.vga()
-    kf, p = make(intr, dims=512)
-    for k in range(4):
-        assert kf.pipeline(bgr[k], dep[k].astype(np.float32)) == KFX_OK
-    cam2vol = O.pose_mul(O.pose_inv(p.volu_pose), Pose.from_matrix(kf.pose_record[-1].astype(np.float32)))
-    Rinv = cam2vol.matrix()[:3, :3].T.copy()
-    maps, queued = {}, {}
-    for cap in (-1, 0, 4, 40, 90):
-        kf.debug_ray_queue(cap)
-        kf.stage_raycast(cam2vol, Rinv)
-        queued[cap] = kf.debug_ray_queued()
-        maps[cap] = [kf.frame_maps(KFX_FRAME_PREV, l)[1:] for l in range(3)]
-    ref = maps[-1]
-    assert (ref[0][0][..., 2] > 0).mean() > 0.5
-    for cap in (0, 4, 40, 90):
-        for l in range(3):
-            assert feq(maps[cap][l][0], ref[l][0]), f"cap {cap} vmap level {l}: {mismatch(maps[cap][l][0], ref[l][0])}"
-            assert feq(maps[cap][l][1], ref[l][1]), f"cap {cap} nmap level {l}: {mismatch(maps[cap][l][1], ref[l][1])}"
-    assert queued[-1] == 0 and queued[0] > 0.5 * 640 * 480 and queued[0] >= queued[4] >= queued[40] > 0, queued
-    # the 64-bit-index kernels (kfx_debug_force_index64) split the same way
-    kf.debug_force_index64(True)
-    for cap in (0, 40):
-        kf.debug_ray_queue(cap)
-        kf.stage_raycast(cam2vol, Rinv)
-        assert kf.debug_ray_queued() > 0
-        for l in range(3):
-            _, gv, gn = kf.frame_maps(KFX_FRAME_PREV, l)
-            assert feq(gv, ref[l][0]) and feq(gn, ref[l][1]), f"index64 cap {cap} level {l}"
     kf.close()
 
 
@@ -476,17 +415,15 @@ def test_pipeline_matches_oracle(which, seq_qvga, seq_vga):
     assert kf.frame_count == pipe.frame_count == len(dep) + 1
     gp, op = kf.pose_record, pipe.poses()
     assert gp.shape == op.shape == (len(dep), 4, 4)
-    # tolerance: 0 if every stage is bit-exact; 1e-6 absorbs a last-ulp
-    # difference of the double cos/sin inside the Rodrigues update
+    # bar: every stage bit-exact, so the poses are identical (0 difference)
     err = np.abs(gp - op).max()
-    assert err <= 1e-6, err
-    if err == 0:
-        t, w, c = kf.volume_soa()
-        ot, ow, oc = pipe.volume()
-        assert np.array_equal(t, ot) and np.array_equal(w, ow) and np.array_equal(c, oc)
-        for l in range(3):
-            _, gv, gn = kf.frame_maps(KFX_FRAME_PREV, l)
-            assert feq(gv, pipe.map(1, 1, l)) and feq(gn, pipe.map(1, 2, l))
+    assert err == 0, err
+    t, w, c = kf.volume_soa()
+    ot, ow, oc = pipe.volume()
+    assert np.array_equal(t, ot) and np.array_equal(w, ow) and np.array_equal(c, oc)
+    for l in range(3):
+        _, gv, gn = kf.frame_maps(KFX_FRAME_PREV, l)
+        assert feq(gv, pipe.map(1, 1, l)) and feq(gn, pipe.map(1, 2, l))
     kf.close()
 
 
@@ -573,7 +510,7 @@ def test_icp_watchdog_stall_switches_to_cooperative_launch(seq_qvga):
         pipe.process(bgr[k], d)
     op = pipe.poses()
     assert kf.pose_record.shape == op.shape and n == 1
-    assert np.abs(kf.pose_record - op).max() <= 1e-6
+    assert np.abs(kf.pose_record - op).max() == 0
     kf.close()
 
 
@@ -716,7 +653,7 @@ def test_full_size_pipeline_512(seq_vga):
     for k in range(n):
         assert pipe.process(bgr[k], dep[k].astype(np.float32)) == 0
     gp, op = kf.pose_record, pipe.poses()
-    assert np.abs(gp - op).max() <= 1e-6
+    assert np.abs(gp - op).max() == 0
     # A3 bias bounds accuracy to ~2 voxels (8 mm) against the analytic truth
     assert np.abs(gp[:, :3, 3] - gt[:n, :3, 3]).max() < 0.012
     kf.close()
@@ -750,7 +687,7 @@ def test_index64_kernels_match_oracle(which, seq_qvga, seq_vga):
     forced at sizes the oracle runs (kfx_debug_force_index64): 128^3 QVGA and
     BASELINE C2 (640x480, 512^3 @ 4 mm) through the whole pipeline against
     O.Pipeline — poses, every level of the raycast model maps and the whole
-    volume bit for bit.  Pose tolerance 1e-6 (0 expected, as everywhere)."""
+    volume bit for bit.  Poses identical (0 difference, as everywhere)."""
     if which == "qvga128":
         bgr, dep, _ = seq_qvga
         intr, dims, n = synth.Intrinsics.qvga(), 128, 6
@@ -767,10 +704,8 @@ def test_index64_kernels_match_oracle(which, seq_qvga, seq_vga):
     gp, op = kf.pose_record, pipe.poses()
     assert gp.shape == op.shape == (n, 4, 4)
     err = float(np.abs(gp - op).max())
-    assert err <= 1e-6, err
+    assert err == 0, err
     assert np.abs(gp[-1] - np.eye(4)).max() > 1e-3  # tracked frames: the raycast maps fed ICP
-    if err != 0:
-        pytest.xfail(f"pose differs from the oracle by {err:.3g} (<= 1e-6): maps and volume not compared")
     for l in range(3):
         _, gv, gn = kf.frame_maps(KFX_FRAME_PREV, l)
         assert feq(gv, pipe.map(1, 1, l)), f"vmap level {l}: {mismatch(gv, pipe.map(1, 1, l))} differ"
@@ -785,5 +720,5 @@ def test_index64_kernels_match_oracle(which, seq_qvga, seq_vga):
     kf.debug_force_index64(False)
     d = dep[n].astype(np.float32)
     assert kf.pipeline(bgr[n], d) == pipe.process(bgr[n], d) == KFX_OK
-    assert np.abs(kf.pose_record - pipe.poses()).max() <= 1e-6
+    assert np.abs(kf.pose_record - pipe.poses()).max() == 0
     kf.close()

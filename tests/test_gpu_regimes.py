@@ -13,8 +13,8 @@ round" item 1) and at the BASELINE sizes where round 1 only self-checked:
   column by column against the oracle through kfx_download_columns;
 - C4 (1024^3 @ 2 mm) as 8 Z-slabs against the single volume.
 
-Bar: bit-exact (float maps by bit pattern, NaN positions equal); poses <= 1e-6
-(0 when every stage is bit-exact).
+Bar: bit-exact (float maps by bit pattern, NaN positions equal); poses
+identical (every stage is bit-exact).
 """
 import numpy as np
 import pytest
@@ -171,7 +171,7 @@ def test_pipeline_80_frames_saturates_like_oracle():
         assert pipe.process(bgr[i], d) == 0
     gp, op = kf.pose_record, pipe.poses()
     assert gp.shape == op.shape == (80, 4, 4)
-    assert np.abs(gp - op).max() <= 1e-6
+    assert np.abs(gp - op).max() == 0
     t, w, c = kf.volume_soa()
     ot, ow, oc = pipe.volume()
     assert np.array_equal(t, ot), f"tsdf: {(t != ot).sum()} voxels differ"
@@ -198,7 +198,7 @@ def test_c2_full_volume_and_maps():
         assert kf.pipeline(bgr[k], d) == KFX_OK
         assert pipe.process(bgr[k], d) == 0
     gp, op = kf.pose_record, pipe.poses()
-    assert np.abs(gp - op).max() <= 1e-6
+    assert np.abs(gp - op).max() == 0
     for l in range(3):
         _, gv, gn = kf.frame_maps(KFX_FRAME_PREV, l)
         assert feq(gv, pipe.map(1, 1, l)), f"vmap level {l}: {nbad(gv, pipe.map(1, 1, l))} differ"

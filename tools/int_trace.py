@@ -29,7 +29,10 @@ lib = kfx.lib()
 buf = (C.c_uint64 * (4 * 65536))()
 n = lib.kfx_debug_integrate_trace(buf, 65536)
 a = np.frombuffer(buf, dtype=np.uint64)[: 4 * n].reshape(n, 4).astype(np.int64)
+launched = n
 a = a[a[:, 1] > 0]
+print(f"launched waves {launched}  with work {len(a)}  empty {launched - len(a)} "
+      f"({(launched - len(a)) / max(launched, 1):.3f})")
 t0 = a[:, 0].min()
 st, en = (a[:, 0] - t0) * 10, (a[:, 1] - t0) * 10  # ns
 dur = en - st
