@@ -173,6 +173,39 @@ __device__ __forceinline__ pf2 sqrt_rn2(pf2 x) {
   return pfma(pfma(-s0, s0, x), pf2{0.5f, 0.5f} * y, s0);
 }
 
+// Integrate's voxel pairs (ipf2): packed FP32 (KFX_INT_PK 1: v_pk_* ops,
+// each 4 cycles per wave on gfx950, tools/valu_calib.hip) or two scalar
+// operations per pair (0: 2 cycles each, no register moves to pair operands).
+#ifndef KFX_INT_PK
+#define KFX_INT_PK 0  // scalar pairs: C2 integrate 0.190 -> 0.178 ms with -fno-slp-vectorize
+#endif
+#if KFX_INT_PK
+typedef pf2 ipf2;
+#else
+struct ipf2 {
+  float x, y;
+  __device__ __forceinline__ float operator[](int k) const { return k ? y : x; }
+};
+__device__ __forceinline__ ipf2 operator+(ipf2 a, ipf2 b) { return {a.x + b.x, a.y + b.y}; }
+__device__ __forceinline__ ipf2 operator-(ipf2 a, ipf2 b) { return {a.x - b.x, a.y - b.y}; }
+__device__ __forceinline__ ipf2 operator*(ipf2 a, ipf2 b) { return {a.x * b.x, a.y * b.y}; }
+__device__ __forceinline__ ipf2 operator-(ipf2 a) { return {-a.x, -a.y}; }
+__device__ __forceinline__ ipf2 pfma(ipf2 a, ipf2 b, ipf2 c) { return {fmaf(a.x, b.x, c.x), fmaf(a.y, b.y, c.y)}; }
+__device__ __forceinline__ ipf2 rcp_rn2(ipf2 d) {
+  const ipf2 r = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  return pfma(pfma(-d, r, ipf2{1.f, 1.f}), r, r);
+}
+__device__ __forceinline__ ipf2 div_rn2(ipf2 x, ipf2 d, ipf2 y) {
+  const ipf2 q0 = x * y;
+  return pfma(pfma(-q0, d, x), y, q0);
+}
+__device__ __forceinline__ ipf2 sqrt_rn2(ipf2 x) {
+  const ipf2 y = {__builtin_amdgcn_rsqf(x.x), __builtin_amdgcn_rsqf(x.y)};
+  const ipf2 s0 = x * y;
+  return pfma(pfma(-s0, s0, x), ipf2{0.5f, 0.5f} * y, s0);
+}
+#endif
+
 // Pixel coordinate rn((a / d) * f + c) as a float, with a / d from one
 // reciprocal y = RN(1/d) shared by both image axes: div_rn(a, d, y) is the
 // correctly rounded quotient (Markstein; checked on 2e10 random general pairs,
@@ -1736,11 +1769,11 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
       static_assert(kB % 2 == 0, "voxel pairs");
 #pragma unroll
       for (int j = 0; j < kB; j += 2) {
-        const pf2 pz = {p[j].z, p[j + 1].z};
-        const pf2 yv = rcp_rn2(pz);
-        const pf2 px = {p[j].x, p[j + 1].x}, py = {p[j].y, p[j + 1].y};
-        const pf2 uu = div_rn2(px, pz, yv) * pf2{g.fx, g.fx} + pf2{g.cx, g.cx};
-        const pf2 vv = div_rn2(py, pz, yv) * pf2{g.fy, g.fy} + pf2{g.cy, g.cy};
+        const ipf2 pz = {p[j].z, p[j + 1].z};
+        const ipf2 yv = rcp_rn2(pz);
+        const ipf2 px = {p[j].x, p[j + 1].x}, py = {p[j].y, p[j + 1].y};
+        const ipf2 uu = div_rn2(px, pz, yv) * ipf2{g.fx, g.fx} + ipf2{g.cx, g.cx};
+        const ipf2 vv = div_rn2(py, pz, yv) * ipf2{g.fy, g.fy} + ipf2{g.cy, g.cy};
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
           // uu, vv are finite here (|vc| components in {0} u [2^-40, 2^40]).
@@ -1777,7 +1810,7 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
       for (int j = 0; j < kB; j += 2) {
         // d - il |vc| = -(il |vc| - d) exactly (RN is odd-symmetric); only the
         // sign of a zero sdf can differ, and no result depends on it
-        const pf2 sd = pf2{d[j].x, d[j + 1].x} - pf2{d[j].y, d[j + 1].y} * sqrt_rn2(pf2{n2[j], n2[j + 1]});
+        const ipf2 sd = ipf2{d[j].x, d[j + 1].x} - ipf2{d[j].y, d[j + 1].y} * sqrt_rn2(ipf2{n2[j], n2[j + 1]});
         sdf[j] = sd.x;
         sdf[j + 1] = sd.y;
       }
@@ -1824,12 +1857,12 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
     int qv[kB];
 #pragma unroll
     for (int j = 0; j < kB; j += 2) {
-      const pf2 tq = div_rn2(pf2{sdf[j], sdf[j + 1]}, pf2{trunc, trunc}, pf2{v.inv_trunc, v.inv_trunc});
-      const pf2 ts = {fminf(1.f, tq.x), fminf(1.f, tq.y)};
-      const pf2 pt = pf2{(float)t0[j], (float)t0[j + 1]} * pf2{kDivShortMax, kDivShortMax};
-      const pf2 pw = {(float)w0[j], (float)w0[j + 1]};
-      const pf2 nt = div_rn2(pfma(pt, pw, ts), pw + pf2{1.f, 1.f}, pf2{rtab[w0[j] + 1], rtab[w0[j + 1] + 1]}) *
-                     pf2{(float)kShortMax, (float)kShortMax};
+      const ipf2 tq = div_rn2(ipf2{sdf[j], sdf[j + 1]}, ipf2{trunc, trunc}, ipf2{v.inv_trunc, v.inv_trunc});
+      const ipf2 ts = {fminf(1.f, tq.x), fminf(1.f, tq.y)};
+      const ipf2 pt = ipf2{(float)t0[j], (float)t0[j + 1]} * ipf2{kDivShortMax, kDivShortMax};
+      const ipf2 pw = {(float)w0[j], (float)w0[j + 1]};
+      const ipf2 nt = div_rn2(pfma(pt, pw, ts), pw + ipf2{1.f, 1.f}, ipf2{rtab[w0[j] + 1], rtab[w0[j + 1] + 1]}) *
+                     ipf2{(float)kShortMax, (float)kShortMax};
 #pragma unroll
       for (int k = 0; k < 2; ++k) qv[j + k] = max(-kShortMax, min(kShortMax, (int)nt[k]));
     }
