@@ -470,8 +470,12 @@ def issue_figures(sq, kernel):
     q = (sq or {}).get(kernel)
     if not q:
         return None
-    return {k: q.get(k) for k in ("valu_issue_frac_2cyc", "valu_active_frac", "valu_insts_per_wave",
-                                  "wave_cycles_split", "kernel_cycles")}
+    # valu_busy_frac_bounds: VALU issue cycles / SIMD-cycles, bracketed by the
+    # calibration of SQ_INSTS_VALU / SQ_ACTIVE_INST_VALU (tools/traffic.py
+    # sq_issue, profiles/r06_valu_calib.json); records measured before it carry
+    # none (their valu_active_frac is not a fraction of the SIMD's cycles)
+    return {k: q.get(k) for k in ("valu_issue_frac_2cyc", "valu_busy_frac_bounds", "valu_insts_per_wave",
+                                  "wave_cycles_split", "kernel_cycles") if k in q}
 
 
 def single_record(a, name, intr, n, L, frames, D, local, traffic_path=None):

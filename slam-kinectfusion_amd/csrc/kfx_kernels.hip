@@ -176,6 +176,9 @@ __device__ __forceinline__ pf2 sqrt_rn2(pf2 x) {
 // Integrate's voxel pairs (ipf2): packed FP32 (KFX_INT_PK 1: v_pk_* ops,
 // each 4 cycles per wave on gfx950, tools/valu_calib.hip) or two scalar
 // operations per pair (0: 2 cycles each, no register moves to pair operands).
+#ifndef KFX_INT_BSKIP
+#define KFX_INT_BSKIP 0  // integrate: skip a batch's loads and update when no voxel of the wave passes
+#endif
 #ifndef KFX_INT_PK
 #define KFX_INT_PK 0  // scalar pairs: C2 integrate 0.190 -> 0.178 ms with -fno-slp-vectorize
 #endif
@@ -1836,6 +1839,17 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
         }
       continue;
     }
+#if KFX_INT_BSKIP
+    // a batch in which no voxel of any lane passes (behind the surfaces, out
+    // of the image): no loads, update arithmetic or stores (wave-uniform)
+    bool anyok = false;
+#pragma unroll
+    for (int j = 0; j < kB; ++j) anyok = anyok | ok[j];
+    if (!__any(anyok)) {
+      iz += (Idx)kB * slice;
+      continue;
+    }
+#endif
     // tsdf/weight of the voxels that pass (issuing them with the depth
     // gathers, before the depth test, measured slower: the rejected voxels'
     // extra reads cost more than the saved round trip)

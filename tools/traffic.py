@@ -148,18 +148,29 @@ def per_counter(root):
 def sq_issue(d):
     """Issue figures of one kernel from the SQ pass (means per dispatch).
     GRBM_GUI_ACTIVE sums the busy cycles of the 8 XCDs, so the dispatch spans
-    GRBM_GUI_ACTIVE / 8 shader cycles on each of the 1024 SIMDs; a wave64 VALU
-    instruction occupies its SIMD for 2 cycles (MI355X_MICROARCH.md, wave
-    scheduling), SQ_ACTIVE_INST_VALU counts quad-cycles summed over waves."""
+    GRBM_GUI_ACTIVE / 8 shader cycles on each of the 1024 SIMDs.  VALU issue
+    cycles, calibrated on known instruction streams (tools/valu_calib.hip,
+    profiles/r06_valu_calib.json): a wave64 v_add_f32 occupies its SIMD for 2
+    cycles, v_pk_fma_f32 and v_mad_u32_u24 for 4, v_rcp_f32 for 8, and
+    SQ_ACTIVE_INST_VALU (A) counts 1 for the first three, 2 for v_rcp, while
+    SQ_INSTS_VALU (I) counts 1 each.  With n2 + n4 = 2I - A instructions of 2 or
+    4 cycles and n8 = A - I of 8, the issue cycles lie in [6A - 4I, 4A]; their
+    fraction of the SIMD-cycles is the bracket reported (never above 1: a
+    SIMD issues at most one VALU instruction at a time).  The round-5 figure
+    4A / SIMD-cycles (`valu_active_frac`) counted every 2-cycle instruction
+    as 4 and read above 1 on C3 / C5."""
     cyc = d.get("GRBM_GUI_ACTIVE", 0.0) / 8.0
     rec = {c: d[c] for c in sorted(d) if c != "dispatches"}
     rec["dispatches"] = d.get("dispatches")
     if cyc > 0:
         rec["kernel_cycles"] = cyc
-        if "SQ_INSTS_VALU" in d:
-            rec["valu_issue_frac_2cyc"] = round(2.0 * d["SQ_INSTS_VALU"] / (N_SIMD * cyc), 4)
-        if "SQ_ACTIVE_INST_VALU" in d:
-            rec["valu_active_frac"] = round(4.0 * d["SQ_ACTIVE_INST_VALU"] / (N_SIMD * cyc), 4)
+        I, A = d.get("SQ_INSTS_VALU"), d.get("SQ_ACTIVE_INST_VALU")
+        if I is not None:
+            rec["valu_issue_frac_2cyc"] = round(2.0 * I / (N_SIMD * cyc), 4)
+        if I is not None and A is not None:
+            lo = max(2.0 * I, 6.0 * A - 4.0 * I) / (N_SIMD * cyc)
+            hi = 4.0 * A / (N_SIMD * cyc)
+            rec["valu_busy_frac_bounds"] = [round(min(lo, 1.0), 4), round(min(hi, 1.0), 4)]
     if d.get("SQ_WAVES"):
         rec["valu_insts_per_wave"] = round(d.get("SQ_INSTS_VALU", 0.0) / d["SQ_WAVES"], 1)
     if d.get("SQ_WAVE_CYCLES"):
