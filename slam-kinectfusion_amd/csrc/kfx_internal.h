@@ -57,7 +57,14 @@ struct LevelGeom {
 };
 
 #ifndef KFX_ICP_SHARDS
-#define KFX_ICP_SHARDS 4  // ICP: partial-sum rows (atomic spread vs rows every solver reads; 4: C2 ICP -3 us vs 8)
+// ICP: partial-sum rows (atomic spread vs rows every solver reads).  With the
+// flat arrival counter 4 measured best (C2 ICP -3 us vs 8); with the per-XCD
+// arrival counters (KFX_ICP_HIER) 8: tools/icp_barrier_bench.hip, 300 blocks
+// 4.35 us per hand-off at 4 shards, 3.33 at 8, 3.19 at 16
+#define KFX_ICP_SHARDS 8
+#endif
+#ifndef KFX_ICP_HIER
+#define KFX_ICP_HIER 1  // ICP arrival: per-residue (b % 8, one XCD each) counters, then a top counter of 8
 #endif
 constexpr int kIcpShards = KFX_ICP_SHARDS;
 constexpr int kIcpMaxSlots = 64;  // ICP iterations per frame in the persistent kernel
@@ -85,6 +92,10 @@ constexpr int kIcpStrideMax = 16;
 struct IcpSync {
   unsigned arrive, pad0[31];   // arrivals, all iterations (own 128-B line)
   unsigned exit, pad1[31];
+  struct {
+    unsigned v, pad[31];
+  } sub[8];                    // KFX_ICP_HIER: arrivals of the blocks b % 8 == r, all iterations
+  unsigned top, pad2[31];      // KFX_ICP_HIER: residues complete, all iterations
   struct {
     unsigned v, pad[31];
   } release[8];                // iterations released so far; 8 copies polled by block % 8

@@ -905,6 +905,7 @@ __global__ __launch_bounds__(kIcpThreads, KFX_ICP_MINB) void k_icp_track(IcpPlan
   int fail = 0;
   const bool withhold = blockIdx.x == 0 && st->debug_stall;  // test hook: never arrive at slot 0
   unsigned target = 0;
+  unsigned tsub = 0, ttop = 0;  // KFX_ICP_HIER: this block's residue's and the top counter's targets
   int slot = 0;
   for (int l = pl.levels - 1; l >= 0 && !fail; --l) {
     const LevelGeom g = pl.g[l];
@@ -934,6 +935,11 @@ __global__ __launch_bounds__(kIcpThreads, KFX_ICP_MINB) void k_icp_track(IcpPlan
     for (int it = 0; it < pl.iters[l] && !fail; ++it, ++slot) {
       unsigned long long *sh = sy->sums + (size_t)slot * kIcpShards * 27;
       target += min(pl.groups[l], (int)gridDim.x);  // arrivals: the blocks with a group
+      {
+        const int m = min(pl.groups[l], (int)gridDim.x), r = (int)(blockIdx.x & 7u);
+        tsub += r < m ? (unsigned)((m - r + 7) / 8) : 0u;  // participants of residue r (blocks 0 .. m-1)
+        ttop += (unsigned)min(m, 8);
+      }
 #ifdef KFX_ICP_TRACE
       const bool tr = threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x - 1);
 #else
@@ -994,12 +1000,30 @@ __global__ __launch_bounds__(kIcpThreads, KFX_ICP_MINB) void k_icp_track(IcpPlan
           if (threadIdx.x == 0 && !(withhold && slot == 0)) {
             // the last arriver releases the iteration: spinners poll 8 flag
             // copies instead of the contended arrival counter
+#if KFX_ICP_HIER
+            // arrivals counted per residue b % 8 (one XCD each under the
+            // round-robin placement; placement decides speed only): ~38
+            // atomics per counter instead of 300 on one, whose serialisation
+            // (~11 ns each) was ~1.7 us of every iteration's hand-off
+            // (tools/icp_barrier_bench.hip); a residue's last arriver adds to
+            // the top counter, whose last arriver releases
+            const unsigned n = __hip_atomic_fetch_add(&sy->sub[blockIdx.x & 7u].v, 1u, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT);
+            if (n == tsub - 1) {
+              const unsigned m = __hip_atomic_fetch_add(&sy->top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              if (m == ttop - 1)
+                for (int k = 0; k < 8; ++k)
+                  __hip_atomic_store(&sy->release[k].v, (unsigned)(slot + 1), __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+            }
+#else
             const unsigned n =
                 __hip_atomic_fetch_add(&sy->arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (n == target - 1)
               for (int k = 0; k < 8; ++k)
                 __hip_atomic_store(&sy->release[k].v, (unsigned)(slot + 1), __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
+#endif
           }
         }
       }
@@ -1090,9 +1114,12 @@ __global__ __launch_bounds__(kIcpThreads, KFX_ICP_MINB) void k_icp_track(IcpPlan
     if (threadIdx.x == 0) {
       __hip_atomic_store(&sy->arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(&sy->exit, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&sy->top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    if (threadIdx.x < 8)
+    if (threadIdx.x < 8) {
       __hip_atomic_store(&sy->release[threadIdx.x].v, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&sy->sub[threadIdx.x].v, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 

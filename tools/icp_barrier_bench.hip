@@ -18,11 +18,15 @@
 #include <vector>
 
 constexpr int kIters = 2000;
-constexpr int kShards = 4;
+constexpr int kShards = 16;  // most shards a case uses
 constexpr int kThreads = 256;
 
 struct Sync {
   unsigned arrive, pad0[31];
+  struct {
+    unsigned v, pad[31];
+  } sub[8];  // hierarchical arrival: per residue b % 8
+  unsigned top, pad1[31];
   struct {
     unsigned v, pad[31];
   } release[8];
@@ -30,7 +34,7 @@ struct Sync {
 };
 
 // mode 0: participants are blocks 0..P-1; mode 1: blocks with b % 8 == 0 (rank b / 8)
-__global__ __launch_bounds__(kThreads) void k_handoff(Sync *sy, int P, int mode, unsigned long long *out) {
+__global__ __launch_bounds__(kThreads) void k_handoff(Sync *sy, int P, int mode, int nload, int hier, int nadd, int nsh, unsigned long long *out) {
   const int b = blockIdx.x;
   int rank;
   if (mode == 0) {
@@ -49,15 +53,28 @@ __global__ __launch_bounds__(kThreads) void k_handoff(Sync *sy, int P, int mode,
     if (it == 1 && rank == 0 && threadIdx.x == 0) t0 = __builtin_amdgcn_s_memtime();
     unsigned long long *sh = sy->sums[it];
     if (threadIdx.x < 64) {
-      if (threadIdx.x < 27)
-        __hip_atomic_fetch_add(&sh[(rank % kShards) * 27 + threadIdx.x], (unsigned long long)(rank + 1 + carry),
+      if (threadIdx.x < nadd)
+        __hip_atomic_fetch_add(&sh[(rank % nsh) * 27 + threadIdx.x], (unsigned long long)(rank + 1 + carry),
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (threadIdx.x == 0) {
+      if (threadIdx.x == 0 && !hier) {
         const unsigned n = __hip_atomic_fetch_add(&sy->arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (n == (unsigned)P * (unsigned)(it + 1) - 1u)
           for (int k = 0; k < 8; ++k)
             __hip_atomic_store(&sy->release[k].v, (unsigned)(it + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else if (threadIdx.x == 0) {
+        // per-residue counter (rank % 8: ranks of one residue), then the
+        // residue's last arriver adds to the top counter (8 adds)
+        const int r = rank & 7;
+        const unsigned nr = (unsigned)((P - r + 7) / 8);  // ranks of residue r
+        const unsigned n = __hip_atomic_fetch_add(&sy->sub[r].v, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (n == nr * (unsigned)(it + 1) - 1u) {
+          const unsigned groups = (unsigned)(P < 8 ? P : 8);
+          const unsigned m = __hip_atomic_fetch_add(&sy->top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (m == groups * (unsigned)(it + 1) - 1u)
+            for (int k = 0; k < 8; ++k)
+              __hip_atomic_store(&sy->release[k].v, (unsigned)(it + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
       }
     }
     if (threadIdx.x == 0) {
@@ -66,12 +83,12 @@ __global__ __launch_bounds__(kThreads) void k_handoff(Sync *sy, int P, int mode,
         __builtin_amdgcn_s_sleep(1);
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < kShards * 27; i += kThreads)
-      red[i] = __longlong_as_double((long long)__hip_atomic_load(&sh[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    for (int i = threadIdx.x; i < nsh * 27; i += kThreads)
+      red[i] = i < nload ? __longlong_as_double((long long)__hip_atomic_load(&sh[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) : 0.0;
     __syncthreads();
     if (threadIdx.x < 27) {
       long long a = 0;
-      for (int k = 0; k < kShards; ++k) a += __double_as_longlong(red[k * 27 + threadIdx.x]);
+      for (int k = 0; k < nsh; ++k) a += __double_as_longlong(red[k * 27 + threadIdx.x]);
       sums[threadIdx.x] = a;
     }
     __syncthreads();
@@ -102,15 +119,22 @@ int main() {
   CK(hipEventCreate(&e1));
   struct Case {
     const char *name;
-    int grid, P, mode;
-  } cases[] = {{"240 blocks, spread", 240, 240, 0},   {"32 blocks, one XCD", 256, 32, 1},
-               {"30 blocks, one XCD", 256, 30, 1},    {"32 blocks, spread", 32, 32, 0},
-               {"70 blocks, spread", 70, 70, 0},      {"8 blocks, one XCD", 256, 8, 1}};
+    int grid, P, mode, nload, hier, nadd, nsh;
+  } cases[] = {{"240 blocks, spread", 240, 240, 0, 108, 0, 27, 4},   {"32 blocks, one XCD", 256, 32, 1, 108, 0, 27, 4},
+               {"30 blocks, one XCD", 256, 30, 1, 108, 0, 27, 4},    {"32 blocks, spread", 32, 32, 0, 108, 0, 27, 4},
+               {"70 blocks, spread", 70, 70, 0, 108, 0, 27, 4},      {"8 blocks, one XCD", 256, 8, 1, 108, 0, 27, 4},
+               {"240 blocks, 12 loads", 240, 240, 0, 12, 0, 27, 4},  {"240 blocks, no loads", 240, 240, 0, 0, 0, 27, 4},
+               {"300 blocks, spread", 300, 300, 0, 108, 0, 27, 4},   {"240 blocks, hier", 240, 240, 0, 108, 1, 27, 4},
+               {"300 blocks, hier", 300, 300, 0, 108, 1, 27, 4},     {"70 blocks, hier", 70, 70, 0, 108, 1, 27, 4},
+               {"240 hier, no adds", 240, 240, 0, 0, 1, 0, 4},  {"300 hier, no adds", 300, 300, 0, 0, 1, 0, 4},
+               {"240 flat, no adds", 240, 240, 0, 0, 0, 0, 4},  {"300 hier, 8 adds", 300, 300, 0, 108, 1, 8, 4},
+               {"300 hier, 8 shards", 300, 300, 0, 216, 1, 27, 8},  {"300 hier, 16 shards", 300, 300, 0, 432, 1, 27, 16},
+               {"240 hier, 8 shards", 240, 240, 0, 216, 1, 27, 8},  {"300 flat, 8 shards", 300, 300, 0, 216, 0, 27, 8}};
   for (int rep = 0; rep < 2; ++rep) {
     for (const Case &c : cases) {
       CK(hipMemset(sy, 0, sizeof(Sync)));
       CK(hipEventRecord(e0, 0));
-      hipLaunchKernelGGL(k_handoff, dim3(c.grid), dim3(kThreads), 0, 0, sy, c.P, c.mode, out);
+      hipLaunchKernelGGL(k_handoff, dim3(c.grid), dim3(kThreads), 0, 0, sy, c.P, c.mode, c.nload, c.hier, c.nadd, c.nsh, out);
       CK(hipEventRecord(e1, 0));
       CK(hipEventSynchronize(e1));
       float ms = 0.f;
