@@ -180,6 +180,14 @@ int kfx_debug_force_icp_stall(kfx_ctx *ctx);
  * device_utils.cuh:31, tsdf_volume.cpp:24) at any volume size, so the oracle
  * can pin them at sizes it runs.  Results are identical either way. */
 int kfx_debug_force_index64(kfx_ctx *ctx, int on);
+/* Measurement hook (tools/slab_record.py): device time of the sharded ICP's
+ * per-rank launches for band `rank` of `world` (kfx_set_icp_allreduce's
+ * k_icp_acc over the band's rows of every level + the k_icp_solve, 19
+ * iterations at the default parameters) on the current frame maps, without
+ * the all-reduces, which the caller prices separately; *ms = the mean of
+ * `reps` runs.  The tracking state is saved before and restored after, so the
+ * context's frames are unaffected. */
+int kfx_debug_icp_band_ms(kfx_ctx *ctx, int rank, int world, int reps, float *ms);
 /* Slab contexts (SURVEY.md §8e alternative): instead of every rank running
  * the whole ICP (default), rank r accumulates the 27 products over its band
  * of each level's rows and the exact int64 partials are all-reduced (SUM)

@@ -1422,6 +1422,46 @@ int kfx_debug_force_icp_stall(kfx_ctx *c) {
   return write_field(c, offsetof(DevState, debug_stall), 1);
 }
 
+int kfx_debug_icp_band_ms(kfx_ctx *c, int rank, int world, int reps, float *ms) {
+  int r = check_ctx(c);
+  if (r) return r;
+  if (!ms || world < 1 || rank < 0 || rank >= world || reps < 1) return set_err(KFX_ERR_ARG, "band rank/world/reps");
+  HIPCHK(hipStreamSynchronize(c->pstream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  DevState saved;
+  HIPCHK(hipMemcpy(&saved, c->st, sizeof(DevState), hipMemcpyDeviceToHost));
+  DevState run = saved;
+  run.mode = MODE_TRACK;  // (a bootstrap state would make every launch return at once)
+  run.icp_fail = 0;
+  hipEvent_t e[2] = {nullptr, nullptr};
+  HIPCHK(hipEventCreate(&e[0]));
+  HIPCHK(hipEventCreate(&e[1]));
+  double total = 0.0;
+  hipError_t err = hipSuccess;
+  for (int k = 0; k < reps && err == hipSuccess; ++k) {
+    err = hipMemcpy(c->st, &run, sizeof(DevState), hipMemcpyHostToDevice);
+    if (err == hipSuccess) err = hipEventRecord(e[0], c->stream);
+    for (int level = c->L - 1; level >= 0 && err == hipSuccess; --level)
+      for (int it = 0; it < c->p.icp_iter_count[level]; ++it) {
+        launch_icp(c->stream, c->g[level], c->cur.v[level], c->cur.n[level], c->prev.v[level], c->prev.n[level],
+                   c->p.icp_dist_threshold, c->angle_thr, c->st, c->icp_shards, c->icp_ticket, 0, 0, rank, world);
+        launch_icp_solve(c->stream, c->st);
+      }
+    if (err == hipSuccess) err = hipEventRecord(e[1], c->stream);
+    if (err == hipSuccess) err = hipEventSynchronize(e[1]);
+    float t = 0.f;
+    if (err == hipSuccess) err = hipEventElapsedTime(&t, e[0], e[1]);
+    total += t;
+  }
+  (void)hipEventDestroy(e[0]);
+  (void)hipEventDestroy(e[1]);
+  const hipError_t err2 = hipMemcpy(c->st, &saved, sizeof(DevState), hipMemcpyHostToDevice);
+  if (err != hipSuccess || err2 != hipSuccess)
+    return set_err(KFX_ERR_HIP, std::string("icp band timing: ") + hipGetErrorString(err != hipSuccess ? err : err2));
+  *ms = (float)(total / reps);
+  return KFX_OK;
+}
+
 int kfx_debug_force_index64(kfx_ctx *c, int on) {
   int r = check_ctx(c);
   if (r) return r;

@@ -29,7 +29,7 @@ LIB_PATH = os.environ.get("KFX_LIB_PATH") or os.path.join(_PKG, "lib", "libkfx.s
 EXPORTS = [
     "kfx_abi_version", "kfx_last_error", "kfx_default_params", "kfx_create", "kfx_destroy", "kfx_reset",
     "kfx_pipeline", "kfx_pipeline_u16", "kfx_stage_frames", "kfx_pipeline_staged", "kfx_synchronize",
-    "kfx_set_graph_mode", "kfx_set_frame_overlap", "kfx_set_kernel_timing", "kfx_get_kernel_timing", "kfx_get_kernel_timing_ex", "kfx_set_icp_persistent", "kfx_debug_force_icp_stall", "kfx_debug_force_index64", "kfx_get_icp_trace", "kfx_get_cur_camera_pose", "kfx_get_frame_count", "kfx_get_pose_record",
+    "kfx_set_graph_mode", "kfx_set_frame_overlap", "kfx_set_kernel_timing", "kfx_get_kernel_timing", "kfx_get_kernel_timing_ex", "kfx_set_icp_persistent", "kfx_debug_force_icp_stall", "kfx_debug_force_index64", "kfx_debug_icp_band_ms", "kfx_get_icp_trace", "kfx_get_cur_camera_pose", "kfx_get_frame_count", "kfx_get_pose_record",
     "kfx_write_poses_txt", "kfx_get_frame_maps", "kfx_set_frame_maps", "kfx_download_tsdf",
     "kfx_upload_tsdf", "kfx_download_volume_soa", "kfx_stage_preprocess", "kfx_stage_icp_accumulate",
     "kfx_stage_icp", "kfx_stage_integrate", "kfx_stage_raycast", "kfx_set_profiling", "kfx_get_stage_ms",
@@ -83,6 +83,7 @@ def lib():
         "kfx_set_icp_persistent": ([vp, i], i),
         "kfx_debug_force_icp_stall": ([vp], i),
         "kfx_debug_force_index64": ([vp, i], i),
+        "kfx_debug_icp_band_ms": ([vp, i, i, i, P(C.c_float)], i),
         "kfx_get_icp_trace": ([vp, P(C.c_uint64), i], i),
         "kfx_get_cur_camera_pose": ([vp, P(Pose)], i),
         "kfx_get_frame_count": ([vp, P(i)], i),
@@ -464,6 +465,14 @@ class KinectFusion:
         """Test hook: integrate / raycast take the 64-bit-index kernels (the
         >= 2^31-voxel path) at any volume size."""
         _check(lib().kfx_debug_force_index64(self._h, int(on)), "kfx_debug_force_index64")
+
+    def debug_icp_band_ms(self, rank, world, reps=5) -> float:
+        """Device ms of the sharded ICP's launches for band rank of world (no
+        all-reduces; the tracking state is restored afterwards)."""
+        ms = C.c_float()
+        _check(lib().kfx_debug_icp_band_ms(self._h, int(rank), int(world), int(reps), C.byref(ms)),
+               "kfx_debug_icp_band_ms")
+        return float(ms.value)
 
     def icp_trace(self):
         """(iterations, 5) s_memrealtime stamps of the last persistent-ICP frame."""

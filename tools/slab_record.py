@@ -32,6 +32,9 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--groups", default="equal,balanced,balanced_unbounded,calibrated",
                     help="cut sets to time (A/B runs: e.g. calibrated)")
+    ap.add_argument("--rccl-us", type=float, default=25.0,
+                    help="assumed latency of one 27 x int64 RCCL all-reduce over the ranks (not measured here: "
+                         "one GPU), used to price the sharded ICP (19 all-reduces per frame)")
     a = ap.parse_args()
     import kfx
     from kfx import synth
@@ -91,6 +94,14 @@ def main():
                           "combine_ms": k["combine"], "integrate_updated": w["updated"], "samples": k["samples"]})
         if not os.environ.get("KFX_TIMING_ONLY"):  # (timing-only variants compute wrong values)
             assert all(np.array_equal(m.pose_record, sp) for m in members), "slab poses differ from the single volume"
+        # the sharded ICP's per-rank device work (kfx_set_icp_allreduce: band r of
+        # every level's rows, 19 k_icp_acc + k_icp_solve launches) on the last
+        # frame's maps, without its 19 all-reduces (priced at --rccl-us)
+        iters = int(sum(p.icp_iter_count[:3]))
+        for r, (m, sl) in enumerate(zip(members, slabs)):
+            sl["icp_banded_ms"] = m.debug_icp_band_ms(r, a.world, reps=5)
+            sl["icp_sharded_ms_priced"] = sl["icp_banded_ms"] + iters * a.rccl_us * 1e-3
+        full_launches = members[0].debug_icp_band_ms(0, 1, reps=5)
         for m in members:
             m.close()
         it = np.array([s["integrate_ms"] for s in slabs])
@@ -99,7 +110,12 @@ def main():
         crit = [s["icp_ms"] + s["integrate_ms"] + s["raycast_local_ms"] for s in slabs]
         crit_c = [c + s["combine_ms"] for c, s in zip(crit, slabs)]
         rc = np.array([s["raycast_local_ms"] for s in slabs])
+        crit_sh = [s["icp_sharded_ms_priced"] + s["integrate_ms"] + s["raycast_local_ms"] + s["combine_ms"]
+                   for s in slabs]
         return {"cuts": cuts, "slab_bound": bound, "slabs": slabs,
+                "icp_per_iteration_launches_whole_frame_ms": full_launches,
+                "rccl_allreduce_us_assumed": a.rccl_us,
+                "max_rank_crit_sharded_icp_ms": float(max(crit_sh)),
                 "group_wall_ms_per_frame": 1e3 * t_group / a.frames,
                 "max_slab_over_single_raycast": float(rc.max() / rec["single"]["raycast_ms"]),
                 "max_rank_icp_integrate_raycast_combine_ms": float(max(crit_c)),
