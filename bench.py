@@ -68,12 +68,12 @@ def parse():
                     help="frames fed from host memory through kfx_pipeline_async for host_input (0 = skip)")
     ap.add_argument("--c1-frames", type=int, default=100,
                     help="oracle frames of the C1 record (128^3, same frames; 0 = skip)")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r05_integrate_pmc.json"),
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r06_integrate_pmc.json"),
                     help="integrate PMC traffic record; attached only when it was measured on this command's "
                          "workload and step counts with the same libkfx.so (sha256)")
-    ap.add_argument("--traffic-c3", default=os.path.join(ROOT, "profiles", "r05_c3_pmc.json"),
+    ap.add_argument("--traffic-c3", default=os.path.join(ROOT, "profiles", "r06_c3_pmc.json"),
                     help="PMC record of the C3 workload (attached to c3_record under the same rule)")
-    ap.add_argument("--traffic-c5", default=os.path.join(ROOT, "profiles", "r05_c5_pmc.json"),
+    ap.add_argument("--traffic-c5", default=os.path.join(ROOT, "profiles", "r06_c5_pmc.json"),
                     help="PMC record of the C5 single-volume workload (attached to c5_record under the same rule)")
     ap.add_argument("--graph", choices=["auto", "0", "1", "2"], default="auto",
                     help="kfx_set_graph_mode of the timed frames: 0 eager, 1 the pyrDown+preprocess graph, 2 also "

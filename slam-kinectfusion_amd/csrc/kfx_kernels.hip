@@ -904,7 +904,7 @@ __global__ __launch_bounds__(kIcpThreads, KFX_ICP_MINB) void k_icp_track(IcpPlan
   __shared__ int sfail, sstall;
   int fail = 0;
   const bool withhold = blockIdx.x == 0 && st->debug_stall;  // test hook: never arrive at slot 0
-  unsigned target = 0;
+  unsigned target = 0;  // (flat arrival counter: KFX_ICP_HIER 0)
   unsigned tsub = 0, ttop = 0;  // KFX_ICP_HIER: this block's residue's and the top counter's targets
   int slot = 0;
   for (int l = pl.levels - 1; l >= 0 && !fail; --l) {
@@ -935,6 +935,7 @@ __global__ __launch_bounds__(kIcpThreads, KFX_ICP_MINB) void k_icp_track(IcpPlan
     for (int it = 0; it < pl.iters[l] && !fail; ++it, ++slot) {
       unsigned long long *sh = sy->sums + (size_t)slot * kIcpShards * 27;
       target += min(pl.groups[l], (int)gridDim.x);  // arrivals: the blocks with a group
+      (void)target;
       {
         const int m = min(pl.groups[l], (int)gridDim.x), r = (int)(blockIdx.x & 7u);
         tsub += r < m ? (unsigned)((m - r + 7) / 8) : 0u;  // participants of residue r (blocks 0 .. m-1)
