@@ -176,6 +176,9 @@ __device__ __forceinline__ pf2 sqrt_rn2(pf2 x) {
 // Integrate's voxel pairs (ipf2): packed FP32 (KFX_INT_PK 1: v_pk_* ops,
 // each 4 cycles per wave on gfx950, tools/valu_calib.hip) or two scalar
 // operations per pair (0: 2 cycles each, no register moves to pair operands).
+#ifndef KFX_INT_LDALL
+#define KFX_INT_LDALL 1  // integrate: pin the batch's tsdf / weight loads before the update branches (C2 -1.5 us)
+#endif
 #ifndef KFX_INT_BSKIP
 #define KFX_INT_BSKIP 0  // integrate: skip a batch's loads and update when no voxel of the wave passes
 #endif
@@ -1890,6 +1893,13 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
       t0[j] = mem.ld_t(i);
       w0[j] = mem.ld_w(i);
     }
+#if KFX_INT_LDALL
+    // all kB voxels' loads issued together, one wait: the compiler otherwise
+    // sinks a voxel's loads into its update branch (the loaded values are
+    // only used there), which puts them on a round trip of their own
+#pragma unroll
+    for (int j = 0; j < kB; ++j) asm volatile("" ::"v"(t0[j]), "v"(w0[j]));
+#endif
     iz += (Idx)kB * slice;
     // The update arithmetic of all kB voxels, two voxels per packed op and
     // without branches (voxels that do not pass compute values nobody
