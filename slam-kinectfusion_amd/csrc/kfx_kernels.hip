@@ -63,10 +63,17 @@
 #define KFX_INT_MAXCHUNK 8  // integrate: most z-chunks per column tile
 #endif
 #ifndef KFX_INT_SLAB_CHUNK
-#define KFX_INT_SLAB_CHUNK 128  // integrate, Z-slab contexts: chunks of at most about this many slices
+#define KFX_INT_SLAB_CHUNK 96  // integrate, Z-slab contexts: chunks of at most about this many slices (with KFX_FF_MIN_SLAB 128; 128 / 64: slab sum +0.3 % / +3 %)
 #endif
 #ifndef KFX_FF_MIN
 #define KFX_FF_MIN 768  // fast-forward replays of at least this many adds (shorter ones: the adds; A/B r3m: 384 costs C2 +8 %)
+#endif
+#ifndef KFX_FF_MIN_SLAB
+// Z-slabs that do not start at z = 0: every chunk replays its column from
+// z = 1 to past the slab's start, so the exact fast-forward pays from fewer
+// adds (C4 calibrated slabs: integrate sum 1.563-1.577 -> 1.545-1.548 ms, worst
+// slab 0.219-0.221 -> 0.214-0.215 ms; C2 is unaffected)
+#define KFX_FF_MIN_SLAB 128
 #endif
 #ifndef KFX_INT_SLAB_CAPW
 #define KFX_INT_SLAB_CAPW 4  // integrate, Z-slab contexts: at most this many times KFX_INT_WAVES waves
@@ -1459,8 +1466,8 @@ __device__ __forceinline__ f3 replay_add(f3 a, f3 b) {
 // a advanced from slice z to slice za (za - z adds when za > z): the exact
 // fast-forward of kfx_ffadd.h for long replays, the adds themselves (8 per
 // trip) for short ones
-__device__ __forceinline__ f3 replay(f3 a, f3 b, int z, int za) {
-  if (za - z >= KFX_FF_MIN) {
+__device__ __forceinline__ f3 replay(f3 a, f3 b, int z, int za, int ffmin = KFX_FF_MIN) {
+  if (za - z >= ffmin) {
     a.x = ff_add(a.x, b.x, za - z);
     a.y = ff_add(a.y, b.y, za - z);
     a.z = ff_add(a.z, b.z, za - z);
@@ -1752,7 +1759,9 @@ __global__ __launch_bounds__(KFX_INT_BLOCK) __attribute__((amdgpu_waves_per_eu(K
   za = __builtin_amdgcn_readfirstlane(za);
   zb = __builtin_amdgcn_readfirstlane(zb);
   z = 1;
-  vc = replay(vc, zs, z, za);
+  // (Z-slabs: the fast-forward from a lower count, KFX_FF_MIN_SLAB — every
+  // chunk of a far slab replays its column from z = 1)
+  vc = replay(vc, zs, z, za, v.zb > 0 ? KFX_FF_MIN_SLAB : KFX_FF_MIN);
   z = max(z, za);
   const int la = max(za, zl), lb = min(zb, zh);  // this lane's voxels of the chunk
   const bool live = lb >= la;

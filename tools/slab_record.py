@@ -167,7 +167,7 @@ def main():
             sl["stored_slots"] = float(n * n * (z1 - z0))
             # k_integrate's waves for this slab (kfx_kernels.hip integrate_chunks)
             tiles, zn = (n // 8) ** 2, z1 - z0
-            nc = max(nc_min := (12288 + tiles - 1) // tiles, min((zn + 127) // 128, 4 * 12288 // tiles))
+            nc = max(nc_min := (12288 + tiles - 1) // tiles, min((zn + 95) // 96, 4 * 12288 // tiles))
             sl["waves"] = float(tiles * max(1, min(8, max(nc, nc_min))))
     if not all(k in rec for k in ("equal_cuts", "balanced_cuts")):
         out = a.out or os.path.join(ROOT, "gpurun_out", f"slabs_{a.config}.json")
