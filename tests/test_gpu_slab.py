@@ -445,6 +445,10 @@ def test_slab_bound_switch_with_captured_graphs(seq_qvga):
     single, st = _single(intr, p, bgr, dep)
     m = KinectFusion(Intrinsics.from_any(intr), p, slab=(0, 1))
     m.comm_init(comm_unique_id())
+    # a mode outside 0..2 still enters the collective check (as the sentinel
+    # -1) and fails on every rank, leaving the mode and the context usable
+    with pytest.raises(KfxError, match="slab bound modes"):
+        m.set_slab_bound(3)
     m.set_graph_mode(2)
     gst = []
     for k in range(len(dep)):
@@ -466,3 +470,25 @@ def test_slab_bound_switch_with_captured_graphs(seq_qvga):
     single2.synchronize()
     _compare(single2, [m])
     m.close()
+
+
+def test_icp_band_timing_leaves_tracking_unchanged(seq_qvga):
+    """kfx_debug_icp_band_ms (tools/slab_record.py's pricing of the sharded
+    ICP: a band's 19 k_icp_acc + k_icp_solve launches on the frame's maps)
+    returns a positive device time and restores the tracking state: the
+    frames after it equal those of a context that never called it."""
+    bgr, dep, _ = seq_qvga
+    intr = synth.Intrinsics.qvga()
+    p = default_params(dims=64, range_m=L_VOL)
+    ref, st = _single(intr, p, bgr, dep)
+    m = KinectFusion(Intrinsics.from_any(intr), p)
+    for k in range(len(dep)):
+        assert m.pipeline(bgr[k], dep[k].astype(np.float32)) == st[k]
+        if k in (2, 5):
+            assert m.debug_icp_band_ms(0, 2, reps=2) > 0.0
+            assert m.debug_icp_band_ms(0, 1, reps=1) > 0.0
+    _compare(ref, [m])
+    with pytest.raises(KfxError):
+        m.debug_icp_band_ms(2, 2)
+    m.close()
+    ref.close()
