@@ -2004,9 +2004,12 @@ static int comm_check_slab_bound(kfx_ctx *c, int mode) {
   if (e == ncclSuccess) e = ncclAllReduce(d + 1, d + 1, 1, ncclInt32, ncclMax, c->comm, c->stream);
   const ncclResult_t e2 = ncclGroupEnd();
   if (e == ncclSuccess) e = e2;
+  // (the upload reads h0 on this stack frame: the stream is drained before
+  // returning on every path)
+  const bool drained = hipStreamSynchronize(c->stream) == hipSuccess;
   if (e != ncclSuccess)
     r = set_err(KFX_ERR_COMM, std::string("slab bound check: ") + ncclGetErrorString(e));
-  else if (hipStreamSynchronize(c->stream) != hipSuccess || hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost) != hipSuccess)
+  else if (!drained || hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost) != hipSuccess)
     r = set_err(KFX_ERR_HIP, "slab bound check: download");
   else if (!up)
     r = set_err(KFX_ERR_HIP, "slab bound check: upload");
