@@ -112,7 +112,7 @@ struct kfx_ctx {
   bool overlap = true;
   hipStream_t pstream = nullptr;
   hipEvent_t ev_prep = nullptr, ev_free[2]{};
-  hipEvent_t ev_icp = nullptr;  // after the last overlapped frame's ICP (the next preprocess starts there)
+  hipEvent_t ev_icp = nullptr;  // after the last overlapped frame's ICP, or its integrate (KFX_PREP_AFTER_INT): the next preprocess starts there
   hipEvent_t ev_group = nullptr;  // kfx_pipeline_group combine: fork (member 0) / join (the others)
   bool group_chain = false;     // kfx_pipeline_group member: record ev_icp after every ICP
   bool graphs_stale = false;    // a refused persistent ICP launch: captured graphs still hold it
@@ -222,6 +222,13 @@ int dalloc(kfx_ctx *c, void **p, size_t bytes) {
 
 #ifndef KFX_PREP_AFTER_ICP
 #define KFX_PREP_AFTER_ICP 1  // overlapped frames: next preprocess waits for this frame's ICP
+#endif
+#ifndef KFX_PREP_AFTER_INT
+// ... for this frame's integrate instead: the preprocess then shares the GPU
+// with the raycast (memory-latency bound, 0.2-0.4 VALU issue) rather than the
+// issue-bound integrate; C2 integrate -12 us, raycast +8 us, frame -0.4 to
+// -1.4 % (7 alternating pairs)
+#define KFX_PREP_AFTER_INT 1
 #endif
 #ifndef KFX_COST_UPDATED
 #define KFX_COST_UPDATED 32  // slab balancing: weight of an updated voxel (64 = one visited slot; slice_cost)
@@ -424,13 +431,18 @@ void enqueue_slab_resume(kfx_ctx *c, hipStream_t s) {
 }
 
 // integrate + raycast of the frame whose maps are in the current set
-void enqueue_map(kfx_ctx *c, FrameInput in, hipEvent_t *ev) {
+int enqueue_map(kfx_ctx *c, FrameInput in, hipEvent_t *ev, bool rec_int = false) {
   hipStream_t s = c->stream;
   launch_integrate(s, c->vol, c->g[0], c->dl0, c->cur.d[0], c->inv_lambda, in.bgr, c->st, c->pose_log,
                    to_dev(c->p.volu_pose), nullptr, nullptr);
   if (ev) (void)hipEventRecord(ev[3], s);
+  if (rec_int) {
+    const int r = record_icp_event(c, s);
+    if (r) return r;
+  }
   launch_raycast(s, c->vol, c->L, c->g, c->cur, c->prev, c->st, c->pose_log,
                  to_dev(c->p.volu_pose), nullptr, c->slab ? c->key_local : nullptr, nullptr, slab_pass1(c));
+  return KFX_OK;
 }
 
 // The persistent ICP launch, if this context uses it.  False when it does not,
@@ -465,9 +477,10 @@ int enqueue_track(kfx_ctx *c, FrameInput in, hipEvent_t *ev, bool begin) {
   if (ev) (void)hipEventRecord(ev[2], s);
   // overlapped frames: the next preprocess waits here; a group: the next
   // member's ICP on this device waits here
-  if ((begin || c->group_chain) && !r && (r = record_icp_event(c, s))) return r;
-  enqueue_map(c, in, ev);
-  return r;
+  const bool after_int = KFX_PREP_AFTER_INT && begin && !c->group_chain;
+  if ((begin || c->group_chain) && !after_int && !r && (r = record_icp_event(c, s))) return r;
+  const int rm = enqueue_map(c, in, ev, after_int && !r);
+  return r ? r : rm;
 }
 
 // Frame overlap: the preprocess of this frame runs on pstream into the set the
@@ -522,8 +535,9 @@ int enqueue_frame_overlap(kfx_ctx *c, FrameInput in, hipEvent_t *ev, hipGraphExe
   HIPCHK(hipStreamWaitEvent(b, c->ev_free[p], 0));  // the frame before last is done with set p
   if (in.ready) HIPCHK(hipStreamWaitEvent(b, in.ready, 0));  // host input uploaded
 #if KFX_PREP_AFTER_ICP
-  // start behind the previous frame's ICP: the latency-bound persistent ICP
-  // then runs alone and the preprocess shares the GPU with integrate/raycast
+  // start behind the previous frame's ICP (KFX_PREP_AFTER_INT: its integrate;
+  // ev_icp is recorded there): the latency-bound persistent ICP then runs
+  // alone and the preprocess shares the GPU with the raycast
   HIPCHK(hipStreamWaitEvent(b, c->ev_icp, 0));
 #endif
   if (gx) HIPCHK(hipGraphLaunch(gx[0], b));
