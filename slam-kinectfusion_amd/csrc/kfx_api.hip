@@ -112,8 +112,23 @@ struct kfx_ctx {
   bool overlap = true;
   hipStream_t pstream = nullptr;
   hipEvent_t ev_prep = nullptr, ev_free[2]{};
+  // ev_free[p] elision (enqueue_frame_overlap): free_rec[p] = the last frame
+  // that used set p recorded ev_free[p]; ov_linked = the last API call into
+  // this context (api_seq, counted by check_ctx) enqueued an overlapped frame
+  // whose ev_icp record follows its integrate
+  bool free_rec[2]{};
+  bool ov_linked = false;
+  unsigned long long api_seq = 0, ov_api_seq = 0;
   hipEvent_t ev_icp = nullptr;  // after the last overlapped frame's ICP, or its integrate (KFX_PREP_AFTER_INT): the next preprocess starts there
   hipEvent_t ev_group = nullptr;  // kfx_pipeline_group combine: fork (member 0) / join (the others)
+  // raycast start signal (KFX_PREP_SIG): fine-grained word the frame's raycast
+  // stores sig_serial to as it starts; the next preprocess waits for it with
+  // hipStreamWaitValue32 on its own stream (null: unsupported, ev_icp instead)
+  unsigned *start_sig = nullptr;
+  unsigned sig_serial = 0;
+  bool sig_prev = false;    // the last overlapped frame signalled sig_serial
+  bool ray_sig_on = false;  // enqueue_map: pass the signal to this raycast
+  unsigned frame_sig = 0;   // the serial the frame run_frame just enqueued signals (0: none)
   bool group_chain = false;     // kfx_pipeline_group member: record ev_icp after every ICP
   bool graphs_stale = false;    // a refused persistent ICP launch: captured graphs still hold it
 
@@ -183,6 +198,7 @@ struct kfx_ctx {
   size_t ring_slot = 0;  // bytes per slot: f32 depth + BGR8
   hipEvent_t ring_h2d[kRing]{}, ring_done[kRing]{};
   bool ring_used[kRing]{};
+  unsigned ring_sig[kRing]{};  // the raycast start signal of the slot's last frame (0: wait ring_done)
   hipGraphExec_t ring_graph[kRing][2][4]{};  // overlapped-frame graphs per slot and [u16 input]
   int ring_next = 0;
   bool ring_ready = false;  // every ring resource above created
@@ -222,6 +238,12 @@ int dalloc(kfx_ctx *c, void **p, size_t bytes) {
 
 #ifndef KFX_PREP_AFTER_ICP
 #define KFX_PREP_AFTER_ICP 1  // overlapped frames: next preprocess waits for this frame's ICP
+#endif
+#ifndef KFX_PREP_SIG
+#define KFX_PREP_SIG 1  // overlapped frames: the raycast's start signal replaces the ev_icp record
+#endif
+#ifndef KFX_FREE_ELIDE
+#define KFX_FREE_ELIDE 1  // overlapped frames: no ev_free record when the next frame's ev_icp wait covers it
 #endif
 #ifndef KFX_PREP_AFTER_INT
 // ... for this frame's integrate instead: the preprocess then shares the GPU
@@ -441,7 +463,8 @@ int enqueue_map(kfx_ctx *c, FrameInput in, hipEvent_t *ev, bool rec_int = false)
     if (r) return r;
   }
   launch_raycast(s, c->vol, c->L, c->g, c->cur, c->prev, c->st, c->pose_log,
-                 to_dev(c->p.volu_pose), nullptr, c->slab ? c->key_local : nullptr, nullptr, slab_pass1(c));
+                 to_dev(c->p.volu_pose), nullptr, c->slab ? c->key_local : nullptr, nullptr, slab_pass1(c),
+                 c->ray_sig_on ? c->start_sig : nullptr, c->sig_serial);
   return KFX_OK;
 }
 
@@ -477,8 +500,9 @@ int enqueue_track(kfx_ctx *c, FrameInput in, hipEvent_t *ev, bool begin) {
   if (ev) (void)hipEventRecord(ev[2], s);
   // overlapped frames: the next preprocess waits here; a group: the next
   // member's ICP on this device waits here
-  const bool after_int = KFX_PREP_AFTER_INT && begin && !c->group_chain;
-  if ((begin || c->group_chain) && !after_int && !r && (r = record_icp_event(c, s))) return r;
+  // (with the raycast start signal the next preprocess waits for that instead)
+  const bool after_int = KFX_PREP_AFTER_INT && begin && !c->group_chain && !c->ray_sig_on;
+  if ((begin || c->group_chain) && !after_int && !c->ray_sig_on && !r && (r = record_icp_event(c, s))) return r;
   const int rm = enqueue_map(c, in, ev, after_int && !r);
   return r ? r : rm;
 }
@@ -532,23 +556,70 @@ int enqueue_frame_overlap(kfx_ctx *c, FrameInput in, hipEvent_t *ev, hipGraphExe
   const int p = c->par ^ 1;
   set_par(c, p);
   hipStream_t b = c->pstream;
-  HIPCHK(hipStreamWaitEvent(b, c->ev_free[p], 0));  // the frame before last is done with set p
+  // Set p was last used by the frame before last.  When the previous API call
+  // enqueued the previous overlapped frame and that frame records ev_icp after
+  // its integrate, the ev_icp wait below already orders this preprocess after
+  // that frame's integrate, and so (one in-order stream) after everything
+  // enqueued on the frame stream before it — the frame before last included:
+  // no ev_free record is needed (each record between two frame kernels costs
+  // the frame stream 2-5 us).  Otherwise wait for ev_free[p],
+  // recorded now at the frame stream's tail if its last user did not record it.
+  const bool linked = KFX_FREE_ELIDE && KFX_PREP_AFTER_ICP && c->ov_linked && c->api_seq == c->ov_api_seq + 1;
+  if (!linked) {
+    if (!c->free_rec[p]) HIPCHK(hipEventRecord(c->ev_free[p], c->stream));
+    HIPCHK(hipStreamWaitEvent(b, c->ev_free[p], 0));  // the frame before last is done with set p
+  }
+  c->ov_linked = false;
+  c->free_rec[p] = false;
   if (in.ready) HIPCHK(hipStreamWaitEvent(b, in.ready, 0));  // host input uploaded
 #if KFX_PREP_AFTER_ICP
   // start behind the previous frame's ICP (KFX_PREP_AFTER_INT: its integrate;
-  // ev_icp is recorded there): the latency-bound persistent ICP then runs
+  // ev_icp is recorded there; KFX_PREP_SIG: as its raycast starts, which
+  // stores the frame's serial): the latency-bound persistent ICP then runs
   // alone and the preprocess shares the GPU with the raycast
-  HIPCHK(hipStreamWaitEvent(b, c->ev_icp, 0));
+  if (c->sig_prev)
+    HIPCHK(hipStreamWaitValue32(b, c->start_sig, c->sig_serial, hipStreamWaitValueGte, 0xffffffffu));
+  else
+    HIPCHK(hipStreamWaitEvent(b, c->ev_icp, 0));
 #endif
   if (gx) HIPCHK(hipGraphLaunch(gx[0], b));
   else enqueue_prep_overlap(c, in);
   HIPCHK(hipEventRecord(c->ev_prep, b));
   HIPCHK(hipStreamWaitEvent(c->stream, c->ev_prep, 0));
   int r = KFX_OK;
+  // this frame's raycast signals its start (not inside a captured main graph,
+  // whose launch arguments are fixed: it records ev_icp)
+  const bool use_sig = KFX_PREP_SIG && KFX_PREP_AFTER_ICP && KFX_PREP_AFTER_INT && c->start_sig && !c->group_chain &&
+                       !(gx && gx[1]);
+  c->sig_prev = false;
+  if (use_sig) {
+    if (c->sig_serial >= 0x7fffffffu) {  // wrap: restart the serials from a drained context
+      HIPCHK(hipStreamSynchronize(c->stream));
+      HIPCHK(hipStreamSynchronize(b));
+      if (c->cstream) HIPCHK(hipStreamSynchronize(c->cstream));
+      HIPCHK(hipMemset(c->start_sig, 0, 64));
+      c->sig_serial = 0;
+      for (unsigned &v : c->ring_sig) v = 0u;  // (their frames are complete)
+    }
+    c->sig_serial += 1;
+    c->ray_sig_on = true;
+  }
   if (gx && gx[1]) HIPCHK(hipGraphLaunch(gx[1], c->stream));
   else r = enqueue_main_overlap(c, in, ev);
-  HIPCHK(hipEventRecord(c->ev_free[p], c->stream));
-  if (in.done) HIPCHK(hipEventRecord(in.done, c->stream));
+  c->ray_sig_on = false;
+  c->sig_prev = use_sig && !r;
+  c->frame_sig = c->sig_prev ? c->sig_serial : 0u;
+  // the next overlapped frame may rely on this frame's ev_icp (recorded after
+  // its integrate: enqueue_track) instead of ev_free[p]
+  const bool link = KFX_FREE_ELIDE && KFX_PREP_AFTER_ICP && KFX_PREP_AFTER_INT && !c->group_chain && !r;
+  if (!link) {
+    HIPCHK(hipEventRecord(c->ev_free[p], c->stream));
+    c->free_rec[p] = true;
+  }
+  c->ov_linked = link;
+  c->ov_api_seq = c->api_seq;
+  // (a signalling frame's input slot is released by its raycast start signal)
+  if (in.done && !c->frame_sig) HIPCHK(hipEventRecord(in.done, c->stream));
   return r;
 }
 
@@ -703,6 +774,7 @@ int run_frame(kfx_ctx *c, FrameInput in, hipGraphExec_t *graph, bool overlap = f
     c->graphs_stale = false;
   }
   c->last_bgr = in.bgr;
+  c->frame_sig = 0u;
   hipEvent_t *tev = timing_sample(c);  // this frame's timing sample, if sampled
   if (overlap && c->overlap && !c->profiling) {
     hipGraphExec_t *gx = nullptr;
@@ -850,6 +922,7 @@ int do_reset(kfx_ctx *c) {
 
 int check_ctx(kfx_ctx *c) {
   if (!c) return set_err(KFX_ERR_ARG, "null context");
+  c->api_seq += 1;
   hipError_t e = hipSetDevice(c->device);
   if (e != hipSuccess) return set_err(KFX_ERR_HIP, std::string("hipSetDevice: ") + hipGetErrorString(e));
   return KFX_OK;
@@ -1083,6 +1156,17 @@ static int create_impl(const kfx_intrinsics *intr, const kfx_params *params, int
     for (size_t i = 0; i < items; ++i) iota[i] = (unsigned)i;
     HIPCHK(hipMemcpy(c->vol.iperm, iota.data(), items * 4, hipMemcpyHostToDevice));
   }
+  {
+    int can_wait = 0;
+    if (hipDeviceGetAttribute(&can_wait, hipDeviceAttributeCanUseStreamWaitValue, device) == hipSuccess && can_wait &&
+        hipExtMallocWithFlags((void **)&c->start_sig, 64, hipDeviceMallocFinegrained) == hipSuccess) {
+      c->allocs.push_back(c->start_sig);
+      HIPCHK(hipMemset(c->start_sig, 0, 64));
+    } else {
+      (void)hipGetLastError();
+      c->start_sig = nullptr;
+    }
+  }
   if ((r = dalloc(c, (void **)&c->st, sizeof(DevState)))) return fail(r);
   c->pose_cap = kInitialPoseCap;
   if ((r = dalloc(c, (void **)&c->pose_log, sizeof(DevPose) * (size_t)c->pose_cap))) return fail(r);
@@ -1249,8 +1333,14 @@ static int pipeline_async(kfx_ctx *c, const uint8_t *bgr, const void *depth, boo
     map_d = c->ring_host_dev + c->ring_slot * k;
     map_c = map_d + np * 4;
   }
-  // the device slot is free once the frame that read it has finished
-  if (c->ring_used[k]) HIPCHK(hipStreamWaitEvent(c->cstream, c->ring_done[k], 0));
+  // the device slot is free once the frame that read it has finished (its
+  // preprocess and integrate: its raycast has started, when it signals that)
+  if (c->ring_used[k]) {
+    if (c->ring_sig[k])
+      HIPCHK(hipStreamWaitValue32(c->cstream, c->start_sig, c->ring_sig[k], hipStreamWaitValueGte, 0xffffffffu));
+    else
+      HIPCHK(hipStreamWaitEvent(c->cstream, c->ring_done[k], 0));
+  }
   launch_host_fetch(c->cstream, map_d, ds, dbytes, map_c, ds + np * 4, np * 3);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(c->ring_h2d[k], c->cstream));
@@ -1258,7 +1348,10 @@ static int pipeline_async(kfx_ctx *c, const uint8_t *bgr, const void *depth, boo
   FrameInput in{u16 ? c->raw[0] : (const float *)ds, u16 ? (const uint16_t *)ds : nullptr, ds + np * 4};
   in.ready = c->ring_h2d[k];
   in.done = c->ring_done[k];
-  return run_frame(c, in, nullptr, true, c->ring_graph[k][u16 ? 1 : 0]);
+  c->ring_sig[k] = 0u;
+  r = run_frame(c, in, nullptr, true, c->ring_graph[k][u16 ? 1 : 0]);
+  if (!r) c->ring_sig[k] = c->frame_sig;
+  return r;
 }
 
 int kfx_pipeline_async(kfx_ctx *c, const uint8_t *bgr, const float *depth_mm) {

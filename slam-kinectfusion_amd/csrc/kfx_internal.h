@@ -274,7 +274,7 @@ struct SlabPass {
 void launch_raycast(hipStream_t s, VolView v, int levels, const LevelGeom *g, FrameView cur,
                     FrameView prev, const DevState *st, const DevPose *log, DevPose vpose,
                     const float *xpose, uint32_t *keys, unsigned long long *stats = nullptr,
-                    const SlabPass &sp = SlabPass{});
+                    const SlabPass &sp = SlabPass{}, unsigned *start_sig = nullptr, unsigned start_val = 0);
 // the reference raycast's distinct voxels read (out[0]) and reads (out[1]),
 // count-only (bits: one bit per stored voxel, workspace)
 void launch_ray_pose(hipStream_t s, DevState *st, const DevPose *log, DevPose vpose);

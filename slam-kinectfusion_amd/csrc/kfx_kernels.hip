@@ -2179,6 +2179,13 @@ struct RayArgs {
   int slab_pass;
   const uint32_t *kmin;
   float bound_abs, bound_rel;  // pass-1 margin: metres, fraction of the distance
+  // start signal (overlapped frames, kfx_api.hip enqueue_frame_overlap): the
+  // first wave of block 0 stores start_val to *start_sig (fine-grained device
+  // memory, system scope; relaxed: it orders nothing, the launch itself implies
+  // the integrate before it is complete) as the launch begins; the preprocess stream waits
+  // for it (hipStreamWaitValue32) instead of an event record on this stream
+  unsigned *start_sig;
+  unsigned start_val;
 };
 
 __device__ void resize_tile(const RayArgs &ra, int kind, int tx0, int ty0, int lx, int ly, f3 vout,
@@ -2330,6 +2337,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((kSlab || !
     else if (d >= KFX_RAY_HINT_T0 * 11 / 8) __builtin_amdgcn_s_setprio(2);
     else if (d >= KFX_RAY_HINT_T0) __builtin_amdgcn_s_setprio(1);
   }
+  if (!kStats && ra.start_sig && blockIdx.x == 0 && threadIdx.x == 0)
+    __hip_atomic_store(ra.start_sig, ra.start_val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   const LevelGeom g = ra.g[0];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int nbx = (g.w + 15) / 16;
@@ -3870,7 +3879,8 @@ namespace kfx {
 #endif
 void launch_raycast(hipStream_t s, VolView v, int levels, const LevelGeom *g, FrameView cur,
                     FrameView prev, const DevState *st, const DevPose *log, DevPose vpose,
-                    const float *xpose, uint32_t *keys, unsigned long long *stats, const SlabPass &sp) {
+                    const float *xpose, uint32_t *keys, unsigned long long *stats, const SlabPass &sp,
+                    unsigned *start_sig, unsigned start_val) {
   const bool want_stats = stats != nullptr;
 #ifdef KFX_RAY_TRACE
   if (!stats) {
@@ -3899,6 +3909,8 @@ void launch_raycast(hipStream_t s, VolView v, int levels, const LevelGeom *g, Fr
   ra.kmin = sp.kmin;
   ra.bound_abs = sp.bound_abs;
   ra.bound_rel = sp.bound_rel;
+  ra.start_sig = start_sig;
+  ra.start_val = start_val;
   for (int l = 0; l < levels; ++l) ra.g[l] = g[l];
   dim3 grd(((g[0].w + 15) / 16) * ((g[0].h + 15) / 16));
   // 32-bit tsdf byte offsets (24-bit operands of the tile * zn products)
