@@ -8,6 +8,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -1157,8 +1158,14 @@ static int create_impl(const kfx_intrinsics *intr, const kfx_params *params, int
     HIPCHK(hipMemcpy(c->vol.iperm, iota.data(), items * 4, hipMemcpyHostToDevice));
   }
   {
+    // the raycast start signal (KFX_PREP_SIG) needs hipStreamWaitValue32; it
+    // is off under rocprofv3 counter collection (ROCPROF_COUNTER_COLLECTION),
+    // whose per-dispatch serialisation hung on the waiting preprocess queue,
+    // and with KFX_STREAM_SIGNAL=0 (events instead; results identical)
+    const char *pmc = std::getenv("ROCPROF_COUNTER_COLLECTION"), *ss = std::getenv("KFX_STREAM_SIGNAL");
+    const bool sig_ok = !(pmc && *pmc && std::strcmp(pmc, "0") != 0) && !(ss && std::strcmp(ss, "0") == 0);
     int can_wait = 0;
-    if (hipDeviceGetAttribute(&can_wait, hipDeviceAttributeCanUseStreamWaitValue, device) == hipSuccess && can_wait &&
+    if (sig_ok && hipDeviceGetAttribute(&can_wait, hipDeviceAttributeCanUseStreamWaitValue, device) == hipSuccess && can_wait &&
         hipExtMallocWithFlags((void **)&c->start_sig, 64, hipDeviceMallocFinegrained) == hipSuccess) {
       c->allocs.push_back(c->start_sig);
       HIPCHK(hipMemset(c->start_sig, 0, 64));
