@@ -129,6 +129,7 @@ struct kfx_ctx {
   unsigned sig_serial = 0;
   bool sig_prev = false;    // the last overlapped frame signalled sig_serial
   bool ray_sig_on = false;  // enqueue_map: pass the signal to this raycast
+  bool ov_order = false, ov_order_prev = false;    // enqueue_map: the next preprocess stream launches k_int_order (KFX_ORDER_OFF_PATH)
   unsigned frame_sig = 0;   // the serial the frame run_frame just enqueued signals (0: none)
   bool group_chain = false;     // kfx_pipeline_group member: record ev_icp after every ICP
   bool graphs_stale = false;    // a refused persistent ICP launch: captured graphs still hold it
@@ -242,6 +243,9 @@ int dalloc(kfx_ctx *c, void **p, size_t bytes) {
 #endif
 #ifndef KFX_PREP_SIG
 #define KFX_PREP_SIG 1  // overlapped frames: the raycast's start signal replaces the ev_icp record
+#endif
+#ifndef KFX_ORDER_OFF_PATH
+#define KFX_ORDER_OFF_PATH 1  // overlapped frames: k_int_order on the preprocess stream, beside the raycast
 #endif
 #ifndef KFX_FREE_ELIDE
 #define KFX_FREE_ELIDE 1  // overlapped frames: no ev_free record when the next frame's ev_icp wait covers it
@@ -457,7 +461,7 @@ void enqueue_slab_resume(kfx_ctx *c, hipStream_t s) {
 int enqueue_map(kfx_ctx *c, FrameInput in, hipEvent_t *ev, bool rec_int = false) {
   hipStream_t s = c->stream;
   launch_integrate(s, c->vol, c->g[0], c->dl0, c->cur.d[0], c->inv_lambda, in.bgr, c->st, c->pose_log,
-                   to_dev(c->p.volu_pose), nullptr, nullptr);
+                   to_dev(c->p.volu_pose), nullptr, nullptr, !c->ov_order);
   if (ev) (void)hipEventRecord(ev[3], s);
   if (rec_int) {
     const int r = record_icp_event(c, s);
@@ -585,6 +589,11 @@ int enqueue_frame_overlap(kfx_ctx *c, FrameInput in, hipEvent_t *ev, hipGraphExe
 #endif
   if (gx) HIPCHK(hipGraphLaunch(gx[0], b));
   else enqueue_prep_overlap(c, in);
+  // the dispatch order of this frame's integrate from the previous frame's
+  // intervals, off the frame stream: the wait above (its raycast has started,
+  // or ev_icp behind its integrate) orders it after the integrate that read
+  // the old order, and ev_prep before this frame's integrate
+  if (c->ov_order_prev) launch_int_order(b, c->vol);
   HIPCHK(hipEventRecord(c->ev_prep, b));
   HIPCHK(hipStreamWaitEvent(c->stream, c->ev_prep, 0));
   int r = KFX_OK;
@@ -605,9 +614,13 @@ int enqueue_frame_overlap(kfx_ctx *c, FrameInput in, hipEvent_t *ev, hipGraphExe
     c->sig_serial += 1;
     c->ray_sig_on = true;
   }
+  // (not for a captured main graph: it holds its own k_int_order launch)
+  c->ov_order = KFX_ORDER_OFF_PATH && KFX_PREP_AFTER_ICP && KFX_PREP_AFTER_INT && !c->group_chain && !(gx && gx[1]);
   if (gx && gx[1]) HIPCHK(hipGraphLaunch(gx[1], c->stream));
   else r = enqueue_main_overlap(c, in, ev);
   c->ray_sig_on = false;
+  c->ov_order_prev = c->ov_order && !r;
+  c->ov_order = false;
   c->sig_prev = use_sig && !r;
   c->frame_sig = c->sig_prev ? c->sig_serial : 0u;
   // the next overlapped frame may rely on this frame's ev_icp (recorded after

@@ -256,7 +256,12 @@ void launch_group_sum_icp(hipStream_t s, DevState *const *st, int n);
 void launch_integrate(hipStream_t s, VolView v, LevelGeom g0, const float2 *dl0, const float *dmap,
                       const float *invl, const uint8_t *bgr, DevState *st, DevPose *log, DevPose vpose,
                       const float *xpose,
-                      unsigned long long *counters /* non-null: count-only, 32 words */);
+                      unsigned long long *counters /* non-null: count-only, 32 words */,
+                      bool order = true /* false: the caller launches launch_int_order itself */);
+// the next frame's integrate dispatch order from this frame's intervals
+// (k_int_order; deep volumes only, a no-op otherwise).  It rewrites the order
+// the integrate just read: enqueue it after that integrate has completed.
+void launch_int_order(hipStream_t s, VolView v);
 // Z-slab raycast passes: pass 0 marches every ray to its end;
 // pass 1 stops at the previous frame's model distance along the ray (+
 // bound_abs metres + bound_rel of the distance) and records the first sample

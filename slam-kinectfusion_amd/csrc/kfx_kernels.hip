@@ -3769,26 +3769,32 @@ int integrate_chunks(const VolView &v) {
 // chunks of len_t / ct slices, len_t = the tile's interval length in the last
 // integrate (frames are temporally coherent); surplus items (c >= ct) go last.
 // A counting sort into descending length buckets by one block; any
-// permutation integrates the same volume.
+// permutation integrates the same volume (the bucket is only a priority, so
+// it may use any deterministic arithmetic: the capped chunk count is counted
+// with compares, the chunk length is a float quotient).  Items of the empty
+// bucket (most of them) take their slots with one LDS atomic per wave.
 constexpr int kOrderBuckets = 1024;
 __global__ __launch_bounds__(1024) void k_int_order(const unsigned *__restrict__ work, unsigned *__restrict__ perm,
                                                     int tiles, int nchunk, int zn, int capped, int chunkr) {
   __shared__ unsigned hist[kOrderBuckets];
   __shared__ unsigned wsum[16];
-  const int t = threadIdx.x;
+  const int t = threadIdx.x, lane = t & 63;
   hist[t] = 0u;
   __syncthreads();
   const int n = tiles * nchunk;
   const float scale = (float)(kOrderBuckets - 2) / ((float)zn + 2.f);
   auto bucket = [&](int item) {
-    const unsigned len = work[item % tiles];
-    const int c = item / tiles;
+    const int tile = item % tiles, c = item / tiles;
+    const unsigned len = work[tile];
     if (len == 0u) return kOrderBuckets - 1;
     int clen;
     if (capped) {
-      const int ct = min(nchunk, max(1, (int)(((long long)len * nchunk + zn - 1) / zn)));
+      // ct = min(nchunk, ceil(len * nchunk / zn)) = #{k < nchunk : k zn < len nchunk}
+      const unsigned a = len * (unsigned)nchunk;
+      int ct = 0;
+      for (int k = 0; k < nchunk; ++k) ct += (unsigned)k * (unsigned)zn < a ? 1 : 0;
       if (c >= ct) return kOrderBuckets - 1;
-      clen = (int)len / ct;
+      clen = (int)((float)len / (float)ct);
     } else {  // the chunk's length under the split k_integrate uses (geometric / equal)
       VolView q{};
       q.iadapt = 0;
@@ -3798,7 +3804,15 @@ __global__ __launch_bounds__(1024) void k_int_order(const unsigned *__restrict__
     }
     return kOrderBuckets - 2 - min(kOrderBuckets - 2, (int)((float)max(clen, 0) * scale));
   };
-  for (int i = t; i < n; i += 1024) atomicAdd(&hist[bucket(i)], 1u);
+  // (n is a multiple of nothing in particular: the loop runs whole waves, the
+  // lanes past n take no bucket)
+  const int nw = (n + 1023) & ~1023;
+  for (int i = t; i < nw; i += 1024) {
+    const int b = i < n ? bucket(i) : -1;
+    const unsigned long long empty = __ballot(b == kOrderBuckets - 1);
+    if (b >= 0 && b != kOrderBuckets - 1) atomicAdd(&hist[b], 1u);
+    if (lane == 0 && empty) atomicAdd(&hist[kOrderBuckets - 1], (unsigned)__popcll(empty));
+  }
   __syncthreads();
   // exclusive scan of the 1024 bucket counts: waves, then wave totals
   const unsigned c = hist[t];
@@ -3814,12 +3828,22 @@ __global__ __launch_bounds__(1024) void k_int_order(const unsigned *__restrict__
   __syncthreads();
   hist[t] = base + incl - c;
   __syncthreads();
-  for (int i = t; i < n; i += 1024) perm[atomicAdd(&hist[bucket(i)], 1u)] = (unsigned)i;
+  for (int i = t; i < nw; i += 1024) {
+    const int b = i < n ? bucket(i) : -1;
+    const unsigned long long empty = __ballot(b == kOrderBuckets - 1);
+    unsigned e0 = 0u;
+    if (lane == 0 && empty) e0 = atomicAdd(&hist[kOrderBuckets - 1], (unsigned)__popcll(empty));
+    e0 = __shfl(e0, 0);
+    if (b == kOrderBuckets - 1)
+      perm[e0 + (unsigned)__popcll(empty & ((1ull << lane) - 1ull))] = (unsigned)i;
+    else if (b >= 0)
+      perm[atomicAdd(&hist[b], 1u)] = (unsigned)i;
+  }
 }
 
 void launch_integrate(hipStream_t s, VolView v, LevelGeom g0, const float2 *dl0, const float *dmap,
                       const float *invl, const uint8_t *bgr, DevState *st, DevPose *log, DevPose vpose,
-                      const float *xpose, unsigned long long *counters) {
+                      const float *xpose, unsigned long long *counters, bool order) {
   const int tiles = v.tiles_x * v.tiles_y;
   const int nchunk = integrate_chunks(v);
   v.inchunk = nchunk;
@@ -3849,9 +3873,15 @@ void launch_integrate(hipStream_t s, VolView v, LevelGeom g0, const float2 *dl0,
   else if (idx32) KFX_LAUNCH_INT(false, true);
   else KFX_LAUNCH_INT(false, false);
 #undef KFX_LAUNCH_INT
-  if (!counters && v.iwork && v.iperm)
-    hipLaunchKernelGGL(k_int_order, dim3(1), dim3(1024), 0, s, v.iwork, v.iperm, tiles, nchunk, v.zn, v.iadapt,
-                       KFX_INT_CHUNKR);
+  if (!counters && order) launch_int_order(s, v);
+}
+
+void launch_int_order(hipStream_t s, VolView v) {
+  const int tiles = v.tiles_x * v.tiles_y;
+  const int nchunk = integrate_chunks(v);
+  if (!integrate_mode(v) || !v.iwork || !v.iperm) return;
+  hipLaunchKernelGGL(k_int_order, dim3(1), dim3(1024), 0, s, v.iwork, v.iperm, tiles, nchunk, v.zn, integrate_mode(v),
+                     KFX_INT_CHUNKR);
 }
 
 #ifdef KFX_RAY_TRACE
