@@ -436,8 +436,13 @@ def test_pipeline_modes_and_inputs_identical(seq_qvga):
     res = []
     for mode in ("graph", "eager", "profile", "u16", "staged", "staged_eager", "staged_full",
                  "staged_graph", "staged_mixed", "staged_per_iter", "icp_per_iter", "icp_coop",
-                 "staged_coop"):
-        kf, p = make(intr, dims=64)
+                 "staged_coop", "staged_events", "staged_mixed_back", "async"):
+        if mode == "staged_events":  # overlapped frames ordered by events, not the raycast start signal
+            os.environ["KFX_STREAM_SIGNAL"] = "0"
+        try:
+            kf, p = make(intr, dims=64)
+        finally:
+            os.environ.pop("KFX_STREAM_SIGNAL", None)
         if mode == "staged_graph":  # staged frames without the two-stream overlap
             kf.set_frame_overlap(False)
         if mode in ("eager", "staged_eager"):  # staged_eager: overlapped frames launched eagerly
@@ -454,7 +459,7 @@ def test_pipeline_modes_and_inputs_identical(seq_qvga):
         if mode == "profile":
             kf.set_profiling(True)
         if mode in ("staged", "staged_eager", "staged_full", "staged_graph", "staged_per_iter",
-                    "staged_coop"):
+                    "staged_coop", "staged_events"):
             kf.stage_frames(bgr, dep.astype(np.float32))
             for k in range(len(dep)):
                 kf.pipeline_staged(k)
@@ -466,6 +471,19 @@ def test_pipeline_modes_and_inputs_identical(seq_qvga):
                 kf.pipeline_staged(k)
             for k in range(half, len(dep)):
                 kf.pipeline(bgr[k], dep[k].astype(np.float32))
+        elif mode == "staged_mixed_back":  # overlapped, single-stream, overlapped again
+            kf.stage_frames(bgr, dep.astype(np.float32))
+            for k in range(3):
+                kf.pipeline_staged(k)
+            for k in range(3, 6):
+                kf.pipeline(bgr[k], dep[k].astype(np.float32))
+            for k in range(6, len(dep)):
+                kf.pipeline_staged(k)
+            kf.synchronize()
+        elif mode == "async":  # pipelined host input through the pinned ring
+            for k in range(len(dep)):
+                kf.pipeline_async(bgr[k], dep[k].astype(np.float32))
+            kf.synchronize()
         else:
             _run_pipeline(kf, bgr, dep, u16=(mode == "u16"))
         if mode == "profile":
