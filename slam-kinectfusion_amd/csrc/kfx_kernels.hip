@@ -76,10 +76,14 @@
 #define KFX_FF_MIN_SLAB 128
 #endif
 #ifndef KFX_INT_SLAB_CAPW
-#define KFX_INT_SLAB_CAPW 4  // integrate, Z-slab contexts: at most this many times KFX_INT_WAVES waves
+#define KFX_INT_SLAB_CAPW 49152  // integrate, Z-slab contexts: at most this many waves
 #endif
 #ifndef KFX_INT_WAVES
-#define KFX_INT_WAVES 12288  // integrate: target wave count (z-chunks per column tile; C2: 3 chunks of 4096 tiles)
+// integrate: target wave count (z-chunks per column tile; C2: 4 chunks of 4096
+// tiles — 3 while the next frame's preprocess shared the GPU with integrate;
+// with it beside the raycast, 4 measured -1.1 % frame time in 6 of 6
+// alternating pairs, 2 and 5 slower or neutral: profiles/r06_int_chunks_ab.txt)
+#define KFX_INT_WAVES 16384
 #endif
 
 namespace kfx {
@@ -3749,18 +3753,18 @@ static int integrate_mode(const VolView &v) {
 int integrate_chunks(const VolView &v) {
   const int tiles = v.tiles_x * v.tiles_y;
   if (integrate_mode(v) == 1) return std::max(1, std::min(KFX_INT_NC, v.zn / 32));  // chunks of >= 32 slices
-  // z-chunks so that >= KFX_INT_WAVES waves exist (12 per SIMD on 1024 SIMDs)
+  // z-chunks so that >= KFX_INT_WAVES waves exist (16 per SIMD on 1024 SIMDs)
   int nc = (KFX_INT_WAVES + tiles - 1) / tiles;
   // Z-slabs (a context storing part of the volume's slices): also at most
   // ~KFX_INT_SLAB_CHUNK slices per chunk.  A slab's waves otherwise cover its
   // whole stored range (C4 slab 0: 344 slices, one chunk per tile: 6150
   // working waves, 70 % of the wave slots filled at the start and a tail of
   // 120-260 us waves, tools/slab_int_trace.py)
-  // — as long as the slab keeps <= 4 KFX_INT_WAVES waves (the chunk-start
+  // — as long as the slab keeps <= KFX_INT_SLAB_CAPW waves (the chunk-start
   // replays of many chunks cost more than the tail they cut: C5 slab 0, 772
   // slices of 65536 tiles, took 1.25 ms in 7 chunks against 0.85 ms in one)
   if (KFX_INT_SLAB_CHUNK > 0 && v.zn < v.Z)
-    nc = std::max(nc, std::min((v.zn + KFX_INT_SLAB_CHUNK - 1) / KFX_INT_SLAB_CHUNK, KFX_INT_SLAB_CAPW * KFX_INT_WAVES / tiles));
+    nc = std::max(nc, std::min((v.zn + KFX_INT_SLAB_CHUNK - 1) / KFX_INT_SLAB_CHUNK, KFX_INT_SLAB_CAPW / tiles));
   return std::max(1, std::min(KFX_INT_MAXCHUNK, nc));
 }
 
