@@ -1200,6 +1200,14 @@ static int create_impl(const kfx_intrinsics *intr, const kfx_params *params, int
   for (int b = 0; b < 2; ++b) c->planb[b].vpose = to_dev(c->p.volu_pose);
   // (both sets: the fit may cap nblocks and select the strided kernel)
   c->icp_persistent = icp_persistent_ok(c->planb[0], c->device) && icp_persistent_ok(c->planb[1], c->device);
+  // The side streams' waits on the raycast start signal run as small spinning
+  // kernels, which may be resident while the next frame's persistent ICP
+  // starts: keep the signal only when the ICP grid leaves two CUs of headroom
+  // (a 720p frame's strided plan fills the GPU: its grid was then not
+  // co-resident and the watchdog fired), else the event path
+  if (c->start_sig && c->icp_persistent &&
+      !(icp_headroom(c->planb[0], c->device, 2) && icp_headroom(c->planb[1], c->device, 2)))
+    c->start_sig = nullptr;  // (the word stays in allocs)
   set_par(c, 0);
   if ((r = dalloc(c, (void **)&c->counters, sizeof(unsigned long long) * 128))) return fail(r);
   if ((r = dalloc(c, (void **)&c->xpose, sizeof(float) * 32))) return fail(r);

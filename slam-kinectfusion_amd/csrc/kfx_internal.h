@@ -230,6 +230,9 @@ int icp_blocks(const LevelGeom &g);
 IcpPlan make_icp_plan(int levels, const LevelGeom *g, const int *iters, FrameView cur,
                       FrameView prev, float dist_thr, float angle_thr);
 bool icp_persistent_ok(IcpPlan &pl, int device);  // grid co-resident + slots fit
+// the persistent ICP grid stays co-resident with `cus_free` CUs' worth of
+// blocks taken by other kernels (icp_persistent_ok's plan)
+bool icp_headroom(const IcpPlan &pl, int device, int cus_free);
 // begin: run the frame's frame_begin inside the launch (no separate kernel)
 // coop: cooperative launch (the runtime guarantees the grid co-resident)
 // Returns the launch error (a refused cooperative launch: the caller falls

@@ -3641,6 +3641,15 @@ IcpPlan make_icp_plan(int levels, const LevelGeom *g, const int *iters, FrameVie
   return pl;
 }
 
+bool icp_headroom(const IcpPlan &pl, int device, int cus_free) {
+  int per_cu = 0, cus = 0;
+  const hipError_t e = pl.stride ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_icp_track<true>, kIcpThreads, 0)
+                                 : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_icp_track<false>, kIcpThreads, 0);
+  if (e != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
+    return false;
+  return (long long)per_cu * (cus - cus_free) >= pl.nblocks;
+}
+
 bool icp_persistent_ok(IcpPlan &pl, int device) {
   if (pl.slots > kIcpMaxSlots) return false;
   int per_cu = 0, cus = 0;
